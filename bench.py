@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Headline benchmark: directed-edge flow updates/s + % HBM roofline; rounds to 1e-9 error.
+
+Workload (BASELINE.json configs[1]): Erdos-Renyi G(n=1,000,000, m=4,000,000), self-loops
+dropped, deduplicated, symmetrised (E ~ 8.0e6 directed edges); node values U[0,100)
+(SplitMix64, seed 0); collect-all generation-synchronous rounds in fp64 on one MI355X.
+A "step" = one round = Peer.on_receive for every directed edge + Peer.avg_and_send for
+every node (flowupdating-collectall.py:93-128) = one launch of the round kernel.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+
+At N > 1 (torch.distributed.run, one process per GPU) every rank runs its own ER-1M
+instance (graph seed 1 + rank), the weak-scaling "independent graphs" mode: the ER graph
+has no locality, so partitioning it would put ~7/8 of its edges on the halo.
+Ranks synchronise with a barrier around the timed region; time = max over ranks; value =
+edge updates of all ranks / that time. torch.distributed (gloo, CPU) is used only for the
+barrier and the max; the hot path is libfu.so.
+
+Printed by rank 0: ONE JSON line (contract in the task statement), with `roofline` (the
+round kernel's algorithmic bytes 24E + 28N per launch / average launch time from HIP
+events on the library's stream, against 8 TB/s) and `cpu_baseline` (the C port of the
+oracle on the host, single thread, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "simgrid-flow-updating-implementation_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=1000, help="timed rounds")
+    ap.add_argument("--warmup", type=int, default=20, help="untimed rounds first")
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--m", type=int, default=4_000_000)
+    ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--conv-rounds", type=int, default=1000,
+                    help="rounds of the (untimed) convergence run for rounds-to-1e-9")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0,
+                    help="target length of the CPU baseline sample (0 = skip)")
+    ap.add_argument("--no-conv", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+
+    import fu
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    def allmax(x: float) -> float:
+        if dist is None:
+            return x
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    t_gen = time.perf_counter()
+    g = fu.Graph.erdos_renyi(args.n, args.m, seed=1 + rank)
+    v = fu.uniform_values(g.n, seed=0)
+    t_gen = time.perf_counter() - t_gen
+    eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
+    eng.run(args.warmup)
+    eng.synchronize()
+
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    kern_ms = eng.run_timed(args.steps)  # HIP events on the engine's own stream
+    eng.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    wall = allmax(t1 - t0)
+    kern_ms = allmax(kern_ms)
+
+    edges_total = g.E * world
+    value = edges_total * args.steps / wall
+    ms_per_step = wall * 1e3 / args.steps
+    # roofline of the round kernel (one launch per round)
+    alg_bytes = 24 * g.E + 28 * g.n
+    avg_launch_s = kern_ms / 1e3 / args.steps
+    achieved = alg_bytes / avg_launch_s / 1e9
+
+    # rounds to 1e-9 vs the per-component means (untimed)
+    rounds_to = None
+    final_err = None
+    if not args.no_conv:
+        tgt, comp = fu.component_means(g.rowptr, g.col, v)
+        eng.reset()
+        eng.set_targets(tgt)
+        tr = eng.run(args.conv_rounds, err_every=1)
+        below = np.nonzero(tr < 1e-9)[0]
+        rounds_to = int(below[0]) + 1 if len(below) else None
+        final_err = float(tr[-1])
+        n_comp = int(comp.max()) + 1
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if world == 1 and args.cpu_seconds > 0:
+            cpu = cpu_baseline(g, v, args.cpu_seconds)
+        traffic = None
+        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc_path):
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            if pmc.get("n") == g.n and pmc.get("E") == g.E and pmc.get("kernel") == args.kernel:
+                traffic = pmc.get("bytes_per_launch")
+        out = {
+            "metric": "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error",
+            "value": value,
+            "unit": "edge-updates/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded ER graph, U[0,100) values)",
+            "config": {
+                "workload": "er:n=1000000,m=4000000 collect-all generation-synchronous rounds",
+                "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
+                "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel,
+                "parallelism": "independent graph per GPU" if world > 1 else "single GPU",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_us": avg_launch_s * 1e6,
+            },
+            "cpu_baseline": cpu,
+            "rounds_to_1e-9": rounds_to,
+            "err_after_conv_rounds": final_err,
+            "conv_rounds": args.conv_rounds,
+            "components": None if args.no_conv else n_comp,
+            "graph_gen_s": t_gen,
+        }
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(g, v, seconds):
+    """C port of the oracle (oracle/fu_oracle.c) on the host, 1 thread, bounded sample:
+    the same ER-1M graph and values, steady-state rounds, about `seconds` of CPU work."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import coracle
+
+    a, f = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 1, nthreads=1)  # round 0
+    t = time.perf_counter()
+    coracle.ca_rounds(g.rowptr, g.col, g.rev, v, 2, a, f, nthreads=1)
+    per = (time.perf_counter() - t) / 2
+    rounds = max(2, int(seconds / max(per, 1e-6)))
+    t = time.perf_counter()
+    coracle.ca_rounds(g.rowptr, g.col, g.rev, v, rounds, a, f, nthreads=1)
+    dt = time.perf_counter() - t
+    return {
+        "value": g.E * rounds / dt,
+        "unit": "edge-updates/s",
+        "cores": 1,
+        "cores_available": os.cpu_count(),
+        "kind": "port",
+        "sample": f"{rounds} steady-state collect-all rounds on the same ER-1M graph "
+                  f"({dt:.1f} s, oracle/fu_oracle.c, gcc -O2, single thread like SimGrid's DES)",
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,200 @@
+/* fu.h — C ABI of libfu.so, the MI355X-native Flow Updating engine.
+ *
+ * Drop-in boundary. The reference (AvilaAndre/simgrid-flow-updating-implementation) has no
+ * library API. Its "operator API" is the SimGrid actor contract of
+ * flowupdating-collectall.py (CA) and flowupdating-pairwise.py (PW):
+ *   e.load_platform(...)            CA:154 / PW:143
+ *   e.register_actor("peer", Peer)  CA:156 / PW:145
+ *   e.load_deployment(...)          CA:157 / PW:146
+ *   e.run_until(10000)              CA:164 / PW:153
+ *   the watcher + global_values     CA:131-148 / PW:120-137
+ * Every `peer` actor and the SimGrid engine behind it are replaced by the entry points
+ * below. Host-side Python (the `fu` package) binds them with ctypes, mirroring the
+ * Engine/Peer surface. The integration stub is in INTEGRATION.md.
+ *
+ * Conventions: every function returns int status, 0 = FU_OK and < 0 = error;
+ * fu_last_error() returns a thread-local message. All pointers are plain host pointers
+ * owned by the caller unless stated. fp64 everywhere (Python float). Indices are int32
+ * (n < 2^31, E < 2^31). Each handle owns one HIP stream. Calls on one handle are
+ * stream-ordered and not reentrant.
+ */
+#ifndef FU_H_
+#define FU_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FU_OK 0
+#define FU_ERR_ARG (-1)
+#define FU_ERR_HIP (-2)
+#define FU_ERR_ALLOC (-3)
+#define FU_ERR_STATE (-4)
+#define FU_ERR_GRAPH (-5)
+#define FU_ERR_NCCL (-6)
+
+/* Thread-local message for the last failing call on this thread. */
+const char *fu_last_error(void);
+/* ABI version (bumped when a signature changes). */
+int fu_version(void);
+/* Number of visible HIP devices (0 without a GPU; never an error on a CPU-only host). */
+int fu_device_count(int32_t *out);
+
+/* ======================================================================================
+ * Host graphs (native C++; no GPU needed)
+ * Replaces the deployment parsing SimGrid does for `peer` actors: neighbour lists from
+ * actors.xml (ACT:4-27) parsed by Peer.__init__ (CA:29-31, CA:38-40). CSR rows keep the
+ * caller's neighbour order, because that order fixes the summation order (CA:106, 110).
+ * Generators provide the synthetic BASELINE configs. All are seeded and deterministic
+ * (SplitMix64 counter streams, independent of thread count).
+ * ==================================================================================== */
+typedef struct fu_graph fu_graph;
+
+/* Undirected edge list -> symmetric CSR: drop self-loops, dedup, rows sorted by id. */
+int fu_graph_from_edges(int32_t n, int64_t m, const int32_t *src, const int32_t *dst,
+                        fu_graph **out);
+/* CSR as given (row order kept). If require_symmetric, fails unless every i->j has j->i. */
+int fu_graph_from_csr(int32_t n, const int64_t *rowptr, const int32_t *col,
+                      int32_t require_symmetric, fu_graph **out);
+/* Erdos-Renyi G(n, m): m uniform pairs, self-loops dropped, deduplicated, symmetrised. */
+int fu_graph_gen_er(int32_t n, int64_t m, uint64_t seed, fu_graph **out);
+/* Random d-regular graph (pairing model + edge switches). n*d must be even. */
+int fu_graph_gen_rr(int32_t n, int32_t d, uint64_t seed, fu_graph **out);
+/* R-MAT (scale, edge factor, a, b, c; d = 1-a-b-c), symmetrised and deduplicated. */
+int fu_graph_gen_rmat(int32_t scale, int32_t edge_factor, double a, double b, double c,
+                      uint64_t seed, fu_graph **out);
+/* Random geometric graph: n points in the unit square, edge iff distance < radius.
+ * Nodes are numbered in cell (x-major) order, which gives locality. */
+int fu_graph_gen_rgg(int32_t n, double radius, uint64_t seed, fu_graph **out);
+/* n, directed edge count, max degree, 1 if symmetric. */
+int fu_graph_info(const fu_graph *g, int32_t *n, int64_t *e, int32_t *max_deg,
+                  int32_t *symmetric);
+/* Copy out; any output may be NULL. rev[e] = index of the reverse edge (symmetric only). */
+int fu_graph_export(const fu_graph *g, int64_t *rowptr, int32_t *col, int32_t *rev);
+int fu_graph_free(fu_graph *g);
+/* value[i] = lo + (hi - lo) * U_i, U_i = (splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) >> 11) * 2^-53 */
+int fu_values_uniform(int64_t n, uint64_t seed, double lo, double hi, double *out);
+
+/* ======================================================================================
+ * Synchronous collect-all engine — THE HOT PATH.
+ * One call to fu_run_collectall(h, R, ...) = R generation-synchronous rounds. Each round
+ * is Peer.on_receive (CA:93-103) for every directed edge, then Peer.avg_and_send
+ * (CA:105-128) for every node, as one data-parallel pass in HBM.
+ * Round 0 = the timeout fire on zero state (CA:33-34, CA:87-91). The graph must be
+ * symmetric (rev index). Results are bitwise equal to the reference's Python floats.
+ * ==================================================================================== */
+typedef struct fu_handle fu_handle;
+
+/* rowptr[n+1], col[e], rev[e] (rev may be NULL: computed natively), value[n]. */
+int fu_create(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
+              const int32_t *rev, const double *value, int32_t device, fu_handle **out);
+int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
+                         fu_handle **out);
+/* Options: "kernel" (0 = auto, 1 = thread-per-node, 2 = wave-tile LDS, 3 = push/inbox),
+ * "hub_threshold" (degree above which a node gets a wave; default 64). */
+int fu_set_option(fu_handle *h, const char *key, int64_t value);
+/* Zero the state: the next round run is round 0. */
+int fu_reset(fu_handle *h);
+/* Per-node convergence targets (e.g. exact component means) for the error check. */
+int fu_set_targets(fu_handle *h, const double *target);
+/* Run `rounds` rounds. If err_every > 0 (targets required), err_trace receives
+ * max_i |a_i - target_i| after every err_every-th round (rounds / err_every entries).
+ * Asynchronous unless err_trace != NULL. */
+int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *err_trace);
+/* Same, timed with HIP events on the handle's stream: *ms = elapsed device time of the
+ * whole region (synchronises). */
+int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms);
+/* max_i |a_i - target_i| on the current estimates (synchronises). */
+int fu_max_err(fu_handle *h, double *out);
+/* Per-node estimate = last_avg (CA:114, CA:56-63). */
+int fu_get_estimates(fu_handle *h, double *a_out);
+/* Per-directed-edge flow f[e] = flows[col[e]] of node i (CA:117-118), CSR order. */
+int fu_get_flows(fu_handle *h, double *f_out);
+int fu_get_round(fu_handle *h, int64_t *rounds_done);
+int fu_synchronize(fu_handle *h);
+int fu_destroy(fu_handle *h);
+
+/* ======================================================================================
+ * Tick-level replay (pairwise mode, and faithful collect-all on small platforms).
+ * Replaces the SimGrid maestro + Peer.loop (CA:70-85 / PW:69-84): the loop's control flow
+ * never depends on fp values, so the whole schedule is precomputed on the host as a trace.
+ * The GPU then replays one tick per batch. Events of one tick are on distinct nodes and
+ * touch only their own row and message slots, so they commute. Mailbox model: SURVEY.md
+ * App. B.
+ * ==================================================================================== */
+#define FU_MODE_COLLECTALL 0
+#define FU_MODE_PAIRWISE 1
+
+#define FU_EV_RECV 0    /* {0, slot, msg_in, 0}     est[slot]=msg.a; flow[slot]=-msg.f (CA:98-99, PW:98-99) */
+#define FU_EV_FIRE_CA 1 /* {1, k, out_off, 0}       avg over slots [0,k), k msgs to out_ids[out_off..] (CA:105-125) */
+#define FU_EV_FIRE_PW 2 /* {2, slot, k, msg_out}    pairwise avg with slot; flows summed over [0,k) (PW:102-117) */
+
+typedef struct fu_trace fu_trace;
+
+/* Declared neighbour lists (ACT:4-27) in CSR: decl_rowptr[n+1], decl_col. ticks = number
+ * of ticks simulated (t = 0 .. ticks-1). order: "fwd" | "rev" | "rand:<seed>" (intra-tick
+ * actor order; SimGrid's real tie order is not observable offline). */
+int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                   int32_t mode, int32_t ticks, const char *order, fu_trace **out);
+/* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
+ * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */
+int fu_trace_info(const fu_trace *t, int64_t info[8]);
+/* union_rowptr[n+1] / union_col: neighbour slots in insertion order (declared, then first
+ * arrival). tick_task_off[ticks+1]; tasks[3*n_tasks] = (node, ev_begin, ev_end);
+ * events[4*n_events]; out_ids[n_out_ids]; first_avg_seq[n] (order of first average:
+ * key order of global_values["last_avg"], -1 = never averaged); fires[n]. Any may be NULL. */
+int fu_trace_export(const fu_trace *t, int64_t *union_rowptr, int32_t *union_col,
+                    int64_t *tick_task_off, int32_t *tasks, int32_t *events,
+                    int32_t *out_ids, int64_t *first_avg_seq, int32_t *fires);
+int fu_trace_free(fu_trace *t);
+
+typedef struct fu_replay fu_replay;
+/* Raw-array form (the trace arrays above, caller-owned). */
+int fu_replay_create(int32_t n, const int64_t *rowptr, const double *value, int32_t ticks,
+                     const int64_t *tick_task_off, int64_t n_tasks, const int32_t *tasks,
+                     int64_t n_events, const int32_t *events, int64_t n_out_ids,
+                     const int32_t *out_ids, int64_t n_msgs, int32_t device,
+                     fu_replay **out);
+int fu_replay_create_from_trace(const fu_trace *t, const double *value, int32_t device,
+                                fu_replay **out);
+/* Run ticks [current, tick_end). snaps[k*n .. ] receives last_avg after tick
+ * snap_ticks[k] (ascending, within the range); snaps may be NULL if n_snap == 0. */
+int fu_replay_run(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
+                  double *snaps);
+/* Timed variant: *ms = device time of the tick kernels (synchronises). */
+int fu_replay_run_timed(fu_replay *r, int32_t tick_end, float *ms);
+int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est);
+int fu_replay_destroy(fu_replay *r);
+
+/* ======================================================================================
+ * Multi-GPU (one process per GPU, RCCL over xGMI). The graph is partitioned into
+ * contiguous node ranges. Each rank holds its rows plus ghost slots for the reverse flows
+ * and estimates of cut edges. One halo exchange per round (ncclSend/ncclRecv to each
+ * neighbouring part in one group) replaces the simulated mailboxes (CA:74, CA:124).
+ * ==================================================================================== */
+#define FU_UNIQUE_ID_BYTES 128
+int fu_dist_unique_id(uint8_t *id_out /* FU_UNIQUE_ID_BYTES */);
+/* Local part, in local numbering:
+ *   n_local rows (global ids [row_begin, row_begin + n_local)), rowptr[n_local+1];
+ *   col[e]: < n_local = local node, >= n_local = ghost estimate slot (n_local + g);
+ *   rev[e]: < e_local = local edge, >= e_local = ghost flow slot (e_local + q).
+ * Halo plan (per peer rank, CSR over peers):
+ *   send_f_off[nranks+1] / send_f_idx: local edges whose flow goes to each peer, in the
+ *     order that peer stores them in its ghost flow slots;
+ *   recv_f_off[nranks+1]: ghost flow slots per peer (contiguous, peer order);
+ *   send_a_off / send_a_idx, recv_a_off: the same for estimates of boundary nodes. */
+int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
+                   const int32_t *col, const int32_t *rev, const double *value,
+                   int32_t n_ghost_a, int64_t n_ghost_f, int32_t nranks, int32_t rank,
+                   const int64_t *send_f_off, const int32_t *send_f_idx,
+                   const int64_t *recv_f_off, const int64_t *send_a_off,
+                   const int32_t *send_a_idx, const int64_t *recv_a_off,
+                   const uint8_t *unique_id, int32_t device, fu_handle **out);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FU_H_ */

@@ -1,0 +1,967 @@
+// libfu device engine for MI355X (gfx950): collect-all round kernels, tick replay kernels,
+// convergence check, handle management. C ABI declared in include/fu.h.
+//
+// Arithmetic spec (bitwise parity with the reference's Python floats):
+//   receive  (flowupdating-collectall.py:98-99):  fr[e] = -f_old[rev e], er[e] = a_old[col e]
+//   fire     (CA:106-119):  S = 0.0 + fr[e0] + fr[e1] + ...  (left to right, row order)
+//                           T = 0.0 + er[e0] + er[e1] + ...
+//                           a = ((v - S) + T) / (deg + 1)
+//                           f_new[e] = (fr[e] + a) - er[e]
+// Compiled with -ffp-contract=off and without fast-math. There are no multiplies to
+// contract, and `/` is the correctly rounded IEEE fp64 division. Every sum is a sequential
+// dependency chain in row order, including for hubs (see k_round_tile's heavy path).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "fu_common.h"
+
+using namespace fu;
+
+#define HIP_TRY(expr)                                                                     \
+  do {                                                                                    \
+    hipError_t _e = (expr);                                                               \
+    if (_e != hipSuccess)                                                                 \
+      return fu::fail(FU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e));     \
+  } while (0)
+
+namespace {
+
+constexpr int kBlock = 256;      // threads per block (4 waves of 64)
+constexpr int kTileEdges = 2048;  // max edges staged in LDS per light tile
+constexpr int kTileNodes = kBlock;
+
+// ------------------------------------------------------------------------------------
+// error reduction: max over |a - target| as uint64 bit patterns (non-negative doubles
+// order like their bits; a NaN (sign cleared) is larger than +inf, so NaN propagates)
+// ------------------------------------------------------------------------------------
+__device__ inline unsigned long long err_bits(double a, double t) {
+  return (unsigned long long)__double_as_longlong(fabs(a - t));
+}
+
+__device__ inline void block_max_to(unsigned long long x, unsigned long long *dst) {
+  for (int off = 32; off > 0; off >>= 1) {
+    unsigned long long y = __shfl_xor(x, off, 64);
+    x = x > y ? x : y;
+  }
+  __shared__ unsigned long long s_w[kBlock / 64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) s_w[w] = x;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned long long m = s_w[0];
+    for (int k = 1; k < kBlock / 64; ++k) m = m > s_w[k] ? m : s_w[k];
+    if (m) atomicMax(dst, m);
+  }
+}
+
+// ------------------------------------------------------------------------------------
+// Round 0: the timeout fire on zero state (CA:33-34, CA:87-91 -> CA:105-128)
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict__ rowptr,
+                                                   const double *__restrict__ v,
+                                                   double *__restrict__ f,
+                                                   double *__restrict__ a) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  int b = rowptr[i], e = rowptr[i + 1];
+  double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
+  a[i] = ai;
+  double fv = (0.0 + ai) - 0.0;
+  for (int k = b; k < e; ++k) f[k] = fv;
+}
+
+// ------------------------------------------------------------------------------------
+// Variant 1: one thread per node, gathers straight from global memory
+// ------------------------------------------------------------------------------------
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void k_round_tpn(
+    int n, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const int *__restrict__ rev, const double *__restrict__ v,
+    const double *__restrict__ f_old, const double *__restrict__ a_old,
+    double *__restrict__ f_new, double *__restrict__ a_new,
+    const double *__restrict__ target, unsigned long long *__restrict__ err) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  unsigned long long eb = 0;
+  if (i < n) {
+    int b = rowptr[i], e = rowptr[i + 1];
+    double S = 0.0, T = 0.0;
+    for (int k = b; k < e; ++k) {
+      S = S + (-f_old[rev[k]]);
+      T = T + a_old[col[k]];
+    }
+    double a = ((v[i] - S) + T) / (double)(e - b + 1);
+    a_new[i] = a;
+    for (int k = b; k < e; ++k) f_new[k] = ((-f_old[rev[k]]) + a) - a_old[col[k]];
+    if (CHECK) eb = err_bits(a, target[i]);
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
+// ------------------------------------------------------------------------------------
+// Variant 2: LDS tiles. A light tile = a contiguous node range with <= kTileNodes nodes
+// and <= kTileEdges edges. Its edges are gathered edge-parallel into LDS (coalesced
+// col/rev, independent gathers), then each node sums its row sequentially from LDS, and
+// the new flows are written edge-parallel (coalesced). A heavy tile = one node with more
+// than hub_threshold edges. The whole block gathers it in chunks, and wave 0 keeps the
+// exact left-to-right sum in a lane-uniform dependency chain (bitwise parity for hubs).
+// tiles[t] = {node_begin, node_end}; node_end < 0 marks a heavy tile (node = begin).
+// ------------------------------------------------------------------------------------
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void k_round_tile(
+    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int *__restrict__ col, const int *__restrict__ rev, const double *__restrict__ v,
+    const double *__restrict__ f_old, const double *__restrict__ a_old,
+    double *__restrict__ f_new, double *__restrict__ a_new,
+    const double *__restrict__ target, unsigned long long *__restrict__ err) {
+  __shared__ double s_fr[kTileEdges];
+  __shared__ double s_er[kTileEdges];
+  __shared__ unsigned char s_own[kTileEdges];
+  __shared__ int s_rp[kTileNodes + 1];
+  __shared__ double s_a[kTileNodes];
+  const int t = threadIdx.x;
+  const int2 tl = tiles[blockIdx.x];
+  unsigned long long eb = 0;
+
+  if (tl.y < 0) {
+    // ---------------- heavy node: block-chunked gather, wave-0 sequential chain ----------
+    const int i = tl.x;
+    const int b = rowptr[i], e = rowptr[i + 1];
+    double S = 0.0, T = 0.0;
+    for (int c0 = b; c0 < e; c0 += kTileEdges) {
+      const int cn = min(kTileEdges, e - c0);
+      for (int q = t; q < cn; q += kBlock) {
+        s_fr[q] = -f_old[rev[c0 + q]];
+        s_er[q] = a_old[col[c0 + q]];
+      }
+      __syncthreads();
+      if (t < 64) {
+        for (int q = 0; q < cn; ++q) {  // lane-uniform LDS broadcast reads
+          S = S + s_fr[q];
+          T = T + s_er[q];
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      double a = ((v[i] - S) + T) / (double)(e - b + 1);
+      s_a[0] = a;
+      a_new[i] = a;
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = s_a[0];
+    for (int k = b + t; k < e; k += kBlock) f_new[k] = ((-f_old[rev[k]]) + a) - a_old[col[k]];
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+
+  // ---------------- light tile ----------------
+  const int nb = tl.x, nn = tl.y - tl.x;
+  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
+  __syncthreads();
+  const int e0 = s_rp[0];
+  const int ne = s_rp[nn] - e0;
+#pragma unroll 4
+  for (int q = t; q < ne; q += kBlock) {
+    const int k = e0 + q;
+    s_fr[q] = -f_old[rev[k]];
+    s_er[q] = a_old[col[k]];
+  }
+  if (t < nn) {
+    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
+  }
+  __syncthreads();
+  if (t < nn) {
+    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      S = S + s_fr[q];
+      T = T + s_er[q];
+    }
+    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
+    s_a[t] = a;
+    a_new[nb + t] = a;
+    if (CHECK) eb = err_bits(a, target[nb + t]);
+  }
+  __syncthreads();
+  for (int q = t; q < ne; q += kBlock) f_new[e0 + q] = (s_fr[q] + s_a[s_own[q]]) - s_er[q];
+  if (CHECK) block_max_to(eb, err);
+}
+
+// ------------------------------------------------------------------------------------
+// Variant 3: push / inbox. Message (flow, estimate) from j to i lives at i's own row slot
+// for j (the FlowUpdatingMsg of CA:121, stored where its receiver reads it). A node reads
+// its inbox row contiguously and scatters its new messages to inbox_new[rev[e]]. No col
+// and no random reads; one random 16-byte store per directed edge.
+// ------------------------------------------------------------------------------------
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void k_round_push(
+    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int *__restrict__ rev, const double *__restrict__ v,
+    const double2 *__restrict__ in_old, double2 *__restrict__ in_new,
+    double *__restrict__ a_new, const double *__restrict__ target,
+    unsigned long long *__restrict__ err) {
+  __shared__ double2 s_m[kTileEdges];
+  __shared__ unsigned char s_own[kTileEdges];
+  __shared__ int s_rp[kTileNodes + 1];
+  __shared__ double s_a[kTileNodes];
+  const int t = threadIdx.x;
+  const int2 tl = tiles[blockIdx.x];
+  unsigned long long eb = 0;
+
+  if (tl.y < 0) {
+    const int i = tl.x;
+    const int b = rowptr[i], e = rowptr[i + 1];
+    double S = 0.0, T = 0.0;
+    for (int c0 = b; c0 < e; c0 += kTileEdges) {
+      const int cn = min(kTileEdges, e - c0);
+      for (int q = t; q < cn; q += kBlock) s_m[q] = in_old[c0 + q];
+      __syncthreads();
+      if (t < 64) {
+        for (int q = 0; q < cn; ++q) {
+          const double2 m = s_m[q];
+          S = S + (-m.x);
+          T = T + m.y;
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      double a = ((v[i] - S) + T) / (double)(e - b + 1);
+      s_a[0] = a;
+      a_new[i] = a;
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = s_a[0];
+    for (int k = b + t; k < e; k += kBlock) {
+      const double2 m = in_old[k];
+      in_new[rev[k]] = make_double2(((-m.x) + a) - m.y, a);
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+
+  const int nb = tl.x, nn = tl.y - tl.x;
+  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
+  __syncthreads();
+  const int e0 = s_rp[0];
+  const int ne = s_rp[nn] - e0;
+  for (int q = t; q < ne; q += kBlock) s_m[q] = in_old[e0 + q];
+  if (t < nn) {
+    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
+  }
+  __syncthreads();
+  if (t < nn) {
+    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double2 m = s_m[q];
+      S = S + (-m.x);
+      T = T + m.y;
+    }
+    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
+    s_a[t] = a;
+    a_new[nb + t] = a;
+    if (CHECK) eb = err_bits(a, target[nb + t]);
+  }
+  __syncthreads();
+  for (int q = t; q < ne; q += kBlock) {
+    const double2 m = s_m[q];
+    const double a = s_a[s_own[q]];
+    in_new[rev[e0 + q]] = make_double2(((-m.x) + a) - m.y, a);
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
+// round 0 for the push layout: message i->j = (a_i, a_i) stored at inbox[rev[e]]
+__global__ __launch_bounds__(kBlock) void k_round0_push(int n, const int *__restrict__ rowptr,
+                                                        const int *__restrict__ rev,
+                                                        const double *__restrict__ v,
+                                                        double2 *__restrict__ in_new,
+                                                        double *__restrict__ a) {
+  int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  int b = rowptr[i], e = rowptr[i + 1];
+  double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
+  a[i] = ai;
+  double fv = (0.0 + ai) - 0.0;
+  for (int k = b; k < e; ++k) in_new[rev[k]] = make_double2(fv, ai);
+}
+
+// flows of the push layout in CSR order: f[e] = inbox[rev[e]].x
+__global__ void k_push_flows(long long E, const int *__restrict__ rev,
+                             const double2 *__restrict__ in, double *__restrict__ f) {
+  long long e = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (e < E) f[e] = in[rev[e]].x;
+}
+
+__global__ __launch_bounds__(kBlock) void k_max_err(int n, const double *__restrict__ a,
+                                                    const double *__restrict__ target,
+                                                    unsigned long long *__restrict__ err) {
+  unsigned long long eb = 0;
+  for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) {
+    unsigned long long x = err_bits(a[i], target[i]);
+    eb = x > eb ? x : eb;
+  }
+  block_max_to(eb, err);
+}
+
+// ------------------------------------------------------------------------------------
+// Tick replay: one thread per task (= one node's events in one tick, in program order).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_replay_tick(
+    long long task_begin, int ntasks, const int *__restrict__ tasks,
+    const long long *__restrict__ rowptr, const int *__restrict__ events,
+    const int *__restrict__ out_ids, const double *__restrict__ v, double *__restrict__ flow,
+    double *__restrict__ est, double *__restrict__ last, double2 *__restrict__ msg) {
+  int q = blockIdx.x * kBlock + threadIdx.x;
+  if (q >= ntasks) return;
+  const int *tk = tasks + 3 * (task_begin + q);
+  const int node = tk[0], evb = tk[1], eve = tk[2];
+  double *fl = flow + rowptr[node];
+  double *es = est + rowptr[node];
+  const double val = v[node];
+  for (int p = evb; p < eve; ++p) {
+    const int4 ev = *reinterpret_cast<const int4 *>(events + 4 * (long long)p);
+    if (ev.x == FU_EV_RECV) {  // CA:98-99 / PW:98-99
+      const double2 m = msg[ev.z];
+      es[ev.y] = m.y;
+      fl[ev.y] = -m.x;
+    } else if (ev.x == FU_EV_FIRE_CA) {  // CA:105-125
+      const int k = ev.y;
+      double S = 0.0, T = 0.0;
+      for (int j = 0; j < k; ++j) S = S + fl[j];
+      const double estimate = val - S;
+      for (int j = 0; j < k; ++j) T = T + es[j];
+      const double avg = (estimate + T) / (double)(k + 1);
+      last[node] = avg;
+      for (int j = 0; j < k; ++j) {
+        const double nf = (fl[j] + avg) - es[j];
+        fl[j] = nf;
+        es[j] = avg;
+        msg[out_ids[ev.z + j]] = make_double2(nf, avg);
+      }
+    } else {  // FIRE_PW, PW:102-117
+      const int s = ev.y, k = ev.z;
+      double S = 0.0;
+      for (int j = 0; j < k; ++j) S = S + fl[j];
+      const double estimate = val - S;
+      const double avg = (es[s] + estimate) / 2.0;
+      last[node] = avg;
+      const double nf = (fl[s] + avg) - es[s];
+      fl[s] = nf;
+      es[s] = avg;
+      msg[ev.w] = make_double2(nf, avg);
+    }
+  }
+}
+
+template <typename T>
+int dmalloc(T **p, size_t count) {
+  if (count == 0) count = 1;
+  hipError_t e = hipMalloc((void **)p, sizeof(T) * count);
+  if (e != hipSuccess) {
+    *p = nullptr;
+    return fail(FU_ERR_ALLOC, std::string("hipMalloc(") + std::to_string(sizeof(T) * count) + "): " + hipGetErrorString(e));
+  }
+  return FU_OK;
+}
+
+}  // namespace
+
+// ======================================================================================
+// handle
+// ======================================================================================
+struct fu_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int32_t n = 0;
+  int64_t E = 0;
+  int32_t max_deg = 0;
+  int *rowptr = nullptr, *col = nullptr, *rev = nullptr;
+  double *v = nullptr;
+  double *f[2] = {nullptr, nullptr};
+  double *a[2] = {nullptr, nullptr};
+  double2 *inbox[2] = {nullptr, nullptr};
+  double *target = nullptr;
+  unsigned long long *err = nullptr;
+  int errcap = 0;
+  double *ftmp = nullptr;
+  int cur = 0;
+  int64_t rounds = 0;
+  int kernel = 2;
+  int hub_threshold = 64;
+  std::vector<int64_t> h_rowptr;
+  int2 *tiles = nullptr;
+  int ntiles = 0;
+  bool has_target = false;
+  // multi-GPU (fu_dist.hip)
+  void *dist = nullptr;
+};
+
+extern "C" int fu__dist_round_hook(fu_handle *h, int phase);
+extern "C" void fu__dist_free(fu_handle *h);
+
+namespace {
+
+int build_tiles(fu_handle *h) {
+  std::vector<int2> heavy, light;
+  const int32_t n = h->n;
+  int32_t i = 0;
+  while (i < n) {
+    int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
+    if (d > h->hub_threshold || d > kTileEdges) {
+      heavy.push_back(make_int2(i, -1));
+      ++i;
+      continue;
+    }
+    int32_t b = i;
+    int64_t eb = h->h_rowptr[b];
+    while (i < n && i - b < kTileNodes) {
+      int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
+      if (di > h->hub_threshold || di > kTileEdges) break;
+      if (h->h_rowptr[i + 1] - eb > kTileEdges) break;
+      ++i;
+    }
+    light.push_back(make_int2(b, i));
+  }
+  // heavy tiles first so their long sequential chains start early
+  std::vector<int2> all(heavy);
+  all.insert(all.end(), light.begin(), light.end());
+  if (h->tiles) hipFree(h->tiles);
+  h->tiles = nullptr;
+  h->ntiles = (int)all.size();
+  if (int rc = dmalloc(&h->tiles, all.size())) return rc;
+  HIP_TRY(hipMemcpy(h->tiles, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+  return FU_OK;
+}
+
+int ensure_inbox(fu_handle *h) {
+  if (h->inbox[0]) return FU_OK;
+  for (int k = 0; k < 2; ++k)
+    if (int rc = dmalloc(&h->inbox[k], (size_t)h->E)) return rc;
+  return FU_OK;
+}
+
+inline unsigned grid_for(long long work) { return (unsigned)((work + kBlock - 1) / kBlock); }
+
+// One round: state in buffer `cur` -> buffer `cur ^ 1`. err_slot: nullptr = no check.
+int launch_round(fu_handle *h, unsigned long long *err_slot) {
+  const int src = h->cur, dst = h->cur ^ 1;
+  const bool check = err_slot != nullptr;
+  if (h->dist) {
+    if (int rc = fu__dist_round_hook(h, 0)) return rc;
+  }
+  if (h->rounds == 0) {
+    if (h->kernel == 3) {
+      hipLaunchKernelGGL(k_round0_push, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
+                         h->rowptr, h->rev, h->v, h->inbox[dst], h->a[dst]);
+    } else {
+      hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
+                         h->rowptr, h->v, h->f[dst], h->a[dst]);
+    }
+    if (check) {
+      hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
+                         h->stream, h->n, h->a[dst], h->target, err_slot);
+    }
+  } else if (h->kernel == 1) {
+    if (check)
+      hipLaunchKernelGGL(k_round_tpn<true>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream,
+                         h->n, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src], h->f[dst],
+                         h->a[dst], h->target, err_slot);
+    else
+      hipLaunchKernelGGL(k_round_tpn<false>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream,
+                         h->n, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src], h->f[dst],
+                         h->a[dst], h->target, err_slot);
+  } else if (h->kernel == 2) {
+    if (check)
+      hipLaunchKernelGGL(k_round_tile<true>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
+                         h->tiles, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src],
+                         h->f[dst], h->a[dst], h->target, err_slot);
+    else
+      hipLaunchKernelGGL(k_round_tile<false>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
+                         h->tiles, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src],
+                         h->f[dst], h->a[dst], h->target, err_slot);
+  } else {
+    if (check)
+      hipLaunchKernelGGL(k_round_push<true>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
+                         h->tiles, h->rowptr, h->rev, h->v, h->inbox[src], h->inbox[dst],
+                         h->a[dst], h->target, err_slot);
+    else
+      hipLaunchKernelGGL(k_round_push<false>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
+                         h->tiles, h->rowptr, h->rev, h->v, h->inbox[src], h->inbox[dst],
+                         h->a[dst], h->target, err_slot);
+  }
+  HIP_TRY(hipGetLastError());
+  h->cur = dst;
+  h->rounds++;
+  if (h->dist) {
+    if (int rc = fu__dist_round_hook(h, 1)) return rc;
+  }
+  return FU_OK;
+}
+
+int set_device(fu_handle *h) {
+  HIP_TRY(hipSetDevice(h->device));
+  return FU_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fu_device_count(int32_t *out) {
+  if (!out) return fail(FU_ERR_ARG, "fu_device_count: NULL");
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+  *out = c;
+  return FU_OK;
+}
+
+// Internal constructor shared by fu_create / fu_dist_create: uploads the local CSR.
+int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
+                      const int32_t *rev, const double *value, int32_t device,
+                      int64_t f_extra, int32_t a_extra, fu_handle **out) {
+  FU_TRY_BEGIN
+  if (!out || n <= 0 || e < 0 || !rowptr || !value || (e > 0 && (!col || !rev)))
+    return fail(FU_ERR_ARG, "fu_create: bad arguments");
+  if (e + f_extra >= (int64_t)INT32_MAX) return fail(FU_ERR_ARG, "fu_create: more than 2^31-1 edges");
+  if (rowptr[0] != 0 || rowptr[n] != e) return fail(FU_ERR_ARG, "fu_create: rowptr[0] must be 0 and rowptr[n] == e");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FU_ERR_HIP, "fu_create: no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(FU_ERR_ARG, "fu_create: device out of range");
+  auto *h = new fu_handle();
+  h->device = device;
+  h->n = n;
+  h->E = e;
+  h->h_rowptr.assign(rowptr, rowptr + n + 1);
+  std::vector<int32_t> rp32(n + 1);
+  int32_t md = 0;
+  for (int32_t i = 0; i <= n; ++i) {
+    rp32[i] = (int32_t)rowptr[i];
+    if (i < n) {
+      if (rowptr[i + 1] < rowptr[i]) { delete h; return fail(FU_ERR_ARG, "fu_create: rowptr not monotone"); }
+      md = std::max<int32_t>(md, (int32_t)(rowptr[i + 1] - rowptr[i]));
+    }
+  }
+  h->max_deg = md;
+  const int64_t fe = e + f_extra;
+  const int32_t na = n + a_extra;
+  for (int64_t k = 0; k < e; ++k) {
+    if (col[k] < 0 || col[k] >= na || rev[k] < 0 || rev[k] >= fe) {
+      delete h;
+      return fail(FU_ERR_ARG, "fu_create: col/rev index out of range at edge " + std::to_string(k));
+    }
+  }
+  int rc = FU_OK;
+  auto cleanup = [&](int code) { fu_destroy(h); return code; };
+  if ((rc = set_device(h))) return cleanup(rc);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
+  if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (rc = dmalloc(&h->rev, e)) ||
+      (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) ||
+      (rc = dmalloc(&h->a[0], na)) || (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->target, n)) ||
+      (rc = dmalloc(&h->err, 1)))
+    return cleanup(rc);
+  h->errcap = 1;
+  if (hipMemcpy(h->rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
+      (e && hipMemcpy(h->col, col, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
+      (e && hipMemcpy(h->rev, rev, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(h->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
+  if (hipMemset(h->f[0], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
+      hipMemset(h->f[1], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
+      hipMemset(h->a[0], 0, sizeof(double) * na) != hipSuccess ||
+      hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
+  if ((rc = build_tiles(h))) return cleanup(rc);
+  *out = h;
+  return FU_OK;
+  FU_TRY_END
+}
+
+int fu_create(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
+              const int32_t *rev, const double *value, int32_t device, fu_handle **out) {
+  FU_TRY_BEGIN
+  if (!rowptr || n <= 0) return fail(FU_ERR_ARG, "fu_create: bad arguments");
+  std::vector<int32_t> own_rev;
+  if (!rev && e > 0) {
+    fu_graph g;
+    g.n = n;
+    g.rowptr.assign(rowptr, rowptr + n + 1);
+    if (!col) return fail(FU_ERR_ARG, "fu_create: col is NULL");
+    g.col.assign(col, col + e);
+    if (int rc = fu::build_rev(g)) return rc;
+    own_rev.swap(g.rev);
+    rev = own_rev.data();
+  }
+  return fu__create_common(n, e, rowptr, col, rev, value, device, 0, 0, out);
+  FU_TRY_END
+}
+
+int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
+                         fu_handle **out) {
+  if (!g) return fail(FU_ERR_ARG, "fu_create_from_graph: NULL graph");
+  const int64_t E = g->rowptr[g->n];
+  if ((int64_t)g->rev.size() != E) return fail(FU_ERR_GRAPH, "fu_create_from_graph: graph is not symmetric");
+  return fu__create_common(g->n, E, g->rowptr.data(), g->col.data(), g->rev.data(), value, device, 0, 0, out);
+}
+
+int fu_set_option(fu_handle *h, const char *key, int64_t value) {
+  if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
+  if (int rc = set_device(h)) return rc;
+  if (!std::strcmp(key, "kernel")) {
+    if (value < 0 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..3");
+    if (h->dist && value == 3) return fail(FU_ERR_ARG, "fu_set_option: kernel 3 (push) is single-GPU only");
+    if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
+    h->kernel = value == 0 ? 2 : (int)value;
+    if (h->kernel == 3) return ensure_inbox(h);
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "hub_threshold")) {
+    if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: hub_threshold must be >= 1");
+    h->hub_threshold = (int)std::min<int64_t>(value, kTileEdges);
+    return build_tiles(h);
+  }
+  return fail(FU_ERR_ARG, std::string("fu_set_option: unknown key '") + key + "'");
+}
+
+int fu_reset(fu_handle *h) {
+  if (!h) return fail(FU_ERR_ARG, "fu_reset: NULL handle");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->rounds = 0;
+  h->cur = 0;
+  return FU_OK;
+}
+
+int fu_set_targets(fu_handle *h, const double *target) {
+  if (!h || !target) return fail(FU_ERR_ARG, "fu_set_targets: NULL argument");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipMemcpyAsync(h->target, target, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->has_target = true;
+  return FU_OK;
+}
+
+int fu__err_slots(fu_handle *h, int count) {
+  if (count <= h->errcap) return FU_OK;
+  if (h->err) hipFree(h->err);
+  h->err = nullptr;
+  h->errcap = 0;
+  if (int rc = dmalloc(&h->err, count)) return rc;
+  h->errcap = count;
+  return FU_OK;
+}
+
+int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *err_trace) {
+  FU_TRY_BEGIN
+  if (!h || rounds < 0) return fail(FU_ERR_ARG, "fu_run_collectall: bad arguments");
+  if (err_every > 0 && !h->has_target) return fail(FU_ERR_STATE, "fu_run_collectall: err_every > 0 needs fu_set_targets");
+  if (int rc = set_device(h)) return rc;
+  const int nerr = err_every > 0 ? rounds / err_every : 0;
+  if (nerr > 0) {
+    if (int rc = fu__err_slots(h, nerr)) return rc;
+    HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(unsigned long long) * nerr, h->stream));
+  }
+  for (int32_t r = 0; r < rounds; ++r) {
+    unsigned long long *slot = nullptr;
+    if (nerr > 0 && (r + 1) % err_every == 0) slot = h->err + ((r + 1) / err_every - 1);
+    if (int rc = launch_round(h, slot)) return rc;
+  }
+  if (nerr > 0) {
+    if (h->dist) {
+      if (int rc = fu__dist_round_hook(h, 100 + nerr)) return rc;  // all-reduce max, in place
+    }
+    std::vector<unsigned long long> bits(nerr);
+    HIP_TRY(hipMemcpyAsync(bits.data(), h->err, sizeof(unsigned long long) * nerr, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (err_trace) std::memcpy(err_trace, bits.data(), sizeof(double) * nerr);
+  }
+  return FU_OK;
+  FU_TRY_END
+}
+
+int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
+  if (!h || !ms || rounds < 0) return fail(FU_ERR_ARG, "fu_run_collectall_timed: bad arguments");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipEventRecord(h->ev0, h->stream));
+  for (int32_t r = 0; r < rounds; ++r)
+    if (int rc = launch_round(h, nullptr)) return rc;
+  HIP_TRY(hipEventRecord(h->ev1, h->stream));
+  HIP_TRY(hipEventSynchronize(h->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, h->ev0, h->ev1));
+  return FU_OK;
+}
+
+int fu_max_err(fu_handle *h, double *out) {
+  if (!h || !out) return fail(FU_ERR_ARG, "fu_max_err: NULL argument");
+  if (!h->has_target) return fail(FU_ERR_STATE, "fu_max_err: call fu_set_targets first");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(unsigned long long), h->stream));
+  hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream,
+                     h->n, h->a[h->cur], h->target, h->err);
+  HIP_TRY(hipGetLastError());
+  if (h->dist) {
+    if (int rc = fu__dist_round_hook(h, 101)) return rc;  // all-reduce max of slot 0
+  }
+  unsigned long long bits = 0;
+  HIP_TRY(hipMemcpyAsync(&bits, h->err, sizeof(bits), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  std::memcpy(out, &bits, sizeof(double));
+  return FU_OK;
+}
+
+int fu_get_estimates(fu_handle *h, double *a_out) {
+  if (!h || !a_out) return fail(FU_ERR_ARG, "fu_get_estimates: NULL argument");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipMemcpyAsync(a_out, h->a[h->cur], sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FU_OK;
+}
+
+int fu_get_flows(fu_handle *h, double *f_out) {
+  if (!h || (!f_out && h->E)) return fail(FU_ERR_ARG, "fu_get_flows: NULL argument");
+  if (h->E == 0) return FU_OK;
+  if (int rc = set_device(h)) return rc;
+  const double *src = h->f[h->cur];
+  if (h->kernel == 3 && h->rounds > 0) {
+    if (!h->ftmp) {
+      if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
+    }
+    hipLaunchKernelGGL(k_push_flows, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
+                       h->rev, h->inbox[h->cur], h->ftmp);
+    HIP_TRY(hipGetLastError());
+    src = h->ftmp;
+  }
+  HIP_TRY(hipMemcpyAsync(f_out, src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FU_OK;
+}
+
+int fu_get_round(fu_handle *h, int64_t *rounds_done) {
+  if (!h || !rounds_done) return fail(FU_ERR_ARG, "fu_get_round: NULL argument");
+  *rounds_done = h->rounds;
+  return FU_OK;
+}
+
+int fu_synchronize(fu_handle *h) {
+  if (!h) return fail(FU_ERR_ARG, "fu_synchronize: NULL handle");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  return FU_OK;
+}
+
+int fu_destroy(fu_handle *h) {
+  if (!h) return FU_OK;
+  hipSetDevice(h->device);
+  if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->dist) fu__dist_free(h);
+  void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1],
+                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+  if (h->ev0) hipEventDestroy(h->ev0);
+  if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->stream) hipStreamDestroy(h->stream);
+  delete h;
+  return FU_OK;
+}
+
+// ======================================================================================
+// replay
+// ======================================================================================
+struct fu_replay {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int32_t n = 0, ticks = 0, cur_tick = 0;
+  int64_t E = 0, n_msgs = 0;
+  std::vector<int64_t> h_tto;
+  long long *rowptr = nullptr;
+  int *tasks = nullptr, *events = nullptr, *out_ids = nullptr;
+  double *v = nullptr, *flow = nullptr, *est = nullptr, *last = nullptr;
+  double2 *msg = nullptr;
+};
+
+int fu_replay_create(int32_t n, const int64_t *rowptr, const double *value, int32_t ticks,
+                     const int64_t *tick_task_off, int64_t n_tasks, const int32_t *tasks,
+                     int64_t n_events, const int32_t *events, int64_t n_out_ids,
+                     const int32_t *out_ids, int64_t n_msgs, int32_t device,
+                     fu_replay **out) {
+  FU_TRY_BEGIN
+  if (!out || n <= 0 || !rowptr || !value || ticks < 0 || !tick_task_off || n_tasks < 0 || n_events < 0 ||
+      n_out_ids < 0 || n_msgs < 0)
+    return fail(FU_ERR_ARG, "fu_replay_create: bad arguments");
+  if (tick_task_off[0] != 0 || tick_task_off[ticks] != n_tasks) return fail(FU_ERR_ARG, "fu_replay_create: tick_task_off inconsistent");
+  const int64_t E = rowptr[n];
+  // validate the trace on the host: every index a kernel will dereference
+  for (int64_t q = 0; q < n_tasks; ++q) {
+    int32_t node = tasks[3 * q], b = tasks[3 * q + 1], e = tasks[3 * q + 2];
+    if (node < 0 || node >= n || b < 0 || e < b || e > n_events) return fail(FU_ERR_ARG, "fu_replay_create: bad task " + std::to_string(q));
+    const int64_t deg = rowptr[node + 1] - rowptr[node];
+    for (int32_t p = b; p < e; ++p) {
+      const int32_t *ev = events + 4 * (int64_t)p;
+      bool ok;
+      if (ev[0] == FU_EV_RECV) ok = ev[1] >= 0 && ev[1] < deg && ev[2] >= 0 && ev[2] < n_msgs;
+      else if (ev[0] == FU_EV_FIRE_CA) ok = ev[1] >= 0 && ev[1] <= deg && ev[2] >= 0 && (int64_t)ev[2] + ev[1] <= n_out_ids;
+      else if (ev[0] == FU_EV_FIRE_PW) ok = ev[1] >= 0 && ev[1] < deg && ev[2] > ev[1] && ev[2] <= deg && ev[3] >= 0 && ev[3] < n_msgs;
+      else ok = false;
+      if (!ok) return fail(FU_ERR_ARG, "fu_replay_create: bad event " + std::to_string(p));
+    }
+  }
+  for (int64_t q = 0; q < n_out_ids; ++q)
+    if (out_ids[q] < 0 || out_ids[q] >= n_msgs) return fail(FU_ERR_ARG, "fu_replay_create: bad out_id");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FU_ERR_HIP, "fu_replay_create: no HIP device visible");
+  if (device < 0 || device >= ndev) return fail(FU_ERR_ARG, "fu_replay_create: device out of range");
+  auto *r = new fu_replay();
+  auto cleanup = [&](int code) { fu_replay_destroy(r); return code; };
+  r->device = device;
+  r->n = n;
+  r->ticks = ticks;
+  r->E = E;
+  r->n_msgs = n_msgs;
+  r->h_tto.assign(tick_task_off, tick_task_off + ticks + 1);
+  if (hipSetDevice(device) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  if (hipEventCreate(&r->ev0) != hipSuccess || hipEventCreate(&r->ev1) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
+  int rc;
+  if ((rc = dmalloc(&r->rowptr, n + 1)) || (rc = dmalloc(&r->tasks, 3 * n_tasks)) ||
+      (rc = dmalloc(&r->events, 4 * n_events)) || (rc = dmalloc(&r->out_ids, n_out_ids)) ||
+      (rc = dmalloc(&r->v, n)) || (rc = dmalloc(&r->flow, E)) || (rc = dmalloc(&r->est, E)) ||
+      (rc = dmalloc(&r->last, n)) || (rc = dmalloc(&r->msg, n_msgs)))
+    return cleanup(rc);
+  static_assert(sizeof(long long) == sizeof(int64_t), "int64");
+  if (hipMemcpy(r->rowptr, rowptr, sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
+      (n_tasks && hipMemcpy(r->tasks, tasks, sizeof(int32_t) * 3 * n_tasks, hipMemcpyHostToDevice) != hipSuccess) ||
+      (n_events && hipMemcpy(r->events, events, sizeof(int32_t) * 4 * n_events, hipMemcpyHostToDevice) != hipSuccess) ||
+      (n_out_ids && hipMemcpy(r->out_ids, out_ids, sizeof(int32_t) * n_out_ids, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(r->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemset(r->flow, 0, sizeof(double) * (E ? E : 1)) != hipSuccess ||
+      hipMemset(r->est, 0, sizeof(double) * (E ? E : 1)) != hipSuccess ||
+      hipMemset(r->last, 0, sizeof(double) * n) != hipSuccess ||
+      hipMemset(r->msg, 0, sizeof(double2) * (n_msgs ? n_msgs : 1)) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "fu_replay_create: upload failed"));
+  *out = r;
+  return FU_OK;
+  FU_TRY_END
+}
+
+const fu_trace *fu__trace_view(const fu_trace *t, int32_t *n, int32_t *ticks,
+                               const int64_t **urowptr, const int64_t **tto,
+                               const int32_t **tasks, int64_t *n_tasks,
+                               const int32_t **events, int64_t *n_events,
+                               const int32_t **out_ids, int64_t *n_out, int64_t *n_msgs);
+
+int fu_replay_create_from_trace(const fu_trace *t, const double *value, int32_t device,
+                                fu_replay **out) {
+  if (!t) return fail(FU_ERR_ARG, "fu_replay_create_from_trace: NULL trace");
+  int32_t n, ticks;
+  const int64_t *urp, *tto;
+  const int32_t *tasks, *events, *oids;
+  int64_t nt, ne, no, nm;
+  fu__trace_view(t, &n, &ticks, &urp, &tto, &tasks, &nt, &events, &ne, &oids, &no, &nm);
+  return fu_replay_create(n, urp, value, ticks, tto, nt, tasks, ne, events, no, oids, nm, device, out);
+}
+
+static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
+                        double *snaps_dev) {
+  int32_t si = 0;
+  while (si < n_snap && snap_ticks[si] < r->cur_tick) ++si;
+  for (int32_t t = r->cur_tick; t < tick_end; ++t) {
+    const long long b = r->h_tto[t];
+    const int cnt = (int)(r->h_tto[t + 1] - b);
+    if (cnt > 0) {
+      hipLaunchKernelGGL(k_replay_tick, dim3(grid_for(cnt)), dim3(kBlock), 0, r->stream, b, cnt,
+                         r->tasks, r->rowptr, r->events, r->out_ids, r->v, r->flow, r->est,
+                         r->last, r->msg);
+      HIP_TRY(hipGetLastError());
+    }
+    while (si < n_snap && snap_ticks[si] == t) {
+      HIP_TRY(hipMemcpyAsync(snaps_dev + (int64_t)si * r->n, r->last, sizeof(double) * r->n,
+                             hipMemcpyDeviceToDevice, r->stream));
+      ++si;
+    }
+  }
+  r->cur_tick = tick_end;
+  return FU_OK;
+}
+
+int fu_replay_run(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
+                  double *snaps) {
+  if (!r || tick_end < r->cur_tick || tick_end > r->ticks || n_snap < 0 || (n_snap > 0 && (!snap_ticks || !snaps)))
+    return fail(FU_ERR_ARG, "fu_replay_run: bad arguments");
+  for (int32_t k = 1; k < n_snap; ++k)
+    if (snap_ticks[k] <= snap_ticks[k - 1]) return fail(FU_ERR_ARG, "fu_replay_run: snap_ticks must be ascending");
+  HIP_TRY(hipSetDevice(r->device));
+  double *d_snaps = nullptr;
+  if (n_snap > 0) {
+    if (int rc = dmalloc(&d_snaps, (size_t)n_snap * r->n)) return rc;
+    hipMemsetAsync(d_snaps, 0, sizeof(double) * n_snap * r->n, r->stream);
+  }
+  int rc = replay_ticks(r, tick_end, n_snap, snap_ticks, d_snaps);
+  if (rc == FU_OK && n_snap > 0) {
+    if (hipMemcpyAsync(snaps, d_snaps, sizeof(double) * n_snap * r->n, hipMemcpyDeviceToHost, r->stream) != hipSuccess)
+      rc = fail(FU_ERR_HIP, "fu_replay_run: snapshot copy failed");
+  }
+  if (hipStreamSynchronize(r->stream) != hipSuccess && rc == FU_OK) rc = fail(FU_ERR_HIP, "fu_replay_run: sync failed");
+  if (d_snaps) hipFree(d_snaps);
+  return rc;
+}
+
+int fu_replay_run_timed(fu_replay *r, int32_t tick_end, float *ms) {
+  if (!r || !ms || tick_end < r->cur_tick || tick_end > r->ticks) return fail(FU_ERR_ARG, "fu_replay_run_timed: bad arguments");
+  HIP_TRY(hipSetDevice(r->device));
+  HIP_TRY(hipEventRecord(r->ev0, r->stream));
+  if (int rc = replay_ticks(r, tick_end, 0, nullptr, nullptr)) return rc;
+  HIP_TRY(hipEventRecord(r->ev1, r->stream));
+  HIP_TRY(hipEventSynchronize(r->ev1));
+  HIP_TRY(hipEventElapsedTime(ms, r->ev0, r->ev1));
+  return FU_OK;
+}
+
+int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est) {
+  if (!r) return fail(FU_ERR_ARG, "fu_replay_get: NULL replay");
+  HIP_TRY(hipSetDevice(r->device));
+  if (last_avg) HIP_TRY(hipMemcpyAsync(last_avg, r->last, sizeof(double) * r->n, hipMemcpyDeviceToHost, r->stream));
+  if (flows && r->E) HIP_TRY(hipMemcpyAsync(flows, r->flow, sizeof(double) * r->E, hipMemcpyDeviceToHost, r->stream));
+  if (est && r->E) HIP_TRY(hipMemcpyAsync(est, r->est, sizeof(double) * r->E, hipMemcpyDeviceToHost, r->stream));
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  return FU_OK;
+}
+
+int fu_replay_destroy(fu_replay *r) {
+  if (!r) return FU_OK;
+  hipSetDevice(r->device);
+  if (r->stream) hipStreamSynchronize(r->stream);
+  void *ptrs[] = {r->rowptr, r->tasks, r->events, r->out_ids, r->v, r->flow, r->est, r->last, r->msg};
+  for (void *p : ptrs)
+    if (p) hipFree(p);
+  if (r->ev0) hipEventDestroy(r->ev0);
+  if (r->ev1) hipEventDestroy(r->ev1);
+  if (r->stream) hipStreamDestroy(r->stream);
+  delete r;
+  return FU_OK;
+}
+
+}  // extern "C"
+
+// Accessors for fu_dist.hip (fu_handle's layout stays private to this file).
+extern "C" {
+void *fu__handle_dist(fu_handle *h) { return h->dist; }
+void fu__handle_set_dist(fu_handle *h, void *d) { h->dist = d; }
+hipStream_t fu__handle_stream(fu_handle *h) { return h->stream; }
+double *fu__handle_f(fu_handle *h, int which) { return h->f[which]; }
+double *fu__handle_a(fu_handle *h, int which) { return h->a[which]; }
+int fu__handle_cur(fu_handle *h) { return h->cur; }
+unsigned long long *fu__handle_err(fu_handle *h) { return h->err; }
+int fu__handle_device(fu_handle *h) { return h->device; }
+}

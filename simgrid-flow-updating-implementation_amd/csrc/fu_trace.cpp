@@ -1,0 +1,337 @@
+// Tick-level trace generator: the value-independent schedule of the reference run.
+//
+// The reference runs each node as a SimGrid actor executing Peer.loop
+// (flowupdating-collectall.py:70-85, flowupdating-pairwise.py:69-84):
+//     if comm is None: comm = mailbox.get_async()          CA:73-74
+//     if comm.test(): msg = ...; comm = None; on_receive()  CA:76-82
+//     tick()                                                CA:84
+//     sleep_for(1.0)                                        CA:85
+// Mailboxes are rendez-vous points: a put_async matches a posted get_async or is queued
+// FIFO. Every route of the reference platform transfers in (0, 1) simulated seconds
+// (SURVEY.md App. B), so a message matched at tick t is consumed at tick t+1 at the
+// earliest. Whether a node fires depends only on who has been heard (CA:100-103), on tick
+// counters (CA:87-91) and on clocks (PW:86-91), never on fp values. So the whole schedule
+// can be generated here once and replayed on the GPU as one batch per tick.
+//
+// The generator emits, per tick, one task per actor that did something: its events in
+// program order.
+//   RECV    {0, slot, msg, 0}       on_receive cache update        (CA:98-99, PW:98-99)
+//   FIRE_CA {1, k, out_off, 0}      avg_and_send over k neighbours (CA:105-128)
+//   FIRE_PW {2, slot, k, msg_out}   avg_and_send(neigh)            (PW:102-117)
+// Neighbours unknown to a receiver are appended to its row (CA:94-96 / PW:94-96), so each
+// row of the union CSR is in insertion order: declared first (ACT:4-27), then first arrival.
+//
+// Message slots are recycled. A slot consumed at tick t becomes free at the end of tick t,
+// so no slot is both read and written in the same tick batch.
+#include <cstring>
+#include <unordered_map>
+
+#include "fu_common.h"
+
+struct fu_trace {
+  int32_t n = 0, mode = 0, ticks = 0;
+  std::vector<int64_t> urowptr;
+  std::vector<int32_t> ucol;
+  std::vector<int64_t> tick_task_off;
+  std::vector<int32_t> tasks;
+  std::vector<int32_t> events;
+  std::vector<int32_t> out_ids;
+  std::vector<int64_t> first_avg_seq;
+  std::vector<int32_t> fires;
+  int64_t n_msg_slots = 0, dyn_adds = 0, msgs_sent = 0;
+};
+
+namespace {
+
+using namespace fu;
+
+struct Builder {
+  int32_t n;
+  int32_t mode;
+  fu_trace &tr;
+  std::vector<std::vector<int32_t>> nbrs;
+  std::unordered_map<uint64_t, int32_t> slot_of;
+  // collect-all state
+  std::vector<std::vector<uint8_t>> heard;
+  std::vector<int32_t> heard_cnt, counter;
+  // pairwise state (clock of last average per neighbour slot; defaultdict(float) -> 0.0)
+  std::vector<std::vector<double>> last;
+  // receive side: 0 none, 1 posted (unmatched), 2 matched
+  std::vector<int8_t> cstate;
+  std::vector<int32_t> cmsg, ctick;
+  // FIFO queues as linked lists over message ids
+  std::vector<int32_t> qhead, qtail, qnext;
+  std::vector<int32_t> msg_sender;
+  std::vector<int32_t> free_ids, pending_free;
+  int64_t first_seq = 0;
+  int32_t t = 0;
+
+  Builder(int32_t n_, int32_t mode_, fu_trace &tr_) : n(n_), mode(mode_), tr(tr_) {}
+
+  int32_t alloc_msg(int32_t sender) {
+    int32_t id;
+    if (!free_ids.empty()) {
+      id = free_ids.back();
+      free_ids.pop_back();
+    } else {
+      id = (int32_t)msg_sender.size();
+      msg_sender.push_back(-1);
+      qnext.push_back(-1);
+    }
+    msg_sender[id] = sender;
+    qnext[id] = -1;
+    tr.msgs_sent++;
+    return id;
+  }
+
+  void deliver(int32_t dst, int32_t id) {
+    if (cstate[dst] == 1) {  // posted receive: matched now, transfer in flight
+      cstate[dst] = 2;
+      cmsg[dst] = id;
+      ctick[dst] = t;
+    } else {
+      if (qtail[dst] < 0) qhead[dst] = id;
+      else qnext[qtail[dst]] = id;
+      qtail[dst] = id;
+    }
+  }
+
+  void note_fire(int32_t i) {
+    if (tr.fires[i]++ == 0) tr.first_avg_seq[i] = first_seq++;
+  }
+
+  void push_event(int32_t a, int32_t b, int32_t c, int32_t d) {
+    tr.events.push_back(a);
+    tr.events.push_back(b);
+    tr.events.push_back(c);
+    tr.events.push_back(d);
+  }
+
+  void fire_ca(int32_t i) {  // CA:105-128
+    const int32_t k = (int32_t)nbrs[i].size();
+    push_event(FU_EV_FIRE_CA, k, (int32_t)tr.out_ids.size(), 0);
+    note_fire(i);
+    for (int32_t s = 0; s < k; ++s) {
+      int32_t id = alloc_msg(i);
+      tr.out_ids.push_back(id);
+      deliver(nbrs[i][s], id);
+    }
+    std::fill(heard[i].begin(), heard[i].end(), 0);  // CA:127
+    heard_cnt[i] = 0;
+    counter[i] = 0;  // CA:128
+  }
+
+  void fire_pw(int32_t i, int32_t s) {  // PW:102-117
+    const int32_t k = (int32_t)nbrs[i].size();
+    int32_t id = alloc_msg(i);
+    push_event(FU_EV_FIRE_PW, s, k, id);
+    note_fire(i);
+    last[i][s] = (double)t;  // PW:111
+    deliver(nbrs[i][s], id);
+  }
+
+  int32_t slot_for(int32_t i, int32_t sender) {
+    uint64_t key = ((uint64_t)(uint32_t)i << 32) | (uint32_t)sender;
+    auto it = slot_of.find(key);
+    if (it != slot_of.end()) return it->second;
+    int32_t s = (int32_t)nbrs[i].size();  // CA:94-95: append unknown sender
+    nbrs[i].push_back(sender);
+    slot_of.emplace(key, s);
+    if (mode == FU_MODE_COLLECTALL) heard[i].push_back(0);
+    else last[i].push_back(0.0);
+    tr.dyn_adds++;
+    return s;
+  }
+
+  void step(int32_t i) {
+    const int64_t ev0 = (int64_t)tr.events.size() / 4;
+    if (cstate[i] == 0) {  // CA:73-74
+      if (qhead[i] >= 0) {
+        int32_t id = qhead[i];
+        qhead[i] = qnext[id];
+        if (qhead[i] < 0) qtail[i] = -1;
+        cstate[i] = 2;
+        cmsg[i] = id;
+        ctick[i] = t;
+      } else {
+        cstate[i] = 1;
+      }
+    }
+    if (cstate[i] == 2 && ctick[i] < t) {  // CA:76-82
+      int32_t id = cmsg[i];
+      cstate[i] = 0;
+      int32_t s = slot_for(i, msg_sender[id]);
+      push_event(FU_EV_RECV, s, id, 0);
+      pending_free.push_back(id);
+      if (mode == FU_MODE_COLLECTALL) {
+        if (!heard[i][s]) {  // CA:100
+          heard[i][s] = 1;
+          heard_cnt[i]++;
+        }
+        if (heard_cnt[i] == (int32_t)nbrs[i].size()) fire_ca(i);  // CA:102-103
+      } else {
+        fire_pw(i, s);  // PW:100
+      }
+    }
+    if (mode == FU_MODE_COLLECTALL) {  // CA:87-91
+      if (++counter[i] >= 50) fire_ca(i);
+    } else {  // PW:86-91
+      const double thr = (double)t - 50.0;
+      for (int32_t s = 0; s < (int32_t)nbrs[i].size(); ++s)
+        if (last[i][s] < thr) fire_pw(i, s);
+    }
+    const int64_t ev1 = (int64_t)tr.events.size() / 4;
+    if (ev1 > ev0) {
+      tr.tasks.push_back(i);
+      tr.tasks.push_back((int32_t)ev0);
+      tr.tasks.push_back((int32_t)ev1);
+    }
+  }
+};
+
+bool parse_order(const char *order, int &kind, uint64_t &seed) {
+  if (!order || !std::strcmp(order, "fwd")) { kind = 0; return true; }
+  if (!std::strcmp(order, "rev")) { kind = 1; return true; }
+  if (!std::strncmp(order, "rand:", 5)) {
+    char *end = nullptr;
+    seed = std::strtoull(order + 5, &end, 10);
+    if (end == order + 5 || *end) return false;
+    kind = 2;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+extern "C" {
+
+int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                   int32_t mode, int32_t ticks, const char *order, fu_trace **out) {
+  FU_TRY_BEGIN
+  if (!out || n <= 0 || !decl_rowptr || ticks < 0 || (mode != FU_MODE_COLLECTALL && mode != FU_MODE_PAIRWISE))
+    return fail(FU_ERR_ARG, "fu_trace_build: bad arguments");
+  int okind = 0;
+  uint64_t oseed = 0;
+  if (!parse_order(order, okind, oseed)) return fail(FU_ERR_ARG, std::string("fu_trace_build: bad order '") + (order ? order : "") + "'");
+  auto *tr = new fu_trace();
+  tr->n = n;
+  tr->mode = mode;
+  tr->ticks = ticks;
+  tr->first_avg_seq.assign(n, -1);
+  tr->fires.assign(n, 0);
+  Builder B(n, mode, *tr);
+  B.nbrs.resize(n);
+  for (int32_t i = 0; i < n; ++i) {
+    for (int64_t k = decl_rowptr[i]; k < decl_rowptr[i + 1]; ++k) {
+      int32_t j = decl_col[k];
+      if (j < 0 || j >= n || j == i) { delete tr; return fail(FU_ERR_GRAPH, "fu_trace_build: bad neighbour id (out of range or self)"); }
+      uint64_t key = ((uint64_t)(uint32_t)i << 32) | (uint32_t)j;
+      if (B.slot_of.count(key)) { delete tr; return fail(FU_ERR_GRAPH, "fu_trace_build: duplicate neighbour"); }
+      B.slot_of.emplace(key, (int32_t)B.nbrs[i].size());
+      B.nbrs[i].push_back(j);
+    }
+  }
+  if (mode == FU_MODE_COLLECTALL) {
+    B.heard.resize(n);
+    for (int32_t i = 0; i < n; ++i) B.heard[i].assign(B.nbrs[i].size(), 0);
+    B.heard_cnt.assign(n, 0);
+    B.counter.assign(n, 0);
+  } else {
+    B.last.resize(n);
+    for (int32_t i = 0; i < n; ++i) B.last[i].assign(B.nbrs[i].size(), 0.0);
+  }
+  B.cstate.assign(n, 0);
+  B.cmsg.assign(n, -1);
+  B.ctick.assign(n, -1);
+  B.qhead.assign(n, -1);
+  B.qtail.assign(n, -1);
+  std::vector<int32_t> perm(n);
+  for (int32_t i = 0; i < n; ++i) perm[i] = okind == 1 ? n - 1 - i : i;
+  uint64_t st = oseed;
+  tr->tick_task_off.push_back(0);
+  for (int32_t t = 0; t < ticks; ++t) {
+    B.t = t;
+    if (okind == 2) {  // per-tick Fisher-Yates, j = r % (i+1) (same as oracle.tick_orders)
+      for (int32_t i = 0; i < n; ++i) perm[i] = i;
+      for (int32_t i = n - 1; i > 0; --i) {
+        uint64_t j = splitmix_next(st) % (uint64_t)(i + 1);
+        std::swap(perm[i], perm[j]);
+      }
+    }
+    for (int32_t q = 0; q < n; ++q) B.step(perm[q]);
+    for (int32_t id : B.pending_free) B.free_ids.push_back(id);
+    B.pending_free.clear();
+    tr->tick_task_off.push_back((int64_t)tr->tasks.size() / 3);
+    if ((int64_t)tr->events.size() / 4 >= (int64_t)INT32_MAX || (int64_t)tr->out_ids.size() >= (int64_t)INT32_MAX) {
+      delete tr;
+      return fail(FU_ERR_ALLOC, "fu_trace_build: trace exceeds 2^31 events");
+    }
+  }
+  tr->n_msg_slots = (int64_t)B.msg_sender.size();
+  tr->urowptr.assign(n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) tr->urowptr[i + 1] = tr->urowptr[i] + (int64_t)B.nbrs[i].size();
+  tr->ucol.reserve(tr->urowptr[n]);
+  for (int32_t i = 0; i < n; ++i) tr->ucol.insert(tr->ucol.end(), B.nbrs[i].begin(), B.nbrs[i].end());
+  *out = tr;
+  return FU_OK;
+  FU_TRY_END
+}
+
+int fu_trace_info(const fu_trace *t, int64_t info[8]) {
+  if (!t || !info) return fail(FU_ERR_ARG, "fu_trace_info: NULL argument");
+  info[0] = t->urowptr[t->n];
+  info[1] = (int64_t)t->tasks.size() / 3;
+  info[2] = (int64_t)t->events.size() / 4;
+  info[3] = (int64_t)t->out_ids.size();
+  info[4] = t->n_msg_slots;
+  info[5] = t->ticks;
+  info[6] = t->dyn_adds;
+  info[7] = t->msgs_sent;
+  return FU_OK;
+}
+
+int fu_trace_export(const fu_trace *t, int64_t *union_rowptr, int32_t *union_col,
+                    int64_t *tick_task_off, int32_t *tasks, int32_t *events,
+                    int32_t *out_ids, int64_t *first_avg_seq, int32_t *fires) {
+  if (!t) return fail(FU_ERR_ARG, "fu_trace_export: NULL trace");
+  auto cp = [](void *dst, const void *src, size_t bytes) {
+    if (dst && bytes) std::memcpy(dst, src, bytes);
+  };
+  cp(union_rowptr, t->urowptr.data(), sizeof(int64_t) * t->urowptr.size());
+  cp(union_col, t->ucol.data(), sizeof(int32_t) * t->ucol.size());
+  cp(tick_task_off, t->tick_task_off.data(), sizeof(int64_t) * t->tick_task_off.size());
+  cp(tasks, t->tasks.data(), sizeof(int32_t) * t->tasks.size());
+  cp(events, t->events.data(), sizeof(int32_t) * t->events.size());
+  cp(out_ids, t->out_ids.data(), sizeof(int32_t) * t->out_ids.size());
+  cp(first_avg_seq, t->first_avg_seq.data(), sizeof(int64_t) * t->first_avg_seq.size());
+  cp(fires, t->fires.data(), sizeof(int32_t) * t->fires.size());
+  return FU_OK;
+}
+
+int fu_trace_free(fu_trace *t) {
+  delete t;
+  return FU_OK;
+}
+
+// Accessors used by the device side (fu_engine.hip) without exposing the struct layout.
+const fu_trace *fu__trace_view(const fu_trace *t, int32_t *n, int32_t *ticks,
+                               const int64_t **urowptr, const int64_t **tto,
+                               const int32_t **tasks, int64_t *n_tasks,
+                               const int32_t **events, int64_t *n_events,
+                               const int32_t **out_ids, int64_t *n_out, int64_t *n_msgs) {
+  *n = t->n;
+  *ticks = t->ticks;
+  *urowptr = t->urowptr.data();
+  *tto = t->tick_task_off.data();
+  *tasks = t->tasks.data();
+  *n_tasks = (int64_t)t->tasks.size() / 3;
+  *events = t->events.data();
+  *n_events = (int64_t)t->events.size() / 4;
+  *out_ids = t->out_ids.data();
+  *n_out = (int64_t)t->out_ids.size();
+  *n_msgs = t->n_msg_slots;
+  return t;
+}
+
+}  // extern "C"

@@ -404,9 +404,31 @@ def parse_actors_xml(path):
     return out
 
 
+def platform_summary():
+    """Hosts / links / routes of the reference platform (PLAT:4-193) as a JSON fixture, so
+    tests can rebuild an equivalent platform without the reference tree."""
+    import xml.etree.ElementTree as ET
+
+    root = ET.parse(os.path.join(REF, "platforms", "small_platform.xml")).getroot()
+    zone = next(root.iter("zone"))
+    out = {
+        "routing": zone.get("routing"),
+        "hosts": [[h.get("id"), h.get("speed")] for h in root.iter("host")],
+        "links": [[ln.get("id"), ln.get("bandwidth"), ln.get("latency"), ln.get("sharing_policy")]
+                  for ln in root.iter("link")],
+        "routes": [[r.get("src"), r.get("dst"), [c.get("id") for c in r.findall("link_ctn")]]
+                   for r in root.iter("route")],
+    }
+    with open(os.path.join(HERE, "small_platform_summary.json"), "w") as f:
+        json.dump(out, f, indent=0)
+
+
 def main():
     if not os.path.isfile(os.path.join(REF, CA_FILE)):
         print(f"make_golden: reference not found at {REF}; nothing to do")
+        return 0
+    platform_summary()
+    if "--only-platform" in sys.argv:
         return 0
     rng = np.random.default_rng(20250629)
 

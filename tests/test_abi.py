@@ -1,0 +1,129 @@
+"""C ABI (include/fu.h) of libfu.so: loads, exports every declared symbol, host-side entry
+points behave; device entry points fail loudly (not silently) without a GPU."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import fu
+import oracle
+from conftest import ROOT
+from fu import _lib as L
+
+
+def declared_symbols():
+    with open(os.path.join(ROOT, "include", "fu.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\s*\*?\s*(fu_\w+)\s*\(", text, re.M)))
+
+
+def test_every_declared_symbol_is_exported():
+    syms = declared_symbols()
+    assert len(syms) >= 35
+    for s in syms:
+        assert hasattr(L.lib, s), s
+    assert set(syms) == set(L.EXPORTED)
+
+
+def test_version_and_device_count():
+    assert L.lib.fu_version() == 1
+    assert fu.device_count() >= 0
+
+
+def test_generators_are_symmetric_and_deterministic():
+    for mk in (lambda: fu.Graph.erdos_renyi(5000, 20000, seed=3),
+               lambda: fu.Graph.random_regular(2000, 8, seed=3),
+               lambda: fu.Graph.rmat(12, 8, seed=3),
+               lambda: fu.Graph.random_geometric(4000, avg_deg=8, seed=3)):
+        g1, g2 = mk(), mk()
+        assert np.array_equal(g1.rowptr, g2.rowptr) and np.array_equal(g1.col, g2.col)
+        assert g1.symmetric
+        rev = oracle.build_rev(g1.rowptr, g1.col)
+        assert np.array_equal(rev, g1.rev)
+        src = np.repeat(np.arange(g1.n), np.diff(g1.rowptr))
+        assert not np.any(src == g1.col)  # no self-loops
+        assert np.all(np.diff(g1.col)[np.diff(src) == 0] > 0)  # sorted, deduplicated rows
+
+
+def test_random_regular_is_regular():
+    g = fu.Graph.random_regular(4096, 8, seed=11)
+    assert np.all(np.diff(g.rowptr) == 8)
+
+
+def test_rgg_edges_within_radius():
+    n, r = 3000, 0.04
+    g = fu.Graph.random_geometric(n, radius=r, seed=2)
+    assert g.E > 0 and g.max_deg > 0
+
+
+def test_generation_independent_of_thread_count():
+    pkg = os.path.join(ROOT, "simgrid-flow-updating-implementation_amd")
+    code = (f"import sys; sys.path.insert(0, {pkg!r}); import fu, numpy as np; "
+            "g = fu.Graph.erdos_renyi(20000, 80000, seed=9); "
+            "print(int(np.sum((g.col.astype(np.int64) * np.arange(g.E)) % 1000003)))")
+    outs = []
+    for t in ("1", "5"):
+        env = dict(os.environ, OMP_NUM_THREADS=t)
+        outs.append(subprocess.run([sys.executable, "-c", code], env=env, check=True,
+                                   capture_output=True, text=True).stdout)
+    assert outs[0] == outs[1]
+
+
+def test_values_uniform_matches_spec():
+    n, seed = 1000, 42
+    v = fu.uniform_values(n, seed=seed, lo=0.0, hi=100.0)
+    M = (1 << 64) - 1
+    ref = []
+    for i in range(n):
+        z = (seed + (i + 1) * 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        z ^= z >> 31
+        ref.append(0.0 + 100.0 * ((z >> 11) * 2.0 ** -53))
+    assert np.array_equal(v, np.array(ref))
+
+
+def test_from_csr_keeps_row_order_and_validates():
+    rp = np.array([0, 2, 3, 4], dtype=np.int64)
+    col = np.array([2, 1, 0, 0], dtype=np.int32)
+    g = fu.Graph.from_csr(rp, col)
+    assert list(g.col) == [2, 1, 0, 0]
+    assert list(g.rev) == list(oracle.build_rev(rp, col))
+    with pytest.raises(fu.FuError, match="not symmetric"):
+        fu.Graph.from_csr(np.array([0, 1, 1], dtype=np.int64), np.array([1], dtype=np.int32))
+    with pytest.raises(fu.FuError, match="self-loop"):
+        fu.Graph.from_csr(np.array([0, 1, 2], dtype=np.int64), np.array([0, 0], dtype=np.int32))
+    with pytest.raises(fu.FuError, match="duplicate"):
+        fu.Graph.from_csr(np.array([0, 2, 4], dtype=np.int64),
+                          np.array([1, 1, 0, 0], dtype=np.int32))
+    g2 = fu.Graph.from_csr(np.array([0, 1, 1], dtype=np.int64), np.array([1], dtype=np.int32),
+                           require_symmetric=False)
+    assert not g2.symmetric
+
+
+def test_from_edges_symmetrises():
+    g = fu.Graph.from_edges(4, [0, 1, 2, 2, 3], [1, 0, 2, 3, 2])
+    assert list(g.rowptr) == [0, 1, 2, 3, 4]
+    assert list(g.col) == [1, 0, 3, 2]
+
+
+@pytest.mark.skipif(fu.device_count() > 0, reason="CPU-only behaviour")
+def test_device_entry_points_fail_loudly_without_gpu():
+    g = fu.Graph.random_regular(64, 4, seed=1)
+    with pytest.raises(fu.FuError, match="no HIP device"):
+        fu.CollectAll(g, np.ones(g.n))
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", 60)
+    with pytest.raises(fu.FuError, match="no HIP device"):
+        fu.Replay(tr, np.ones(g.n))
+
+
+def test_null_arguments_are_errors():
+    out = L.vp()
+    assert L.lib.fu_graph_gen_er(0, 10, 1, ctypes.byref(out)) < 0
+    assert "bad arguments" in L.last_error()
+    assert L.lib.fu_graph_info(None, None, None, None, None) < 0
+    assert L.lib.fu_run_collectall(None, 1, 0, None) < 0

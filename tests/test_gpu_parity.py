@@ -1,0 +1,208 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the oracle and the golden
+fixtures. Bit-exact everywhere: the kernels keep the reference's left-to-right fp64 sums
+(flowupdating-collectall.py:106-113), so no tolerance is needed. Full-size checks use
+properties (convergence to the component means, flow antisymmetry) and a bitwise
+comparison against the C oracle on a prefix of the rounds."""
+import io
+
+import numpy as np
+import pytest
+
+import coracle
+import fu
+from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, tick_fixtures,
+                      write_deployment_xml, write_platform_xml)
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["thread", "tile", "push"]
+
+
+def _check_fixture(meta, kernel, hub_threshold=None):
+    d = load_npz(meta["file"])
+    rounds = [int(r) for r in d["rounds"]]
+    eng = fu.CollectAll(rowptr=d["rowptr"], col=d["col"], values=d["values"], kernel=kernel,
+                        hub_threshold=hub_threshold)
+    done = 0
+    for k, r in enumerate(rounds):
+        eng.run(r + 1 - done)
+        done = r + 1
+        assert np.array_equal(eng.estimates(), d["last_avg"][k]), (meta["file"], kernel, r)
+        assert np.array_equal(eng.flows(), d["flows"][k]), (meta["file"], kernel, r)
+    eng.close()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("name,meta", ca_sync_fixtures())
+def test_ca_sync_fixture_bitwise(name, meta, kernel):
+    _check_fixture(meta, kernel)
+
+
+@pytest.mark.parametrize("kernel", ["tile", "push"])
+@pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
+def test_ca_sync_fixture_heavy_path(name, kernel):
+    """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
+    meta = dict(ca_sync_fixtures())[name]
+    _check_fixture(meta, kernel, hub_threshold=3)
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_er_vs_c_oracle_bitwise(kernel):
+    g = fu.Graph.erdos_renyi(200_000, 800_000, seed=5)
+    v = fu.uniform_values(g.n, seed=1)
+    eng = fu.CollectAll(g, v, kernel=kernel)
+    eng.run(40)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 40, nthreads=8)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
+@pytest.mark.parametrize("kernel", ["tile", "push"])
+def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
+    g = fu.Graph.rmat(15, 16, seed=2)
+    assert g.max_deg > 2048  # exercises chunked heavy tiles
+    v = fu.uniform_values(g.n, seed=4)
+    eng = fu.CollectAll(g, v, kernel=kernel)
+    eng.run(25)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 25, nthreads=8)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
+def test_err_trace_and_max_err():
+    g = fu.Graph.random_regular(4096, 8, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    tgt, _ = fu.component_means(g.rowptr, g.col, v)
+    eng = fu.CollectAll(g, v)
+    eng.set_targets(tgt)
+    tr = eng.run(400, err_every=1)
+    assert len(tr) == 400
+    est = eng.estimates()
+    assert tr[-1] == np.max(np.abs(est - tgt))
+    assert eng.max_err() == tr[-1]
+    first = int(np.argmax(tr < 1e-9)) + 1
+    assert tr[first - 1] < 1e-9 and 150 < first < 260  # 187 rounds on RR-4096
+    # same trace from a C-oracle run at a few rounds
+    for r in (1, 10, 100):
+        a_ref, _ = coracle.ca_sync(g.rowptr, g.col, g.rev, v, r)
+        assert tr[r - 1] == np.max(np.abs(a_ref - tgt))
+
+
+def test_nan_propagates_to_err():
+    g = fu.Graph.random_regular(256, 4, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    v[17] = np.nan
+    eng = fu.CollectAll(g, v)
+    eng.set_targets(np.zeros(g.n))
+    tr = eng.run(3, err_every=1)
+    assert np.isnan(tr).all()
+
+
+def test_isolated_and_empty():
+    rp = np.array([0, 0, 1, 2, 2], dtype=np.int64)
+    col = np.array([2, 1], dtype=np.int32)
+    v = np.array([3.5, -0.0, 7.0, 1e-310])  # isolated nodes, signed zero, subnormal
+    eng = fu.CollectAll(rowptr=rp, col=col, values=v)
+    eng.run(5)
+    a_ref, f_ref = coracle.ca_sync(rp, col, np.array([1, 0], dtype=np.int32), v, 5)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    assert eng.estimates()[3] == 1e-310
+
+
+def test_option_errors():
+    g = fu.Graph.random_regular(64, 4, seed=1)
+    eng = fu.CollectAll(g, np.ones(g.n))
+    with pytest.raises(fu.FuError):
+        eng.set_option("kernel", 9)
+    with pytest.raises(fu.FuError):
+        eng.set_option("nope", 1)
+    with pytest.raises(fu.FuError):
+        eng.run(5, err_every=1)  # no targets
+    eng.run(2)
+    with pytest.raises(fu.FuError):
+        eng.set_option("kernel", 1)  # after rounds ran
+    eng.reset()
+    eng.set_option("kernel", 1)
+    eng.run(1)
+
+
+@pytest.mark.parametrize("name,fn", tick_fixtures())
+def test_replay_matches_reference_snapshots(name, fn):
+    d = load_json(fn)
+    names, vals, rp, col = fixture_decl_csr(d)
+    tr = fu.Trace(rp, col, "collectall" if d["mode"] == "ca" else "pairwise", d["ticks"],
+                  d["order"])
+    rep = fu.Replay(tr, vals)
+    snaps = rep.run(d["ticks"], snapshot_ticks=range(d["ticks"]))
+    for t in range(d["ticks"]):
+        keys = d["snap_keys"][t]
+        assert [float(snaps[t][i]) for i in keys] == d["snap_vals"][t], (name, t)
+    last, flows, est = rep.state()
+    a = tr.arrays()
+    for i in range(tr.n):
+        assert list(flows[a["rowptr"][i]:a["rowptr"][i + 1]]) == d["flows"][i]
+        assert list(est[a["rowptr"][i]:a["rowptr"][i + 1]]) == d["estimates"][i]
+
+
+@pytest.mark.parametrize("mode", ["collectall", "pairwise"])
+def test_replay_rr64k_vs_c_oracle(mode):
+    """BASELINE config 3: pairwise on a 64K-node random regular graph (and collect-all)."""
+    g = fu.Graph.random_regular(65536, 8, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    tr = fu.Trace(g.rowptr, g.col, mode, 160, "rand:3")
+    a = tr.arrays()
+    rep = fu.Replay(tr, v)
+    snaps = rep.run(160, snapshot_ticks=[60, 120, 159])
+    last, flows, est = rep.state()
+    l_ref, f_ref, e_ref, s_ref = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"],
+                                                a["events"], a["out_ids"], tr.n_msgs,
+                                                [60, 120, 159])
+    assert np.array_equal(last, l_ref)
+    assert np.array_equal(flows, f_ref)
+    assert np.array_equal(est, e_ref)
+    for t in (60, 120, 159):
+        assert np.array_equal(snaps[t], s_ref[t])
+
+
+@pytest.mark.parametrize("mode,tag", [("ca", "fwd"), ("pw", "fwd"), ("ca", "rev"), ("pw", "rand7")])
+def test_engine_small_platform_watcher_lines(tmp_path, mode, tag):
+    """The drop-in Engine on the reference inputs prints the watcher's lines (CA:134-142)
+    with the reference's values at t = 10, 20, ..., 1000."""
+    d = load_json(f"tick_small_platform_{mode}_{tag}.json")
+    plat = tmp_path / "small_platform.xml"
+    dep = tmp_path / "actors.xml"
+    write_platform_xml(plat)
+    write_deployment_xml(dep, d["actors"])
+    order = d["order"]
+    e, res = fu.run_reference_main("collectall" if mode == "ca" else "pairwise", str(plat),
+                                   str(dep), 1000.0, 10.0, order=order, out=io.StringIO())
+    names = d["names"]
+    watch = [ln for ln in e.lines if ":watcher:" in ln and ("last_avg{" in ln or "value{" in ln)]
+    by_t = {}
+    for ln in watch:
+        t = float(ln.split()[1].rstrip("]"))
+        by_t.setdefault(t, []).append(ln.split("] ", 2)[2])
+    for t in range(10, 1001, 10):
+        la = {names[k]: v for k, v in zip(d["snap_keys"][t], d["snap_vals"][t])}
+        vd = {nm: float(a[1]) for nm, a in zip(names, d["actors"])}
+        want = [f"value{vd}"] + ([f"last_avg{la}"] if la else [])
+        assert by_t[float(t)] == want, t
+    assert np.max(np.abs(res["last_avg"] - 190 / 6)) / (190 / 6) < 1e-12
+
+
+def test_full_size_er1m_convergence_and_prefix_parity():
+    """BASELINE config 2 at full size: ER n=1e6 m=4e6. Bitwise vs the C oracle for 60 rounds,
+    then the 1000-round run converges to the per-component means (< 1e-9)."""
+    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    eng = fu.CollectAll(g, v)
+    eng.run(60)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 60, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    tgt, comp = fu.component_means(g.rowptr, g.col, v)
+    eng.set_targets(tgt)
+    tr = eng.run(940, err_every=10)
+    assert tr[-1] < 1e-9
+    assert np.all(np.diff(tr[5:]) <= 0) or tr[-1] < 1e-12  # settles monotonically

@@ -1,0 +1,103 @@
+"""The native tick-trace generator (fu_trace_build) against the reference runs.
+
+The fixtures hold the event log of the reference's own Peer objects driven tick by tick.
+The trace must reproduce that log event for event. Replaying the trace with the oracle's
+replay (C and Python) must reproduce every per-tick snapshot of global_values['last_avg']
+bitwise.
+"""
+import numpy as np
+import pytest
+
+import coracle
+import fu
+import oracle
+from conftest import fixture_decl_csr, load_json, tick_fixtures, trace_events_as_log
+
+
+@pytest.mark.parametrize("name,fn", tick_fixtures())
+def test_trace_matches_reference_event_log(name, fn):
+    d = load_json(fn)
+    names, vals, rp, col = fixture_decl_csr(d)
+    tr = fu.Trace(rp, col, "collectall" if d["mode"] == "ca" else "pairwise", d["ticks"],
+                  d["order"])
+    a = tr.arrays()
+    assert trace_events_as_log(a) == d["events"]
+    assert list(a["fires"]) == d["fires"]
+    # union rows in insertion order (declared, then first arrival: CA:94-95)
+    rows = [list(a["col"][a["rowptr"][i]:a["rowptr"][i + 1]]) for i in range(tr.n)]
+    assert rows == d["neighbors"]
+    # key order of global_values["last_avg"] = order of first average
+    assert tr.last_avg_order() == d["snap_keys"][-1]
+    assert tr.dynamic_additions == d["errors_logged"]
+
+
+@pytest.mark.parametrize("name,fn", tick_fixtures())
+def test_trace_replay_oracle_matches_snapshots(name, fn):
+    d = load_json(fn)
+    names, vals, rp, col = fixture_decl_csr(d)
+    tr = fu.Trace(rp, col, "collectall" if d["mode"] == "ca" else "pairwise", d["ticks"],
+                  d["order"])
+    a = tr.arrays()
+    ticks = list(range(d["ticks"]))
+    last, flow, est, snaps = coracle.replay(a["rowptr"], vals, a["tick_task_off"], a["tasks"],
+                                            a["events"], a["out_ids"], tr.n_msgs, ticks)
+    for t in ticks:
+        keys = d["snap_keys"][t]
+        assert [float(snaps[t][i]) for i in keys] == d["snap_vals"][t], (name, t)
+    # final flows per neighbour slot
+    for i in range(tr.n):
+        assert list(flow[a["rowptr"][i]:a["rowptr"][i + 1]]) == d["flows"][i]
+
+
+def test_trace_order_rand_is_deterministic():
+    rp = np.array([0, 2, 4, 6], dtype=np.int64)
+    col = np.array([1, 2, 0, 2, 0, 1], dtype=np.int32)
+    t1 = fu.Trace(rp, col, "pairwise", 200, "rand:5").arrays()
+    t2 = fu.Trace(rp, col, "pairwise", 200, "rand:5").arrays()
+    assert np.array_equal(t1["events"], t2["events"])
+    t3 = fu.Trace(rp, col, "pairwise", 200, "rand:6").arrays()
+    assert not np.array_equal(t1["tasks"], t3["tasks"])
+
+
+def test_trace_conflict_free_batches():
+    """One task per node per tick, and no message slot is written and read in one tick."""
+    g = fu.Graph.random_regular(512, 6, seed=3)
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", 150, "rand:1")
+    a = tr.arrays()
+    tto, tasks, ev, oids = a["tick_task_off"], a["tasks"], a["events"], a["out_ids"]
+    for t in range(tr.ticks):
+        tk = tasks[tto[t]:tto[t + 1]]
+        assert len(np.unique(tk[:, 0])) == len(tk)
+        reads, writes = set(), set()
+        for node, b, e in tk:
+            for p in range(b, e):
+                if ev[p, 0] == 0:
+                    reads.add(int(ev[p, 2]))
+                elif ev[p, 0] == 2:
+                    writes.add(int(ev[p, 3]))
+                else:
+                    writes.update(int(x) for x in oids[ev[p, 2]:ev[p, 2] + ev[p, 1]])
+        assert not (reads & writes), t
+
+
+def test_trace_pairwise_rr_oracles_agree():
+    """C and Python replays agree on a mid-size pairwise trace (RR n=256, d=8)."""
+    g = fu.Graph.random_regular(256, 8, seed=7)
+    v = fu.uniform_values(g.n, seed=3)
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", 300, "fwd")
+    a = tr.arrays()
+    l1, f1, e1, _ = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"], a["events"],
+                                   a["out_ids"], tr.n_msgs)
+    l2, f2, e2, _ = oracle.replay_trace(a["rowptr"], v, a["tick_task_off"], a["tasks"],
+                                        a["events"], a["out_ids"], tr.n_msgs)
+    assert np.array_equal(l1, l2) and np.array_equal(f1, f2) and np.array_equal(e1, e2)
+
+
+def test_trace_bad_inputs():
+    rp = np.array([0, 1, 2], dtype=np.int64)
+    with pytest.raises(fu.FuError):
+        fu.Trace(rp, np.array([0, 0], dtype=np.int32), "pairwise", 10)  # self-loop
+    with pytest.raises(fu.FuError):
+        fu.Trace(rp, np.array([1, 5], dtype=np.int32), "pairwise", 10)  # out of range
+    with pytest.raises(fu.FuError):
+        fu.Trace(rp, np.array([1, 0], dtype=np.int32), "pairwise", 10, "sideways")

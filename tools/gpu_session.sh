@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU session on the gpurun box: parity tests, smoke, bench, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a crash/timeout (rc not in {0,1}) ends the session.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOTDIR=$(pwd)
+OUT=$ROOTDIR/gpurun_out
+mkdir -p "$OUT"
+: > "$OUT/status.txt"
+STEPS="${STEPS:-pytest smoke bench prof}"
+step() {  # name limit cmd...
+  local name=$1 lim=$2; shift 2
+  echo "[$(date +%T)] start $name" >> "$OUT/status.txt"
+  timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "[$(date +%T)] $name rc=$rc" >> "$OUT/status.txt"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "fatal rc=$rc in $name; stopping"; tail -30 "$OUT/$name.log"; exit $rc; fi
+  return 0
+}
+for s in $STEPS; do
+  case $s in
+    pytest) step pytest 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} ;;
+    smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)   export TMPDIR=/tmp
+            step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOTDIR/bench.py" --steps 200 --no-conv --cpu-seconds 0 ${BENCH_ARGS:-} ;;
+    sweep)  step sweep 900 python tools/sweep.py ${SWEEP_ARGS:-} ;;
+    *) echo "unknown step $s" ;;
+  esac
+done
+tail -5 "$OUT/pytest.log" 2>/dev/null
+cat "$OUT/bench.log" 2>/dev/null | tail -3
+cat "$OUT/status.txt"
