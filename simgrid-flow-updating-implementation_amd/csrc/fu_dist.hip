@@ -179,6 +179,7 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, cons
     d->comm = nullptr;
     return bail(fail(FU_ERR_NCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
   }
+  if (int rc = fu_set_option(h, "kernel", 2)) return bail(rc);  // halo carries flows + estimates
   *out = h;
   return FU_OK;
   FU_TRY_END

@@ -279,6 +279,135 @@ __global__ __launch_bounds__(kBlock) void k_round_push(
   if (CHECK) block_max_to(eb, err);
 }
 
+// ------------------------------------------------------------------------------------
+// Variant 4: flow reconstruction ("recon"). Node j computed, in round r-1,
+//     f_{r-1}[j->i] = ((-f_{r-2}[i->j]) + a_{r-1}[j]) - a_{r-2}[i]        (CA:99, CA:117)
+// from three operands that node i also holds: its own previous flow f_{r-2}[i->j] (its
+// own row), its own estimate a_{r-2}[i], and j's estimate a_{r-1}[j]. So i recomputes the
+// reverse flow with the same IEEE operations on the same operands, and gets the same bits,
+// instead of gathering f_old[rev[e]] from a 64 MB array. Per edge, the only random access
+// left is a_{r-1}[col e] (8 B from an 8 MB array). Flows are updated in place: round r
+// reads f_{r-2} and writes f_r in the same rows, owned by the same block. Buffers:
+// F[r & 1], A[r % 3] (see launch_round). Round 1 reads f_{-1} = -0.0, a_{-1} = 0.0, which
+// reproduces round 0's (0.0 + a) - 0.0 exactly.
+// ------------------------------------------------------------------------------------
+__device__ inline double recon_fr(double f_own_old, double a_nb, double a_own_old2) {
+  const double f_rev = ((-f_own_old) + a_nb) - a_own_old2;  // j's f_{r-1}[j->i], bitwise
+  return -f_rev;                                            // CA:99 flows[j] = -msg.flow
+}
+
+template <typename T>
+__device__ inline T ld_stream(const T *p) {
+  return __builtin_nontemporal_load(p);
+}
+
+template <bool CHECK, bool NT>
+__global__ __launch_bounds__(kBlock) void k_round_recon(
+    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
+    const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
+    double *__restrict__ a_new, const double *__restrict__ target,
+    unsigned long long *__restrict__ err) {
+  __shared__ double s_x[kTileEdges];   // f_{r-2} on load, fr after phase B
+  __shared__ double s_er[kTileEdges];  // a_{r-1}[col e]
+  __shared__ unsigned char s_own[kTileEdges];
+  __shared__ int s_rp[kTileNodes + 1];
+  __shared__ double s_a[kTileNodes];
+  const int t = threadIdx.x;
+  const int2 tl = tiles[blockIdx.x];
+  unsigned long long eb = 0;
+
+  if (tl.y < 0) {
+    // ---------------- heavy node ----------------
+    const int i = tl.x;
+    const int b = rowptr[i], e = rowptr[i + 1];
+    const double own2 = a_prev2[i];
+    double S = 0.0, T = 0.0;
+    for (int c0 = b; c0 < e; c0 += kTileEdges) {
+      const int cn = min(kTileEdges, e - c0);
+      for (int q = t; q < cn; q += kBlock) {
+        const double er = a_prev[col[c0 + q]];
+        s_x[q] = recon_fr(F[c0 + q], er, own2);
+        s_er[q] = er;
+      }
+      __syncthreads();
+      if (t < 64) {
+        for (int q = 0; q < cn; ++q) {  // exact left-to-right chain, lane-uniform
+          S = S + s_x[q];
+          T = T + s_er[q];
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const double a = ((v[i] - S) + T) / (double)(e - b + 1);
+      s_a[0] = a;
+      a_new[i] = a;
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = s_a[0];
+    for (int k = b + t; k < e; k += kBlock) {
+      const double er = a_prev[col[k]];
+      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+
+  // ---------------- light tile ----------------
+  const int nb = tl.x, nn = tl.y - tl.x;
+  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
+  __syncthreads();
+  const int e0 = s_rp[0];
+  const int ne = s_rp[nn] - e0;
+  // phase A: coalesced own-row flows + neighbour-estimate gathers
+#pragma unroll 4
+  for (int q = t; q < ne; q += kBlock) {
+    if (NT) {
+      s_x[q] = ld_stream(F + e0 + q);
+      s_er[q] = a_prev[ld_stream(col + e0 + q)];
+    } else {
+      s_x[q] = F[e0 + q];
+      s_er[q] = a_prev[col[e0 + q]];
+    }
+  }
+  if (t < nn) {
+    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
+  }
+  __syncthreads();
+  // phase B: per node, reconstruct fr and sum in row order (CA:106-113)
+  if (t < nn) {
+    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
+    const double own2 = a_prev2[nb + t];
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double er = s_er[q];
+      const double fr = recon_fr(s_x[q], er, own2);
+      s_x[q] = fr;
+      S = S + fr;
+      T = T + er;
+    }
+    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
+    s_a[t] = a;
+    a_new[nb + t] = a;
+    if (CHECK) eb = err_bits(a, target[nb + t]);
+  }
+  __syncthreads();
+  // phase C: new flows, coalesced, in place (CA:117-118)
+  for (int q = t; q < ne; q += kBlock) {
+    const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
+    if (NT) __builtin_nontemporal_store(fnew, F + e0 + q);
+    else F[e0 + q] = fnew;
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
+__global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
+  long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (q < cnt) p[q] = val;
+}
+
 // round 0 for the push layout: message i->j = (a_i, a_i) stored at inbox[rev[e]]
 __global__ __launch_bounds__(kBlock) void k_round0_push(int n, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rev,
@@ -388,7 +517,7 @@ struct fu_handle {
   int *rowptr = nullptr, *col = nullptr, *rev = nullptr;
   double *v = nullptr;
   double *f[2] = {nullptr, nullptr};
-  double *a[2] = {nullptr, nullptr};
+  double *a[3] = {nullptr, nullptr, nullptr};  // a[2]: third estimate buffer (kernel 4)
   double2 *inbox[2] = {nullptr, nullptr};
   double *target = nullptr;
   unsigned long long *err = nullptr;
@@ -396,8 +525,9 @@ struct fu_handle {
   double *ftmp = nullptr;
   int cur = 0;
   int64_t rounds = 0;
-  int kernel = 2;
+  int kernel = 4;
   int hub_threshold = 64;
+  int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   std::vector<int64_t> h_rowptr;
   int2 *tiles = nullptr;
   int ntiles = 0;
@@ -443,6 +573,23 @@ int build_tiles(fu_handle *h) {
   return FU_OK;
 }
 
+// Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
+inline double *cur_a(fu_handle *h) {
+  if (h->kernel == 4) return h->a[(int)((h->rounds + 2) % 3)];
+  return h->a[h->cur];
+}
+inline double *cur_f(fu_handle *h) {
+  if (h->kernel == 4) return h->f[(int)((h->rounds + 1) & 1)];
+  return h->f[h->cur];
+}
+
+int ensure_a2(fu_handle *h) {
+  if (h->a[2]) return FU_OK;
+  if (int rc = dmalloc(&h->a[2], (size_t)h->n)) return rc;
+  HIP_TRY(hipMemset(h->a[2], 0, sizeof(double) * h->n));
+  return FU_OK;
+}
+
 int ensure_inbox(fu_handle *h) {
   if (h->inbox[0]) return FU_OK;
   for (int k = 0; k < 2; ++k)
@@ -459,7 +606,33 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 0)) return rc;
   }
-  if (h->rounds == 0) {
+  if (h->kernel == 4) {
+    const int64_t r = h->rounds;
+    if (r == 0) {
+      hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
+                         h->rowptr, h->v, h->f[0], h->a[0]);
+      if (h->E)  // f_{-1} = -0.0 so that round 1 reproduces (0.0 + a) - 0.0
+        hipLaunchKernelGGL(k_fill, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
+                           -0.0, h->f[1]);
+      HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->n, h->stream));  // a_{-1} = 0.0
+      if (check)
+        hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
+                           h->stream, h->n, h->a[0], h->target, err_slot);
+    } else {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+#define FU_RECON(C, N)                                                                      \
+  hipLaunchKernelGGL((k_round_recon<C, N>), dim3(h->ntiles), dim3(kBlock), 0, h->stream, h->tiles, \
+                     h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot)
+      if (check) {
+        if (h->nt) FU_RECON(true, true); else FU_RECON(true, false);
+      } else {
+        if (h->nt) FU_RECON(false, true); else FU_RECON(false, false);
+      }
+#undef FU_RECON
+    }
+  } else if (h->rounds == 0) {
     if (h->kernel == 3) {
       hipLaunchKernelGGL(k_round0_push, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
                          h->rowptr, h->rev, h->v, h->inbox[dst], h->a[dst]);
@@ -582,6 +755,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
   if ((rc = build_tiles(h))) return cleanup(rc);
+  if ((rc = ensure_a2(h))) return cleanup(rc);
   *out = h;
   return FU_OK;
   FU_TRY_END
@@ -618,11 +792,17 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..3");
+    if (value < 0 || value > 4) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..4");
     if (h->dist && value == 3) return fail(FU_ERR_ARG, "fu_set_option: kernel 3 (push) is single-GPU only");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
-    h->kernel = value == 0 ? 2 : (int)value;
+    h->kernel = value == 0 ? 4 : (int)value;
+    if (h->dist && h->kernel == 4) h->kernel = 2;  // the halo carries flows; see fu_dist.hip
     if (h->kernel == 3) return ensure_inbox(h);
+    if (h->kernel == 4) return ensure_a2(h);
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "nt")) {
+    h->nt = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "hub_threshold")) {
@@ -707,7 +887,7 @@ int fu_max_err(fu_handle *h, double *out) {
   if (int rc = set_device(h)) return rc;
   HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(unsigned long long), h->stream));
   hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream,
-                     h->n, h->a[h->cur], h->target, h->err);
+                     h->n, cur_a(h), h->target, h->err);
   HIP_TRY(hipGetLastError());
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 101)) return rc;  // all-reduce max of slot 0
@@ -722,7 +902,7 @@ int fu_max_err(fu_handle *h, double *out) {
 int fu_get_estimates(fu_handle *h, double *a_out) {
   if (!h || !a_out) return fail(FU_ERR_ARG, "fu_get_estimates: NULL argument");
   if (int rc = set_device(h)) return rc;
-  HIP_TRY(hipMemcpyAsync(a_out, h->a[h->cur], sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipMemcpyAsync(a_out, cur_a(h), sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FU_OK;
 }
@@ -731,7 +911,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   if (!h || (!f_out && h->E)) return fail(FU_ERR_ARG, "fu_get_flows: NULL argument");
   if (h->E == 0) return FU_OK;
   if (int rc = set_device(h)) return rc;
-  const double *src = h->f[h->cur];
+  const double *src = cur_f(h);
   if (h->kernel == 3 && h->rounds > 0) {
     if (!h->ftmp) {
       if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
@@ -764,7 +944,7 @@ int fu_destroy(fu_handle *h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->dist) fu__dist_free(h);
-  void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1],
+  void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
                   h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles};
   for (void *p : ptrs)
     if (p) hipFree(p);

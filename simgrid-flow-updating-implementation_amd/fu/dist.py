@@ -1,0 +1,209 @@
+"""Multi-GPU collect-all: contiguous node-range partitions with a per-round halo exchange.
+
+The reference simulates every node on one SimGrid host thread; its messages are mailbox
+transfers (Mailbox.put_async CA:124, get_async CA:74). Here a graph that needs more than
+one GPU (for memory or bandwidth) is split into contiguous node ranges, one per rank. A
+message between nodes on different ranks becomes a slot in a packed halo buffer, moved once
+per round by RCCL (fu_dist_create / fu_run_collectall; see fu_dist.hip).
+
+`partition(rowptr, col, rev, nranks, rank)` builds one rank's local CSR in the ghost-slot
+numbering that fu_dist_create expects:
+
+* local rows = global nodes [lo, hi); local edge k = global edge rowptr[lo] + k;
+* col[k] < n_local: a local node; col[k] = n_local + g: ghost estimate slot g. Ghosts are
+  grouped by owner rank, and sorted by global id inside each group;
+* rev[k] < e_local: a local edge; rev[k] = e_local + q: ghost flow slot q. Ghost flows are
+  grouped by owner rank, and sorted by the global index of the remote edge inside each group;
+* the send lists to rank p are this rank's edges into p's range (ascending global edge
+  index) and this rank's nodes adjacent to p's range (ascending id). That is exactly the
+  order in which p stores them, so no unpack pass is needed.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib as L
+
+
+def split_ranges(rowptr, nranks: int, balance: str = "edges") -> np.ndarray:
+    """Boundaries b[0..nranks] of contiguous node ranges, balanced by edges+nodes."""
+    rowptr = np.asarray(rowptr, dtype=np.int64)
+    n = len(rowptr) - 1
+    if balance == "nodes":
+        return np.array([(n * p) // nranks for p in range(nranks + 1)], dtype=np.int64)
+    work = rowptr + np.arange(n + 1, dtype=np.int64)  # edges + nodes prefix
+    targets = [(work[-1] * p) // nranks for p in range(nranks + 1)]
+    b = np.searchsorted(work, targets, side="left").astype(np.int64)
+    b[0], b[-1] = 0, n
+    return np.maximum.accumulate(b)
+
+
+@dataclass
+class Plan:
+    rank: int
+    nranks: int
+    lo: int
+    hi: int
+    rowptr: np.ndarray       # int64 [n_local+1]
+    col: np.ndarray          # int32 [e_local], ghost-extended numbering
+    rev: np.ndarray          # int32 [e_local], ghost-extended numbering
+    n_ghost_a: int
+    n_ghost_f: int
+    ghost_a_gid: np.ndarray  # global node id of each ghost estimate slot
+    ghost_f_gidx: np.ndarray  # global edge index of each ghost flow slot
+    send_f_off: np.ndarray
+    send_f_idx: np.ndarray
+    recv_f_off: np.ndarray
+    send_a_off: np.ndarray
+    send_a_idx: np.ndarray
+    recv_a_off: np.ndarray
+
+    @property
+    def n_local(self):
+        return self.hi - self.lo
+
+    @property
+    def e_local(self):
+        return int(self.rowptr[-1])
+
+
+def partition(rowptr, col, rev, nranks: int, rank: int, bounds=None) -> Plan:
+    rowptr = np.asarray(rowptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    rev = np.asarray(rev, dtype=np.int64)
+    b = split_ranges(rowptr, nranks) if bounds is None else np.asarray(bounds, dtype=np.int64)
+    lo, hi = int(b[rank]), int(b[rank + 1])
+    e0, e1 = int(rowptr[lo]), int(rowptr[hi])
+    n_local, e_local = hi - lo, e1 - e0
+    lcol = col[e0:e1]
+    lrev = rev[e0:e1]
+    owner_of_col = np.searchsorted(b, lcol, side="right") - 1
+    remote = (lcol < lo) | (lcol >= hi)
+
+    # ghost estimates: remote neighbours, grouped by owner (ascending id == grouped by owner,
+    # since ranges are contiguous and ordered)
+    ghost_a_gid = np.unique(lcol[remote])
+    owner_a = np.searchsorted(b, ghost_a_gid, side="right") - 1
+    recv_a_off = np.zeros(nranks + 1, dtype=np.int64)
+    np.add.at(recv_a_off, owner_a + 1, 1)
+    recv_a_off = np.cumsum(recv_a_off)
+    new_col = np.where(remote, 0, lcol - lo)
+    new_col[remote] = n_local + np.searchsorted(ghost_a_gid, lcol[remote])
+
+    # ghost flows: the reverse edges of cut edges, sorted by their global index (owner order
+    # follows, because edge ranges are contiguous per rank)
+    ghost_f_gidx = np.sort(lrev[remote])
+    recv_f_off = np.zeros(nranks + 1, dtype=np.int64)
+    np.add.at(recv_f_off, (np.searchsorted(b, ghost_f_gidx_owner_nodes(rowptr, ghost_f_gidx),
+                                           side="right") - 1) + 1, 1)
+    recv_f_off = np.cumsum(recv_f_off)
+    new_rev = np.where(remote, 0, lrev - e0)
+    new_rev[remote] = e_local + np.searchsorted(ghost_f_gidx, lrev[remote])
+
+    # send lists: my edges into p's range, ascending (== local index order)
+    send_f_idx = []
+    send_a_idx = []
+    send_f_off = [0]
+    send_a_off = [0]
+    src_local = np.repeat(np.arange(n_local, dtype=np.int64), np.diff(rowptr[lo:hi + 1]))
+    for p in range(nranks):
+        if p == rank:
+            send_f_off.append(send_f_off[-1])
+            send_a_off.append(send_a_off[-1])
+            continue
+        m = owner_of_col == p
+        ef = np.nonzero(m)[0]
+        na = np.unique(src_local[m])
+        send_f_idx.append(ef)
+        send_a_idx.append(na)
+        send_f_off.append(send_f_off[-1] + len(ef))
+        send_a_off.append(send_a_off[-1] + len(na))
+    cat = lambda xs: (np.concatenate(xs) if xs else np.zeros(0, dtype=np.int64))  # noqa: E731
+    return Plan(rank, nranks, lo, hi, rowptr[lo:hi + 1] - e0, new_col.astype(np.int32),
+                new_rev.astype(np.int32), len(ghost_a_gid), len(ghost_f_gidx), ghost_a_gid,
+                ghost_f_gidx, np.array(send_f_off, dtype=np.int64),
+                cat(send_f_idx).astype(np.int32), recv_f_off,
+                np.array(send_a_off, dtype=np.int64), cat(send_a_idx).astype(np.int32),
+                recv_a_off)
+
+
+def ghost_f_gidx_owner_nodes(rowptr, gidx):
+    """Source node of each global edge index."""
+    return np.searchsorted(rowptr, gidx, side="right") - 1
+
+
+def unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    L.call("fu_dist_unique_id", buf)
+    return bytes(buf)
+
+
+class DistCollectAll:
+    """One rank of a partitioned collect-all run (RCCL halo exchange every round)."""
+
+    def __init__(self, plan: Plan, values_local, uid: bytes, device: int = 0,
+                 kernel: str = "tile"):
+        from .engine import KERNELS
+
+        self.plan = plan
+        self.values = np.ascontiguousarray(values_local, dtype=np.float64)
+        if len(self.values) != plan.n_local:
+            raise ValueError("values_local must have n_local entries")
+        keep = [plan.rowptr, plan.col, plan.rev, plan.send_f_off, plan.send_f_idx,
+                plan.recv_f_off, plan.send_a_off, plan.send_a_idx, plan.recv_a_off]
+        self._keep = [np.ascontiguousarray(x) for x in keep]
+        (rp, c, r, sfo, sfi, rfo, sao, sai, rao) = self._keep
+        idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        out = L.vp()
+        L.call("fu_dist_create", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c), L.ptr(r),
+               L.ptr(self.values), plan.n_ghost_a, plan.n_ghost_f, plan.nranks, plan.rank,
+               L.ptr(sfo), L.ptr(sfi) if len(sfi) else None, L.ptr(rfo), L.ptr(sao),
+               L.ptr(sai) if len(sai) else None, L.ptr(rao), idbuf, int(device),
+               ctypes.byref(out))
+        self._h = out
+        self.n = plan.n_local
+        self.E = plan.e_local
+        k = KERNELS[kernel]
+        if k:
+            L.call("fu_set_option", self._h, b"kernel", k)
+
+    def run(self, rounds: int, err_every: int = 0):
+        if err_every > 0:
+            trace = np.empty(max(rounds // err_every, 1))
+            L.call("fu_run_collectall", self._h, int(rounds), int(err_every), L.ptr(trace))
+            return trace[:rounds // err_every]
+        L.call("fu_run_collectall", self._h, int(rounds), 0, None)
+        return None
+
+    def run_timed(self, rounds: int) -> float:
+        ms = L.f32()
+        L.call("fu_run_collectall_timed", self._h, int(rounds), ctypes.byref(ms))
+        return float(ms.value)
+
+    def set_targets(self, target_local):
+        self._target = np.ascontiguousarray(target_local, dtype=np.float64)
+        L.call("fu_set_targets", self._h, L.ptr(self._target))
+
+    def estimates(self):
+        a = np.empty(self.n)
+        L.call("fu_get_estimates", self._h, L.ptr(a))
+        return a
+
+    def flows(self):
+        f = np.empty(max(self.E, 1))
+        L.call("fu_get_flows", self._h, L.ptr(f))
+        return f[:self.E]
+
+    def synchronize(self):
+        L.call("fu_synchronize", self._h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            L.lib.fu_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        self.close()

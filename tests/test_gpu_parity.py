@@ -15,7 +15,7 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["thread", "tile", "push"]
+KERNELS = ["thread", "tile", "push", "recon"]
 
 
 def _check_fixture(meta, kernel, hub_threshold=None):
@@ -38,7 +38,7 @@ def test_ca_sync_fixture_bitwise(name, meta, kernel):
     _check_fixture(meta, kernel)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon"])
 @pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
 def test_ca_sync_fixture_heavy_path(name, kernel):
     """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
@@ -57,7 +57,7 @@ def test_er_vs_c_oracle_bitwise(kernel):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon"])
 def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.rmat(15, 16, seed=2)
     assert g.max_deg > 2048  # exercises chunked heavy tiles

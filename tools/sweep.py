@@ -13,7 +13,9 @@ specs = sys.argv[1:] or ["er:n=1000000,m=4000000"]
 for spec in specs:
     g = fu.Graph.from_spec(spec, seed=1)
     v = fu.uniform_values(g.n, seed=0)
-    engs = {k: fu.CollectAll(g, v, kernel=k) for k in ("thread", "tile", "push")}
+    engs = {k: fu.CollectAll(g, v, kernel=k) for k in ("thread", "tile", "push", "recon")}
+    engs["recon_nt"] = fu.CollectAll(g, v, kernel="recon")
+    engs["recon_nt"].set_option("nt", 1)
     for e in engs.values():
         e.run(10)
     res = {k: [] for k in engs}
