@@ -301,7 +301,10 @@ __device__ inline T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);
 }
 
-template <bool CHECK, bool NT>
+// DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
+//   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
+//   2 = no flow load/store (prices the flow stream).
+template <bool CHECK, bool NT, int DIAG = 0>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
@@ -364,12 +367,15 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   // phase A: coalesced own-row flows + neighbour-estimate gathers
 #pragma unroll 4
   for (int q = t; q < ne; q += kBlock) {
+    const int gi = DIAG == 1 ? (e0 + q) % (int)(ne + 1) : 0;
     if (NT) {
-      s_x[q] = ld_stream(F + e0 + q);
-      s_er[q] = a_prev[ld_stream(col + e0 + q)];
+      s_x[q] = DIAG == 2 ? 0.0 : ld_stream(F + e0 + q);
+      const int c = ld_stream(col + e0 + q);
+      s_er[q] = a_prev[DIAG == 1 ? (c & 0) + nb + gi % (nn + 1) : c];
     } else {
-      s_x[q] = F[e0 + q];
-      s_er[q] = a_prev[col[e0 + q]];
+      s_x[q] = DIAG == 2 ? 0.0 : F[e0 + q];
+      const int c = col[e0 + q];
+      s_er[q] = a_prev[DIAG == 1 ? (c & 0) + nb + gi % (nn + 1) : c];
     }
   }
   if (t < nn) {
@@ -397,8 +403,13 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   // phase C: new flows, coalesced, in place (CA:117-118)
   for (int q = t; q < ne; q += kBlock) {
     const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
-    if (NT) __builtin_nontemporal_store(fnew, F + e0 + q);
-    else F[e0 + q] = fnew;
+    if (DIAG == 2) {
+      if (fnew == 12345.678) F[e0 + q] = fnew;  // keep the value live, store ~never
+    } else if (NT) {
+      __builtin_nontemporal_store(fnew, F + e0 + q);
+    } else {
+      F[e0 + q] = fnew;
+    }
   }
   if (CHECK) block_max_to(eb, err);
 }
@@ -528,6 +539,7 @@ struct fu_handle {
   int kernel = 4;
   int hub_threshold = 64;
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
+  int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
   std::vector<int64_t> h_rowptr;
   int2 *tiles = nullptr;
   int ntiles = 0;
@@ -622,13 +634,15 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
-#define FU_RECON(C, N)                                                                      \
-  hipLaunchKernelGGL((k_round_recon<C, N>), dim3(h->ntiles), dim3(kBlock), 0, h->stream, h->tiles, \
+#define FU_RECON(C, N, D)                                                                   \
+  hipLaunchKernelGGL((k_round_recon<C, N, D>), dim3(h->ntiles), dim3(kBlock), 0, h->stream, h->tiles, \
                      h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot)
-      if (check) {
-        if (h->nt) FU_RECON(true, true); else FU_RECON(true, false);
+      if (h->diag == 1) FU_RECON(false, false, 1);
+      else if (h->diag == 2) FU_RECON(false, false, 2);
+      else if (check) {
+        if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
       } else {
-        if (h->nt) FU_RECON(false, true); else FU_RECON(false, false);
+        if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
       }
 #undef FU_RECON
     }
@@ -799,6 +813,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     if (h->dist && h->kernel == 4) h->kernel = 2;  // the halo carries flows; see fu_dist.hip
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4) return ensure_a2(h);
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "diag")) {
+    h->diag = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "nt")) {

@@ -16,8 +16,12 @@ for spec in specs:
     engs = {k: fu.CollectAll(g, v, kernel=k) for k in ("thread", "tile", "push", "recon")}
     engs["recon_nt"] = fu.CollectAll(g, v, kernel="recon")
     engs["recon_nt"].set_option("nt", 1)
-    for e in engs.values():
+    for d in (1, 2):  # timing-only ablations (wrong results): price the gather / the flows
+        engs[f"recon_diag{d}"] = fu.CollectAll(g, v, kernel="recon")
+    for k, e in engs.items():
         e.run(10)
+        if k.startswith("recon_diag"):
+            e.set_option("diag", int(k[-1]))
     res = {k: [] for k in engs}
     for rep in range(5):
         for k, e in engs.items():
