@@ -113,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tpn(
 // ------------------------------------------------------------------------------------
 template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void k_round_tile(
-    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const int *__restrict__ rev, const double *__restrict__ v,
     const double *__restrict__ f_old, const double *__restrict__ a_old,
     double *__restrict__ f_new, double *__restrict__ a_new,
@@ -124,7 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tile(
   __shared__ int s_rp[kTileNodes + 1];
   __shared__ double s_a[kTileNodes];
   const int t = threadIdx.x;
-  const int2 tl = tiles[blockIdx.x];
+  const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
 
   if (tl.y < 0) {
@@ -201,7 +201,7 @@ __global__ __launch_bounds__(kBlock) void k_round_tile(
 // ------------------------------------------------------------------------------------
 template <bool CHECK>
 __global__ __launch_bounds__(kBlock) void k_round_push(
-    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ rev, const double *__restrict__ v,
     const double2 *__restrict__ in_old, double2 *__restrict__ in_new,
     double *__restrict__ a_new, const double *__restrict__ target,
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(kBlock) void k_round_push(
   __shared__ int s_rp[kTileNodes + 1];
   __shared__ double s_a[kTileNodes];
   const int t = threadIdx.x;
-  const int2 tl = tiles[blockIdx.x];
+  const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
 
   if (tl.y < 0) {
@@ -304,20 +304,21 @@ __device__ inline T ld_stream(const T *p) {
 // DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
 //   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
 //   2 = no flow load/store (prices the flow stream).
-template <bool CHECK, bool NT, int DIAG = 0>
+template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
-    const int2 *__restrict__ tiles, const int *__restrict__ rowptr,
+    const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
     const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
     unsigned long long *__restrict__ err) {
-  __shared__ double s_x[kTileEdges];   // f_{r-2} on load, fr after phase B
-  __shared__ double s_er[kTileEdges];  // a_{r-1}[col e]
-  __shared__ unsigned char s_own[kTileEdges];
-  __shared__ int s_rp[kTileNodes + 1];
-  __shared__ double s_a[kTileNodes];
+  static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
+  __shared__ double s_x[TE];   // f_{r-2} on load, fr after phase B
+  __shared__ double s_er[TE];  // a_{r-1}[col e]
+  __shared__ unsigned char s_own[TE];
+  __shared__ int s_rp[TN + 1];
+  __shared__ double s_a[TN];
   const int t = threadIdx.x;
-  const int2 tl = tiles[blockIdx.x];
+  const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
 
   if (tl.y < 0) {
@@ -326,8 +327,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int b = rowptr[i], e = rowptr[i + 1];
     const double own2 = a_prev2[i];
     double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += kTileEdges) {
-      const int cn = min(kTileEdges, e - c0);
+    for (int c0 = b; c0 < e; c0 += TE) {
+      const int cn = min(TE, e - c0);
       for (int q = t; q < cn; q += kBlock) {
         const double er = a_prev[col[c0 + q]];
         s_x[q] = recon_fr(F[c0 + q], er, own2);
@@ -359,56 +360,83 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   }
 
   // ---------------- light tile ----------------
+  // Every global load of the tile is issued up front with no dependence on an earlier load
+  // except the a_{r-1}[col] gathers (one hop): 2 serial memory latencies per tile.
   const int nb = tl.x, nn = tl.y - tl.x;
-  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
-  __syncthreads();
-  const int e0 = s_rp[0];
-  const int ne = s_rp[nn] - e0;
-  // phase A: coalesced own-row flows + neighbour-estimate gathers
-#pragma unroll 4
-  for (int q = t; q < ne; q += kBlock) {
-    const int gi = DIAG == 1 ? (e0 + q) % (int)(ne + 1) : 0;
-    if (NT) {
-      s_x[q] = DIAG == 2 ? 0.0 : ld_stream(F + e0 + q);
-      const int c = ld_stream(col + e0 + q);
-      s_er[q] = a_prev[DIAG == 1 ? (c & 0) + nb + gi % (nn + 1) : c];
-    } else {
-      s_x[q] = DIAG == 2 ? 0.0 : F[e0 + q];
-      const int c = col[e0 + q];
-      s_er[q] = a_prev[DIAG == 1 ? (c & 0) + nb + gi % (nn + 1) : c];
+  const int e0 = tl.z, ne = tl.w - tl.z;
+  constexpr int kPer = TE / kBlock;
+  int c[kPer];
+  double x[kPer], g[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    c[k] = 0;
+    x[k] = 0.0;
+    if (q < ne) {
+      if (NT) {
+        c[k] = ld_stream(col + e0 + q);
+        x[k] = DIAG == 2 ? 0.0 : ld_stream(F + e0 + q);
+      } else {
+        c[k] = col[e0 + q];
+        x[k] = DIAG == 2 ? 0.0 : F[e0 + q];
+      }
     }
   }
-  if (t < nn) {
-    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
+  const int rp = t <= nn ? rowptr[nb + t] : 0;
+  int rp_last = 0;
+  if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
+  const double vv = t < nn ? v[nb + t] : 0.0;
+  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    g[k] = 0.0;
+    if (q < ne) g[k] = a_prev[DIAG == 1 ? nb + (q % (nn + 1)) : c[k]];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) {
+      s_x[q] = x[k];
+      s_er[q] = g[k];
+    }
+  }
+  if (t <= nn) s_rp[t] = rp;
+  if constexpr (TN == kBlock) {
+    if (t == 0 && nn == kBlock) s_rp[kBlock] = rp_last;
   }
   __syncthreads();
   // phase B: per node, reconstruct fr and sum in row order (CA:106-113)
   if (t < nn) {
     const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
-    const double own2 = a_prev2[nb + t];
     double S = 0.0, T = 0.0;
     for (int q = qb; q < qe; ++q) {
       const double er = s_er[q];
       const double fr = recon_fr(s_x[q], er, own2);
       s_x[q] = fr;
+      s_own[q] = (unsigned char)t;
       S = S + fr;
       T = T + er;
     }
-    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
+    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
     a_new[nb + t] = a;
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
   __syncthreads();
   // phase C: new flows, coalesced, in place (CA:117-118)
-  for (int q = t; q < ne; q += kBlock) {
-    const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
-    if (DIAG == 2) {
-      if (fnew == 12345.678) F[e0 + q] = fnew;  // keep the value live, store ~never
-    } else if (NT) {
-      __builtin_nontemporal_store(fnew, F + e0 + q);
-    } else {
-      F[e0 + q] = fnew;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) {
+      const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
+      if (DIAG == 2) {
+        if (fnew == 12345.678) F[e0 + q] = fnew;  // keep the value live, store ~never
+      } else if (NT) {
+        __builtin_nontemporal_store(fnew, F + e0 + q);
+      } else {
+        F[e0 + q] = fnew;
+      }
     }
   }
   if (CHECK) block_max_to(eb, err);
@@ -541,8 +569,12 @@ struct fu_handle {
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
   std::vector<int64_t> h_rowptr;
-  int2 *tiles = nullptr;
+  int4 *tiles = nullptr;  // 2048-edge tiles (kernels 2, 3)
   int ntiles = 0;
+  int4 *tiles_r = nullptr;  // kernel 4 tiles (geometry: tile_edges)
+  int ntiles_r = 0;
+  int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
+  int tile_nodes = 0;
   bool has_target = false;
   // multi-GPU (fu_dist.hip)
   void *dist = nullptr;
@@ -553,36 +585,42 @@ extern "C" void fu__dist_free(fu_handle *h);
 
 namespace {
 
-int build_tiles(fu_handle *h) {
-  std::vector<int2> heavy, light;
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count) {
+  std::vector<int4> heavy, light;
   const int32_t n = h->n;
   int32_t i = 0;
   while (i < n) {
     int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    if (d > h->hub_threshold || d > kTileEdges) {
-      heavy.push_back(make_int2(i, -1));
+    if (d > h->hub_threshold || d > te) {
+      heavy.push_back(make_int4(i, -1, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
       ++i;
       continue;
     }
     int32_t b = i;
     int64_t eb = h->h_rowptr[b];
-    while (i < n && i - b < kTileNodes) {
+    while (i < n && i - b < tn) {
       int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
-      if (di > h->hub_threshold || di > kTileEdges) break;
-      if (h->h_rowptr[i + 1] - eb > kTileEdges) break;
+      if (di > h->hub_threshold || di > te) break;
+      if (h->h_rowptr[i + 1] - eb > te) break;
       ++i;
     }
-    light.push_back(make_int2(b, i));
+    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
   // heavy tiles first so their long sequential chains start early
-  std::vector<int2> all(heavy);
+  std::vector<int4> all(heavy);
   all.insert(all.end(), light.begin(), light.end());
-  if (h->tiles) hipFree(h->tiles);
-  h->tiles = nullptr;
-  h->ntiles = (int)all.size();
-  if (int rc = dmalloc(&h->tiles, all.size())) return rc;
-  HIP_TRY(hipMemcpy(h->tiles, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+  if (*dst) hipFree(*dst);
+  *dst = nullptr;
+  *count = (int)all.size();
+  if (int rc = dmalloc(dst, all.size())) return rc;
+  HIP_TRY(hipMemcpy(*dst, all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
   return FU_OK;
+}
+
+int build_tiles(fu_handle *h) {
+  if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
+  const int te = h->tile_edges, tn = te == 2048 ? 256 : te == 1024 ? (h->tile_nodes ? h->tile_nodes : 128) : 64;
+  return build_tiles_geom(h, te, tn, &h->tiles_r, &h->ntiles_r);
 }
 
 // Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
@@ -634,9 +672,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
+#define FU_RECON_G(C, N, D, TE, TN)                                                         \
+  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_r), dim3(kBlock), 0, h->stream, \
+                     h->tiles_r, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot)
 #define FU_RECON(C, N, D)                                                                   \
-  hipLaunchKernelGGL((k_round_recon<C, N, D>), dim3(h->ntiles), dim3(kBlock), 0, h->stream, h->tiles, \
-                     h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot)
+  do {                                                                                      \
+    if (h->tile_edges == 2048) FU_RECON_G(C, N, D, 2048, 256);                              \
+    else if (h->tile_edges == 1024 && h->tile_nodes == 256) FU_RECON_G(C, N, D, 1024, 256); \
+    else if (h->tile_edges == 1024) FU_RECON_G(C, N, D, 1024, 128);                         \
+    else FU_RECON_G(C, N, D, 512, 64);                                                      \
+  } while (0)
       if (h->diag == 1) FU_RECON(false, false, 1);
       else if (h->diag == 2) FU_RECON(false, false, 2);
       else if (check) {
@@ -645,6 +690,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
       }
 #undef FU_RECON
+#undef FU_RECON_G
     }
   } else if (h->rounds == 0) {
     if (h->kernel == 3) {
@@ -823,6 +869,16 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->nt = value != 0;
     return FU_OK;
   }
+  if (!std::strcmp(key, "tile_edges")) {
+    if (value != 2048 && value != 1024 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: tile_edges must be 2048, 1024 or 512");
+    h->tile_edges = (int)value;
+    return build_tiles(h);
+  }
+  if (!std::strcmp(key, "tile_nodes")) {
+    if (value != 0 && value != 128 && value != 256) return fail(FU_ERR_ARG, "fu_set_option: tile_nodes must be 0, 128 or 256");
+    h->tile_nodes = (int)value;
+    return build_tiles(h);
+  }
   if (!std::strcmp(key, "hub_threshold")) {
     if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: hub_threshold must be >= 1");
     h->hub_threshold = (int)std::min<int64_t>(value, kTileEdges);
@@ -963,7 +1019,7 @@ int fu_destroy(fu_handle *h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->dist) fu__dist_free(h);
   void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
-                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles};
+                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_r};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

@@ -1,6 +1,10 @@
 #!/usr/bin/env python3
-"""Kernel-variant sweep on the headline workload (ER-1M): device time per round for each
-round-kernel variant, interleaved in one process (cdna guide §5.4 rule 24)."""
+"""Kernel-variant sweep: device time per round for each round-kernel variant, interleaved
+in one process (cdna guide §5.4 rule 24). Variants named diag* are timing-only ablations
+with WRONG results (they price one memory stream each).
+
+    python tools/sweep.py [spec ...] [--variants a,b,c]
+"""
 import json
 import os
 import sys
@@ -9,19 +13,39 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "simgrid-flow-updating-implementation_amd"))
 import fu  # noqa: E402
 
-specs = sys.argv[1:] or ["er:n=1000000,m=4000000"]
+VARIANTS = {
+    "thread": ("thread", {}),
+    "tile": ("tile", {}),
+    "push": ("push", {}),
+    "recon": ("recon", {}),
+    "recon_nt": ("recon", {"nt": 1}),
+    "recon_1024": ("recon", {"tile_edges": 1024}),
+    "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
+    "recon_1024_nt": ("recon", {"tile_edges": 1024, "nt": 1}),
+    "recon_512": ("recon", {"tile_edges": 512}),
+    "diag1_gather_free": ("recon", {"diag": 1}),
+    "diag2_flow_free": ("recon", {"diag": 2}),
+    "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
+}
+
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+opts = [a for a in sys.argv[1:] if a.startswith("--variants=")]
+names = opts[0].split("=", 1)[1].split(",") if opts else list(VARIANTS)
+specs = args or ["er:n=1000000,m=4000000"]
 for spec in specs:
     g = fu.Graph.from_spec(spec, seed=1)
     v = fu.uniform_values(g.n, seed=0)
-    engs = {k: fu.CollectAll(g, v, kernel=k) for k in ("thread", "tile", "push", "recon")}
-    engs["recon_nt"] = fu.CollectAll(g, v, kernel="recon")
-    engs["recon_nt"].set_option("nt", 1)
-    for d in (1, 2):  # timing-only ablations (wrong results): price the gather / the flows
-        engs[f"recon_diag{d}"] = fu.CollectAll(g, v, kernel="recon")
-    for k, e in engs.items():
+    engs = {}
+    for nm in names:
+        kern, o = VARIANTS[nm]
+        e = fu.CollectAll(g, v, kernel=kern)
+        for k, val in o.items():
+            if k != "diag":
+                e.set_option(k, val)
         e.run(10)
-        if k.startswith("recon_diag"):
-            e.set_option("diag", int(k[-1]))
+        if "diag" in o:
+            e.set_option("diag", o["diag"])
+        engs[nm] = e
     res = {k: [] for k in engs}
     for rep in range(5):
         for k, e in engs.items():
