@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20, help="untimed rounds first")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--m", type=int, default=4_000_000)
+    ap.add_argument("--workload", default="er", choices=["er", "rgg", "rmat", "rr"],
+                    help="er = the headline ER-1M (default); others are exploratory: rgg "
+                         "(--n nodes, avg deg 8), rmat (scale = --n, edge factor 16), rr (d = 8)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
@@ -79,7 +82,18 @@ def main():
         return float(t.item())
 
     t_gen = time.perf_counter()
-    g = fu.Graph.erdos_renyi(args.n, args.m, seed=1 + rank)
+    if args.workload == "er":
+        g = fu.Graph.erdos_renyi(args.n, args.m, seed=1 + rank)
+        wl = f"er:n={args.n},m={args.m} collect-all generation-synchronous rounds"
+    elif args.workload == "rgg":
+        g = fu.Graph.random_geometric(args.n, avg_deg=8.0, seed=1 + rank)
+        wl = f"rgg:n={args.n},deg=8 collect-all generation-synchronous rounds"
+    elif args.workload == "rmat":
+        g = fu.Graph.rmat(args.n, 16, seed=1 + rank)
+        wl = f"rmat:scale={args.n},ef=16 collect-all generation-synchronous rounds"
+    else:
+        g = fu.Graph.random_regular(args.n, 8, seed=1 + rank)
+        wl = f"rr:n={args.n},d=8 collect-all generation-synchronous rounds"
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
@@ -143,7 +157,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (seeded ER graph, U[0,100) values)",
             "config": {
-                "workload": "er:n=1000000,m=4000000 collect-all generation-synchronous rounds",
+                "workload": wl,
                 "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
                 "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel,
                 "parallelism": "independent graph per GPU" if world > 1 else "single GPU",

@@ -11,6 +11,10 @@
 // slot order, so no unpack pass is needed. The round kernels are the single-GPU ones: they
 // index the extended arrays and do not know about ranks.
 //
+// With kernel 4 (flow reconstruction, the default) a node rebuilds its neighbours' flows
+// from their estimates, so the halo carries only the boundary estimates (8 B per boundary
+// node per neighbouring part) and the ghost flow slots are unused.
+//
 // The convergence check all-reduces the per-rank max |a - target| with ncclMax on the
 // uint64 bit patterns (ordered like non-negative doubles).
 #include <hip/hip_runtime.h>
@@ -60,6 +64,9 @@ extern "C" double *fu__handle_a(fu_handle *h, int which);
 extern "C" int fu__handle_cur(fu_handle *h);
 extern "C" unsigned long long *fu__handle_err(fu_handle *h);
 extern "C" int fu__handle_device(fu_handle *h);
+extern "C" double *fu__handle_cur_a(fu_handle *h);
+extern "C" double *fu__handle_cur_f(fu_handle *h);
+extern "C" int fu__handle_kernel(fu_handle *h);
 
 #define NCCL_TRY(expr)                                                                     \
   do {                                                                                     \
@@ -91,10 +98,11 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
     NCCL_TRY(ncclAllReduce(err, err, (size_t)k, ncclUint64, ncclMax, d->comm, s));
     return FU_OK;
   }
-  const int cur = fu__handle_cur(h);
-  double *f = fu__handle_f(h, cur);
-  double *a = fu__handle_a(h, cur);
-  if (d->n_send_f > 0) {
+  // kernel 4 (flow reconstruction) needs only the neighbours' estimates: no ghost flows
+  const bool flows = fu__handle_kernel(h) != 4;
+  double *f = fu__handle_cur_f(h);
+  double *a = fu__handle_cur_a(h);
+  if (flows && d->n_send_f > 0) {
     hipLaunchKernelGGL(k_pack, dim3((unsigned)((d->n_send_f + 255) / 256)), dim3(256), 0, s,
                        (long long)d->n_send_f, d->send_f_idx, f, d->sbuf_f);
   }
@@ -107,8 +115,8 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
   NCCL_TRY(ncclGroupStart());
   for (int p = 0; p < d->nranks; ++p) {
     if (p == d->rank) continue;
-    const int64_t sf = d->send_f_off[p + 1] - d->send_f_off[p];
-    const int64_t rf = d->recv_f_off[p + 1] - d->recv_f_off[p];
+    const int64_t sf = flows ? d->send_f_off[p + 1] - d->send_f_off[p] : 0;
+    const int64_t rf = flows ? d->recv_f_off[p + 1] - d->recv_f_off[p] : 0;
     const int64_t sa = d->send_a_off[p + 1] - d->send_a_off[p];
     const int64_t ra = d->recv_a_off[p + 1] - d->recv_a_off[p];
     if (sf) NCCL_TRY(ncclSend(d->sbuf_f + d->send_f_off[p], (size_t)sf, ncclDouble, p, d->comm, s));
@@ -179,7 +187,7 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, cons
     d->comm = nullptr;
     return bail(fail(FU_ERR_NCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
   }
-  if (int rc = fu_set_option(h, "kernel", 2)) return bail(rc);  // halo carries flows + estimates
+  if (int rc = fu_set_option(h, "kernel", 4)) return bail(rc);  // halo: boundary estimates only
   *out = h;
   return FU_OK;
   FU_TRY_END

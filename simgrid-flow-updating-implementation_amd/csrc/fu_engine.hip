@@ -552,6 +552,7 @@ struct fu_handle {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   int32_t n = 0;
   int64_t E = 0;
+  int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
   int32_t max_deg = 0;
   int *rowptr = nullptr, *col = nullptr, *rev = nullptr;
   double *v = nullptr;
@@ -635,8 +636,8 @@ inline double *cur_f(fu_handle *h) {
 
 int ensure_a2(fu_handle *h) {
   if (h->a[2]) return FU_OK;
-  if (int rc = dmalloc(&h->a[2], (size_t)h->n)) return rc;
-  HIP_TRY(hipMemset(h->a[2], 0, sizeof(double) * h->n));
+  if (int rc = dmalloc(&h->a[2], (size_t)h->na)) return rc;
+  HIP_TRY(hipMemset(h->a[2], 0, sizeof(double) * h->na));
   return FU_OK;
 }
 
@@ -664,7 +665,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (h->E)  // f_{-1} = -0.0 so that round 1 reproduces (0.0 + a) - 0.0
         hipLaunchKernelGGL(k_fill, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
                            -0.0, h->f[1]);
-      HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->n, h->stream));  // a_{-1} = 0.0
+      HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
       if (check)
         hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
                            h->stream, h->n, h->a[0], h->target, err_slot);
@@ -787,6 +788,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   h->max_deg = md;
   const int64_t fe = e + f_extra;
   const int32_t na = n + a_extra;
+  h->na = na;
   for (int64_t k = 0; k < e; ++k) {
     if (col[k] < 0 || col[k] >= na || rev[k] < 0 || rev[k] >= fe) {
       delete h;
@@ -853,10 +855,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
     if (value < 0 || value > 4) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..4");
-    if (h->dist && value == 3) return fail(FU_ERR_ARG, "fu_set_option: kernel 3 (push) is single-GPU only");
+    if (h->dist && value != 0 && value != 2 && value != 4)
+      return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     h->kernel = value == 0 ? 4 : (int)value;
-    if (h->dist && h->kernel == 4) h->kernel = 2;  // the halo carries flows; see fu_dist.hip
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4) return ensure_a2(h);
     return FU_OK;
@@ -1218,4 +1220,7 @@ double *fu__handle_a(fu_handle *h, int which) { return h->a[which]; }
 int fu__handle_cur(fu_handle *h) { return h->cur; }
 unsigned long long *fu__handle_err(fu_handle *h) { return h->err; }
 int fu__handle_device(fu_handle *h) { return h->device; }
+double *fu__handle_cur_a(fu_handle *h) { return cur_a(h); }
+double *fu__handle_cur_f(fu_handle *h) { return cur_f(h); }
+int fu__handle_kernel(fu_handle *h) { return h->kernel; }
 }

@@ -1,0 +1,162 @@
+"""Multi-rank partition + halo plan (fu.dist.partition), exercised on the CPU with
+torch.distributed/gloo at world_size 2 and 3.
+
+Each rank runs the collect-all rounds on its local CSR in the ghost-slot numbering that
+fu_dist_create consumes, and exchanges the halo exactly as fu_dist.hip does: it packs
+send_*_idx in order and receives into the contiguous ghost ranges recv_*_off. The gathered
+per-node estimates and flows must equal the single-process oracle bitwise, for both halo
+contents: pull (ghost flows + ghost estimates) and recon (ghost estimates only). Only the
+transport (RCCL instead of gloo) and the kernels differ on the GPU.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import oracle
+from fu.dist import partition, split_ranges
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rows(rowptr, fr, er, v):
+    """Sequential row sums (CA:106-113) on per-edge fr/er; returns (a, f_new)."""
+    n = len(rowptr) - 1
+    a = np.empty(n)
+    f = np.empty(len(fr))
+    for i in range(n):
+        b, e = rowptr[i], rowptr[i + 1]
+        S = 0.0
+        T = 0.0
+        for k in range(b, e):
+            S = S + fr[k]
+            T = T + er[k]
+        a[i] = ((v[i] - S) + T) / (e - b + 1)
+        for k in range(b, e):
+            f[k] = (fr[k] + a[i]) - er[k]
+    return a, f
+
+
+def _exchange(plan, src_local, ghost_out, send_off, send_idx, recv_off):
+    """Pack send_idx from src_local per peer, receive into ghost_out[recv_off[p]:...]."""
+    reqs = []
+    for p in range(plan.nranks):
+        if p == plan.rank:
+            continue
+        s = torch.from_numpy(np.ascontiguousarray(src_local[send_idx[send_off[p]:send_off[p + 1]]]))
+        r = torch.empty(int(recv_off[p + 1] - recv_off[p]), dtype=torch.float64)
+        if len(s):
+            reqs.append(dist.isend(s, p))
+        if len(r):
+            reqs.append((dist.irecv(r, p), r, p))
+    for q in reqs:
+        if isinstance(q, tuple):
+            q[0].wait()
+            ghost_out[recv_off[q[2]]:recv_off[q[2] + 1]] = q[1].numpy()
+        else:
+            q.wait()
+
+
+def _worker(rank, world, port, rowptr, col, rev, v, rounds, mode, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    plan = partition(rowptr, col, rev, world, rank)
+    nl, el = plan.n_local, plan.e_local
+    rp = plan.rowptr
+    vl = v[plan.lo:plan.hi]
+    deg = np.diff(rp)
+    src = np.repeat(np.arange(nl), deg)
+    # round 0 (CA:87-91)
+    a = ((vl - 0.0) + 0.0) / (deg + 1)
+    f = (0.0 + a[src]) - 0.0
+    a_ext = np.zeros(nl + plan.n_ghost_a)
+    f_ext = np.zeros(el + plan.n_ghost_f)
+    a_prev2 = np.zeros(nl)  # a_{r-2}; a_{-1} = 0.0
+    F = np.full(el, -0.0)   # recon: f_{r-2}; f_{-1} = -0.0
+    hist_f = [F, f.copy()]
+    for r in range(1, rounds):
+        a_ext[:nl] = a
+        f_ext[:el] = f
+        _exchange(plan, a, a_ext[nl:], plan.send_a_off, plan.send_a_idx, plan.recv_a_off)
+        if mode == "pull":
+            _exchange(plan, f, f_ext[el:], plan.send_f_off, plan.send_f_idx, plan.recv_f_off)
+            fr = -f_ext[plan.rev]
+            er = a_ext[plan.col]
+        else:  # recon: rebuild -f_{r-1}[j->i] from f_{r-2}[i->j], a_{r-1}[j], a_{r-2}[i]
+            er = a_ext[plan.col]
+            fr = -(((-hist_f[0]) + er) - a_prev2[src])
+        a_new, f_new = _rows(rp, fr, er, vl)
+        a_prev2 = a
+        hist_f = [hist_f[1], f_new]
+        a, f = a_new, f_new
+    out_q.put((rank, plan.lo, plan.hi, a, f))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("mode", ["pull", "recon"])
+@pytest.mark.parametrize("kind", ["er", "rgg"])
+def test_partitioned_rounds_match_oracle(world, mode, kind):
+    import fu
+
+    g = (fu.Graph.erdos_renyi(600, 2400, seed=4) if kind == "er"
+         else fu.Graph.random_geometric(900, avg_deg=7, seed=4))
+    v = fu.uniform_values(g.n, seed=2)
+    rounds = 12
+    a_ref, f_ref = oracle.ca_sync(g.rowptr, g.col, v, rounds)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, g.rowptr, g.col, g.rev, v, rounds,
+                                               mode, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    a = np.empty(g.n)
+    f = np.empty(g.E)
+    for rank, lo, hi, al, fl in res:
+        a[lo:hi] = al
+        f[g.rowptr[lo]:g.rowptr[hi]] = fl
+    assert np.array_equal(a, a_ref)
+    assert np.array_equal(f, f_ref)
+
+
+def test_plan_shapes_and_symmetry():
+    import fu
+
+    g = fu.Graph.random_geometric(3000, avg_deg=8, seed=9)
+    world = 4
+    plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
+    b = split_ranges(g.rowptr, world)
+    assert b[0] == 0 and b[-1] == g.n
+    for p in plans:
+        for q in plans:
+            if p.rank == q.rank:
+                continue
+            # what p sends to q is exactly what q expects from p, in q's slot order
+            nf = p.send_f_off[q.rank + 1] - p.send_f_off[q.rank]
+            assert nf == q.recv_f_off[p.rank + 1] - q.recv_f_off[p.rank]
+            sent_gidx = p.send_f_idx[p.send_f_off[q.rank]:p.send_f_off[q.rank + 1]] + g.rowptr[p.lo]
+            exp = q.ghost_f_gidx[q.recv_f_off[p.rank]:q.recv_f_off[p.rank + 1]]
+            assert np.array_equal(sent_gidx, exp)
+            sent_a = p.send_a_idx[p.send_a_off[q.rank]:p.send_a_off[q.rank + 1]] + p.lo
+            exp_a = q.ghost_a_gid[q.recv_a_off[p.rank]:q.recv_a_off[p.rank + 1]]
+            assert np.array_equal(sent_a, exp_a)
+        # local numbering in range
+        assert p.col.max() < p.n_local + p.n_ghost_a
+        assert p.rev.max() < p.e_local + p.n_ghost_f

@@ -206,3 +206,26 @@ def test_full_size_er1m_convergence_and_prefix_parity():
     tr = eng.run(940, err_every=10)
     assert tr[-1] < 1e-9
     assert np.all(np.diff(tr[5:]) <= 0) or tr[-1] < 1e-12  # settles monotonically
+
+
+@pytest.mark.parametrize("kernel", ["recon", "tile"])
+def test_dist_single_rank_rccl_matches_engine(kernel):
+    """fu_dist_create + RCCL communicator at world size 1 (the only size one GPU box can
+    run): no ghosts, the per-round halo hook runs with empty send lists. The multi-rank
+    plan is covered on the CPU (tests/test_dist_gloo.py)."""
+    from fu.dist import DistCollectAll, partition, unique_id
+
+    g = fu.Graph.random_geometric(50_000, avg_deg=8, seed=3)
+    v = fu.uniform_values(g.n, seed=1)
+    plan = partition(g.rowptr, g.col, g.rev, 1, 0)
+    d = DistCollectAll(plan, v, unique_id(), kernel=kernel)
+    d.run(30)
+    eng = fu.CollectAll(g, v)
+    eng.run(30)
+    assert np.array_equal(d.estimates(), eng.estimates())
+    assert np.array_equal(d.flows(), eng.flows())
+    tgt, _ = fu.component_means(g.rowptr, g.col, v)
+    d.set_targets(tgt)
+    tr = d.run(10, err_every=5)
+    assert len(tr) == 2 and np.isfinite(tr).all()
+    d.close()
