@@ -303,7 +303,9 @@ __device__ inline T ld_stream(const T *p) {
 
 // DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
 //   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
-//   2 = no flow load/store (prices the flow stream).
+//   2 = no flow load/store (prices the flow stream);
+//   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
+//   5 = hub chains skipped (prices the exact sequential hub sums).
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
@@ -335,7 +337,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         s_er[q] = er;
       }
       __syncthreads();
-      if (t < 64) {
+      if (t < 64 && DIAG != 5) {
         for (int q = 0; q < cn; ++q) {  // exact left-to-right chain, lane-uniform
           S = S + s_x[q];
           T = T + s_er[q];
@@ -391,7 +393,10 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   for (int k = 0; k < kPer; ++k) {
     const int q = t + k * kBlock;
     g[k] = 0.0;
-    if (q < ne) g[k] = a_prev[DIAG == 1 ? nb + (q % (nn + 1)) : c[k]];
+    if (q < ne) {
+      const int gi = DIAG == 1 ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
+      g[k] = a_prev[gi];
+    }
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -685,6 +690,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   } while (0)
       if (h->diag == 1) FU_RECON(false, false, 1);
       else if (h->diag == 2) FU_RECON(false, false, 2);
+      else if (h->diag == 3) FU_RECON(false, false, 3);
+      else if (h->diag == 4) FU_RECON(false, false, 4);
+      else if (h->diag == 5) FU_RECON(false, false, 5);
       else if (check) {
         if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
       } else {

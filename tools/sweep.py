@@ -26,6 +26,11 @@ VARIANTS = {
     "diag1_gather_free": ("recon", {"diag": 1}),
     "diag2_flow_free": ("recon", {"diag": 2}),
     "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
+    "diag3_half_table": ("recon", {"diag": 3}),
+    "diag4_quarter_table": ("recon", {"diag": 4}),
+    "diag5_no_hub_chain": ("recon", {"diag": 5}),
+    "recon_hub256": ("recon", {"hub_threshold": 256}),
+    "recon_hub2048": ("recon", {"hub_threshold": 2048}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
