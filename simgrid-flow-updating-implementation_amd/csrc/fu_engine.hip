@@ -452,6 +452,182 @@ __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
   if (q < cnt) p[q] = val;
 }
 
+// ------------------------------------------------------------------------------------
+// Variant 5: column split ("split"). Identical arithmetic to variant 4. The neighbour
+// estimates a_{r-1}[col e] are gathered by a separate launch in which each group of XCDs
+// owns one half of the estimate table (4 MB instead of 8 MB for ER-1M, so it stays in the
+// XCD's L2). The gather launch reads a part-major copy of col: the edges of every row with
+// col < split first, then the rest, so each part's stream is contiguous. It writes G in the
+// same part-major order. The compute launch then reads G coalesced and never gathers.
+// Rows must be sorted by neighbour id, so that the part-0 edges of a row are its prefix
+// and the row order of the sums is unchanged. Placement (blockIdx % 8 -> XCD) is used
+// for locality only, never for correctness.
+// ------------------------------------------------------------------------------------
+constexpr int kGatherChunk = 2048;  // edges per gather block (8 per thread)
+
+__global__ __launch_bounds__(kBlock) void k_gather_split(const int *__restrict__ col_pm,
+                                                         long long e0_count, long long e_total,
+                                                         const double *__restrict__ a_prev,
+                                                         double *__restrict__ G) {
+  const int b = blockIdx.x;
+  const int part = (b & 7) >> 2;              // XCD group 0..3 -> part 0, 4..7 -> part 1
+  const long long chunk = (long long)(b >> 3) * 4 + (b & 3);
+  const long long pb = part ? e0_count : 0, pe = part ? e_total : e0_count;
+  const long long base = pb + chunk * kGatherChunk;
+  if (base >= pe) return;
+  constexpr int kPer = kGatherChunk / kBlock;
+  int c[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long e = base + threadIdx.x + k * kBlock;
+    c[k] = e < pe ? ld_stream(col_pm + e) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long e = base + threadIdx.x + k * kBlock;
+    if (c[k] >= 0) G[e] = a_prev[c[k]];
+  }
+}
+
+// part-major index of canonical edge k (0-based position inside row t of the tile)
+__device__ inline int split_index(int k, int split_t, int p0, int p1) {
+  return k < split_t ? p0 + k : p1 + (k - split_t);
+}
+
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void k_round_split(
+    const int4 *__restrict__ tiles, const int2 *__restrict__ tiles_g, const int *__restrict__ rowptr,
+    const int *__restrict__ rowptr0, long long e0_count, const double *__restrict__ v,
+    double *__restrict__ F, const double *__restrict__ G, const double *__restrict__ a_prev2,
+    double *__restrict__ a_new, const double *__restrict__ target,
+    unsigned long long *__restrict__ err) {
+  __shared__ double s_x[kTileEdges];  // f_{r-2} on load, fr after phase B (canonical order)
+  __shared__ double s_g[kTileEdges];  // a_{r-1}[col] in part-major order: part 0 | part 1
+  __shared__ unsigned char s_own[kTileEdges];
+  __shared__ int s_rp[kTileNodes + 1];
+  __shared__ int s_rp0[kTileNodes + 1];
+  __shared__ double s_a[kTileNodes];
+  const int t = threadIdx.x;
+  const int4 tl = tiles[blockIdx.x];
+  const int2 tg = tiles_g[blockIdx.x];  // {rowptr0[node_begin], rowptr0[node_end]}
+  unsigned long long eb = 0;
+
+  if (tl.y < 0) {
+    // ---------------- heavy node ----------------
+    const int i = tl.x;
+    const int b = tl.z, e = tl.w;
+    const int split_i = tg.y - tg.x;
+    const int p0 = tg.x, p1 = (int)(e0_count + (b - tg.x));
+    const double own2 = a_prev2[i];
+    double S = 0.0, T = 0.0;
+    for (int c0 = b; c0 < e; c0 += kTileEdges) {
+      const int cn = min(kTileEdges, e - c0);
+      for (int q = t; q < cn; q += kBlock) {
+        const double er = G[split_index(c0 - b + q, split_i, p0, p1)];
+        s_x[q] = recon_fr(F[c0 + q], er, own2);
+        s_g[q] = er;
+      }
+      __syncthreads();
+      if (t < 64) {
+        for (int q = 0; q < cn; ++q) {
+          S = S + s_x[q];
+          T = T + s_g[q];
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const double a = ((v[i] - S) + T) / (double)(e - b + 1);
+      s_a[0] = a;
+      a_new[i] = a;
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = s_a[0];
+    for (int k = b + t; k < e; k += kBlock) {
+      const double er = G[split_index(k - b, split_i, p0, p1)];
+      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+
+  // ---------------- light tile ----------------
+  const int nb = tl.x, nn = tl.y - tl.x;
+  const int e0 = tl.z, ne = tl.w - tl.z;
+  const int g0b = tg.x, n0 = tg.y - tg.x;   // part-0 edges of the tile: G[g0b, g0b + n0)
+  const long long g1b = e0_count + (e0 - g0b);  // part-1 edges: G[g1b, g1b + ne - n0)
+  constexpr int kPer = kTileEdges / kBlock;
+  double x[kPer], g[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    x[k] = 0.0;
+    g[k] = 0.0;
+    if (q < ne) {
+      x[k] = F[e0 + q];
+      g[k] = q < n0 ? G[g0b + q] : G[g1b + (q - n0)];
+    }
+  }
+  const int rp = t <= nn ? rowptr[nb + t] : 0;
+  const int rp0 = t <= nn ? rowptr0[nb + t] : 0;
+  const int rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
+  const int rp0_last = (t == 0 && nn == kBlock) ? rowptr0[nb + kBlock] : 0;
+  const double vv = t < nn ? v[nb + t] : 0.0;
+  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) {
+      s_x[q] = x[k];
+      s_g[q] = g[k];
+    }
+  }
+  if (t <= nn) {
+    s_rp[t] = rp;
+    s_rp0[t] = rp0;
+  }
+  if (t == 0 && nn == kBlock) {
+    s_rp[kBlock] = rp_last;
+    s_rp0[kBlock] = rp0_last;
+  }
+  __syncthreads();
+  if (t < nn) {
+    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
+    const int split_t = s_rp0[t + 1] - s_rp0[t];
+    const int p0 = s_rp0[t] - g0b;                         // LDS index of the row's part 0
+    const int p1 = n0 + ((s_rp[t] - s_rp0[t]) - (e0 - g0b));  // LDS index of the row's part 1
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double er = s_g[split_index(q - qb, split_t, p0, p1)];
+      const double fr = recon_fr(s_x[q], er, own2);
+      s_x[q] = fr;
+      s_own[q] = (unsigned char)t;
+      S = S + fr;
+      T = T + er;
+    }
+    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
+    s_a[t] = a;
+    a_new[nb + t] = a;
+    if (CHECK) eb = err_bits(a, target[nb + t]);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) {
+      const int o = s_own[q];
+      const int qb = s_rp[o] - e0;
+      const int split_t = s_rp0[o + 1] - s_rp0[o];
+      const int p0 = s_rp0[o] - g0b;
+      const int p1 = n0 + ((s_rp[o] - s_rp0[o]) - (e0 - g0b));
+      const double er = s_g[split_index(q - qb, split_t, p0, p1)];
+      F[e0 + q] = (s_x[q] + s_a[o]) - er;
+    }
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
 // round 0 for the push layout: message i->j = (a_i, a_i) stored at inbox[rev[e]]
 __global__ __launch_bounds__(kBlock) void k_round0_push(int n, const int *__restrict__ rowptr,
                                                         const int *__restrict__ rev,
@@ -575,6 +751,14 @@ struct fu_handle {
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
   std::vector<int64_t> h_rowptr;
+  std::vector<int32_t> h_col;  // host copy (column-split preparation)
+  // kernel 5 (column split)
+  int *colpm = nullptr, *rowptr0 = nullptr;
+  double *G = nullptr;
+  int4 *tiles_s = nullptr;
+  int2 *tiles_g = nullptr;
+  int ntiles_s = 0;
+  int64_t e0_count = 0;
   int4 *tiles = nullptr;  // 2048-edge tiles (kernels 2, 3)
   int ntiles = 0;
   int4 *tiles_r = nullptr;  // kernel 4 tiles (geometry: tile_edges)
@@ -591,7 +775,8 @@ extern "C" void fu__dist_free(fu_handle *h);
 
 namespace {
 
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count) {
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
+                     std::vector<int4> *host_out = nullptr) {
   std::vector<int4> heavy, light;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -615,6 +800,7 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count) {
   // heavy tiles first so their long sequential chains start early
   std::vector<int4> all(heavy);
   all.insert(all.end(), light.begin(), light.end());
+  if (host_out) *host_out = all;
   if (*dst) hipFree(*dst);
   *dst = nullptr;
   *count = (int)all.size();
@@ -631,12 +817,55 @@ int build_tiles(fu_handle *h) {
 
 // Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
 inline double *cur_a(fu_handle *h) {
-  if (h->kernel == 4) return h->a[(int)((h->rounds + 2) % 3)];
+  if (h->kernel >= 4) return h->a[(int)((h->rounds + 2) % 3)];
   return h->a[h->cur];
 }
 inline double *cur_f(fu_handle *h) {
-  if (h->kernel == 4) return h->f[(int)((h->rounds + 1) & 1)];
+  if (h->kernel >= 4) return h->f[(int)((h->rounds + 1) & 1)];
   return h->f[h->cur];
+}
+
+// Kernel 5 preparation: split node id (edge-balanced), part-major col, rowptr0, tiles.
+int ensure_split(fu_handle *h) {
+  if (h->G) return FU_OK;
+  const int32_t n = h->n;
+  const int64_t E = h->E;
+  for (int32_t i = 0; i < n; ++i)
+    for (int64_t k = h->h_rowptr[i] + 1; k < h->h_rowptr[i + 1]; ++k)
+      if (h->h_col[k - 1] >= h->h_col[k])
+        return fail(FU_ERR_GRAPH, "kernel 5 (column split) needs rows sorted by neighbour id");
+  // split id: smallest s with rowptr[s] >= E/2 (symmetric graph: in-degree == degree)
+  int32_t split = (int32_t)(std::lower_bound(h->h_rowptr.begin(), h->h_rowptr.end(), E / 2) - h->h_rowptr.begin());
+  if (split > n) split = n;
+  std::vector<int32_t> rp0(n + 1, 0);
+  for (int32_t i = 0; i < n; ++i) {
+    auto b = h->h_col.begin() + h->h_rowptr[i], e = h->h_col.begin() + h->h_rowptr[i + 1];
+    rp0[i + 1] = rp0[i] + (int32_t)(std::lower_bound(b, e, split) - b);
+  }
+  const int64_t E0 = rp0[n];
+  std::vector<int32_t> pm(E > 0 ? E : 1);
+  for (int32_t i = 0; i < n; ++i) {
+    const int64_t b = h->h_rowptr[i], s0 = rp0[i + 1] - rp0[i];
+    for (int64_t k = 0; k < s0; ++k) pm[rp0[i] + k] = h->h_col[b + k];
+    const int64_t d = h->h_rowptr[i + 1] - b, p1 = E0 + (b - rp0[i]);
+    for (int64_t k = s0; k < d; ++k) pm[p1 + (k - s0)] = h->h_col[b + k];
+  }
+  std::vector<int4> tv;
+  if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles_s, &h->ntiles_s, &tv)) return rc;
+  std::vector<int2> tg(tv.size());
+  for (size_t q = 0; q < tv.size(); ++q) {
+    const int4 t = tv[q];
+    tg[q] = t.y < 0 ? make_int2(rp0[t.x], rp0[t.x + 1]) : make_int2(rp0[t.x], rp0[t.y]);
+  }
+  if (int rc = dmalloc(&h->colpm, (size_t)E)) return rc;
+  if (int rc = dmalloc(&h->rowptr0, (size_t)n + 1)) return rc;
+  if (int rc = dmalloc(&h->tiles_g, tg.size())) return rc;
+  if (int rc = dmalloc(&h->G, (size_t)E)) return rc;
+  if (E) HIP_TRY(hipMemcpy(h->colpm, pm.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->rowptr0, rp0.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->tiles_g, tg.data(), sizeof(int2) * tg.size(), hipMemcpyHostToDevice));
+  h->e0_count = E0;
+  return FU_OK;
 }
 
 int ensure_a2(fu_handle *h) {
@@ -662,7 +891,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 0)) return rc;
   }
-  if (h->kernel == 4) {
+  if (h->kernel >= 4) {
     const int64_t r = h->rounds;
     if (r == 0) {
       hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
@@ -674,6 +903,24 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
                            h->stream, h->n, h->a[0], h->target, err_slot);
+    } else if (h->kernel == 5) {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+      const long long E1 = h->E - h->e0_count;
+      const long long mx = std::max<long long>(h->e0_count, E1);
+      const unsigned gblocks = (unsigned)(8 * ((mx + 4LL * kGatherChunk - 1) / (4LL * kGatherChunk)));
+      if (gblocks)
+        hipLaunchKernelGGL(k_gather_split, dim3(gblocks), dim3(kBlock), 0, h->stream, h->colpm,
+                           (long long)h->e0_count, (long long)h->E, ap, h->G);
+      if (check)
+        hipLaunchKernelGGL(k_round_split<true>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
+                           h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
+                           h->target, err_slot);
+      else
+        hipLaunchKernelGGL(k_round_split<false>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
+                           h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
+                           h->target, err_slot);
     } else {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -784,6 +1031,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   h->n = n;
   h->E = e;
   h->h_rowptr.assign(rowptr, rowptr + n + 1);
+  if (e > 0) h->h_col.assign(col, col + e);
   std::vector<int32_t> rp32(n + 1);
   int32_t md = 0;
   for (int32_t i = 0; i <= n; ++i) {
@@ -862,13 +1110,20 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 4) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..4");
-    if (h->dist && value != 0 && value != 2 && value != 4)
+    if (value < 0 || value > 5) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..5");
+    if (h->dist && value != 0 && value != 2 && value != 4)  // 5: single GPU only
       return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     h->kernel = value == 0 ? 4 : (int)value;
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4) return ensure_a2(h);
+    if (h->kernel == 5) {
+      if (int rc = ensure_a2(h)) return rc;
+      if (int rc = ensure_split(h)) {
+        h->kernel = 4;
+        return rc;
+      }
+    }
     return FU_OK;
   }
   if (!std::strcmp(key, "diag")) {
@@ -1029,7 +1284,8 @@ int fu_destroy(fu_handle *h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->dist) fu__dist_free(h);
   void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
-                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_r};
+                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_r,
+                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
