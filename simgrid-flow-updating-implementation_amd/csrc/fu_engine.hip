@@ -312,7 +312,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
     const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err) {
+    unsigned long long *__restrict__ err, const int *__restrict__ perm) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   __shared__ double s_x[TE];   // f_{r-2} on load, fr after phase B
   __shared__ double s_er[TE];  // a_{r-1}[col e]
@@ -322,6 +322,91 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   const int t = threadIdx.x;
   const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
+
+  if constexpr (TE == kTileEdges && TN == kTileNodes) {
+  if (tl.y == -2) {
+    // ---------------- degree bin: R rows of similar degree, one chain per row ----------
+    // Rows perm[tl.x .. tl.x + R) (sorted by degree, longest first). Each iteration stages
+    // C = TE / R positions of every row in LDS, loaded along row segments (coalesced).
+    // Then thread r runs row r's exact left-to-right chain over its C values. Element
+    // (r, k) lives at r*C + (k ^ sw(r)): the XOR swizzle keeps the column reads of the
+    // chain conflict-free without padding.
+    const int R = tl.z, C = tl.w;
+    const int lgC = 31 - __clz(C);
+    // LDS reuse (no extra footprint): node ids and degrees in s_own's 2 KB, row starts in
+    // s_rp, a_{r-2} of each row in s_a until the chains end, then a_r.
+    int *s_node = reinterpret_cast<int *>(s_own);
+    int *s_deg = s_node + kBlock;
+    int *s_rb = s_rp;
+    double *s_own2 = s_a;
+    if (t < R) {
+      const int node = perm[tl.x + t];
+      s_node[t] = node;
+      const int rb = rowptr[node];
+      s_rb[t] = rb;
+      s_deg[t] = rowptr[node + 1] - rb;
+      s_own2[t] = a_prev2[node];
+    }
+    __syncthreads();
+    auto sw = [&](int r) { return C >= 32 ? (r & 31) : ((r >> (5 - lgC)) & (C - 1)); };
+    const int maxd = s_deg[0];
+    const int my_deg = t < R ? s_deg[t] : 0;
+    double S = 0.0, T = 0.0;
+    for (int c0 = 0; c0 < maxd; c0 += C) {
+#pragma unroll 4
+      for (int q = t; q < R * C; q += kBlock) {
+        const int r = q >> lgC, k = q & (C - 1);
+        if (c0 + k < s_deg[r]) {
+          const int e = s_rb[r] + c0 + k;
+          const double er = a_prev[col[e]];
+          const int slot = (r << lgC) + (k ^ sw(r));
+          s_x[slot] = recon_fr(F[e], er, s_own2[r]);
+          s_er[slot] = er;
+        }
+      }
+      __syncthreads();
+      if (t < R) {
+        const int kend = min(C, my_deg - c0);
+        const int base = t << lgC, x = sw(t);
+        for (int k = 0; k < kend; ++k) {
+          S = S + s_x[base + (k ^ x)];
+          T = T + s_er[base + (k ^ x)];
+        }
+      }
+      __syncthreads();
+    }
+    double a_mine = 0.0;
+    if (t < R) {
+      const int node = s_node[t];
+      a_mine = ((v[node] - S) + T) / (double)(my_deg + 1);
+      a_new[node] = a_mine;
+      if (CHECK) eb = err_bits(a_mine, target[node]);
+    }
+    __syncthreads();  // every read of s_own2 (aliases s_a) is done
+    if (t < R) s_a[t] = a_mine;
+    __syncthreads();
+    if (maxd <= C) {  // one iteration: fr and er are still in LDS
+      for (int q = t; q < R * C; q += kBlock) {
+        const int r = q >> lgC, k = q & (C - 1);
+        if (k < s_deg[r]) {
+          const int slot = (r << lgC) + (k ^ sw(r));
+          F[s_rb[r] + k] = (s_x[slot] + s_a[r]) - s_er[slot];
+        }
+      }
+    } else {  // long rows: re-read the flow, re-gather the estimate (L2-warm)
+      for (int r = 0; r < R; ++r) {
+        const int rb = s_rb[r], d = s_deg[r];
+        const double own2 = a_prev2[s_node[r]], a = s_a[r];
+        for (int k = t; k < d; k += kBlock) {
+          const double er = a_prev[col[rb + k]];
+          F[rb + k] = (recon_fr(F[rb + k], er, own2) + a) - er;
+        }
+      }
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+  }  // if constexpr (default geometry)
 
   if (tl.y < 0) {
     // ---------------- heavy node ----------------
@@ -763,6 +848,8 @@ struct fu_handle {
   int ntiles = 0;
   int4 *tiles_r = nullptr;  // kernel 4 tiles (geometry: tile_edges)
   int ntiles_r = 0;
+  int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
+  int bins = 1;         // kernel 4: degree bins for rows above hub_threshold
   int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
   int tile_nodes = 0;
   bool has_target = false;
@@ -809,8 +896,53 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
   return FU_OK;
 }
 
+// Kernel 4 tiles with degree bins: rows of degree > hub_threshold sorted by degree
+// (descending, ties by id) and grouped R per block (R = TE / C, C = the power of two >= the
+// bin's first degree, capped at TE); then light tiles of contiguous low-degree rows.
+int build_tiles_binned(fu_handle *h) {
+  const int32_t n = h->n;
+  std::vector<int32_t> heavy;
+  for (int32_t i = 0; i < n; ++i)
+    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->hub_threshold) heavy.push_back(i);
+  auto deg = [&](int32_t i) { return h->h_rowptr[i + 1] - h->h_rowptr[i]; };
+  std::stable_sort(heavy.begin(), heavy.end(), [&](int32_t x, int32_t y) { return deg(x) > deg(y); });
+  std::vector<int4> all;
+  size_t q = 0;
+  while (q < heavy.size()) {
+    const int64_t d = deg(heavy[q]);
+    int C = 1;
+    while (C < d && C < kTileEdges) C <<= 1;
+    const int R = std::max(1, std::min(kBlock, kTileEdges / C));
+    const int r = (int)std::min<size_t>(R, heavy.size() - q);
+    all.push_back(make_int4((int)q, -2, r, kTileEdges / R));
+    q += r;
+  }
+  // light tiles over the remaining rows (heavy rows are skipped inside build_tiles_geom)
+  std::vector<int4> light;
+  int32_t i = 0;
+  while (i < n) {
+    if (deg(i) > h->hub_threshold) { ++i; continue; }
+    int32_t b = i;
+    int64_t eb = h->h_rowptr[b];
+    while (i < n && i - b < kTileNodes && deg(i) <= h->hub_threshold && h->h_rowptr[i + 1] - eb <= kTileEdges) ++i;
+    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
+  }
+  all.insert(all.end(), light.begin(), light.end());
+  if (h->tiles_r) hipFree(h->tiles_r);
+  if (h->perm) hipFree(h->perm);
+  h->tiles_r = nullptr;
+  h->perm = nullptr;
+  h->ntiles_r = (int)all.size();
+  if (int rc = dmalloc(&h->tiles_r, all.size())) return rc;
+  if (int rc = dmalloc(&h->perm, std::max<size_t>(1, heavy.size()))) return rc;
+  HIP_TRY(hipMemcpy(h->tiles_r, all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
+  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->perm, heavy.data(), sizeof(int32_t) * heavy.size(), hipMemcpyHostToDevice));
+  return FU_OK;
+}
+
 int build_tiles(fu_handle *h) {
   if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
+  if (h->bins && h->tile_edges == 2048) return build_tiles_binned(h);
   const int te = h->tile_edges, tn = te == 2048 ? 256 : te == 1024 ? (h->tile_nodes ? h->tile_nodes : 128) : 64;
   return build_tiles_geom(h, te, tn, &h->tiles_r, &h->ntiles_r);
 }
@@ -927,7 +1059,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *an = h->a[r % 3];
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
   hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_r), dim3(kBlock), 0, h->stream, \
-                     h->tiles_r, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot)
+                     h->tiles_r, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
     if (h->tile_edges == 2048) FU_RECON_G(C, N, D, 2048, 256);                              \
@@ -1134,6 +1266,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->nt = value != 0;
     return FU_OK;
   }
+  if (!std::strcmp(key, "bins")) {
+    h->bins = value != 0;
+    return build_tiles(h);
+  }
   if (!std::strcmp(key, "tile_edges")) {
     if (value != 2048 && value != 1024 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: tile_edges must be 2048, 1024 or 512");
     h->tile_edges = (int)value;
@@ -1285,7 +1421,7 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
                   h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_r,
-                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g};
+                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

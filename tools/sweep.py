@@ -20,6 +20,7 @@ VARIANTS = {
     "recon": ("recon", {}),
     "recon_nt": ("recon", {"nt": 1}),
     "split": ("split", {}),
+    "recon_nobins": ("recon", {"bins": 0}),
     "recon_1024": ("recon", {"tile_edges": 1024}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
     "recon_1024_nt": ("recon", {"tile_edges": 1024, "nt": 1}),
