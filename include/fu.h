@@ -141,6 +141,14 @@ typedef struct fu_trace fu_trace;
  * actor order; SimGrid's real tie order is not observable offline). */
 int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                    int32_t mode, int32_t ticks, const char *order, fu_trace **out);
+/* Same, with fault injection (not in the reference): faults =
+ * "drop=P,delay=D:Q,seed=S" (any subset; NULL or "" = none). Each put is lost with
+ * probability P or delayed by D ticks with probability Q (SplitMix64 stream in put order).
+ * Lost messages exercise the timeouts (CA:87-91, PW:86-91). */
+int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                      int32_t mode, int32_t ticks, const char *order, const char *faults,
+                      fu_trace **out);
+int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed);
 /* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
  * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */
 int fu_trace_info(const fu_trace *t, int64_t info[8]);

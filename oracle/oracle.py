@@ -199,9 +199,24 @@ class TickEmulator:
     mode: "ca" (collect-all) or "pw" (pairwise).
     """
 
-    def __init__(self, actors, mode: str):
+    def __init__(self, actors, mode: str, faults: str | None = None):
+        """faults: "drop=P,delay=D:Q,seed=S" (extension, not in the reference; same spec and
+        draw order as fu_trace.cpp: one U[0,1) draw per put, in put order)."""
         if mode not in ("ca", "pw"):
             raise ValueError(mode)
+        self.p_drop, self.p_delay, self.d_ticks, self.fstate = 0.0, 0.0, 0, 0
+        for kv in filter(None, (faults or "").split(",")):
+            k, v = kv.split("=")
+            if k == "drop":
+                self.p_drop = float(v)
+            elif k == "delay":
+                d, q = v.split(":")
+                self.d_ticks, self.p_delay = int(d), float(q)
+            elif k == "seed":
+                self.fstate = int(v) & MASK64
+            else:
+                raise ValueError(kv)
+        self.delayed = {}
         self.mode = mode
         self.names = [a[0] for a in actors]
         self.idx = {nm: i for i, nm in enumerate(self.names)}
@@ -222,6 +237,17 @@ class TickEmulator:
     def _send(self, src, dst_name, flow, estimate):
         d = self.idx[dst_name]
         msg = (self.names[src], flow, estimate)
+        if self.p_drop > 0.0 or self.p_delay > 0.0:
+            self.fstate, r = splitmix64(self.fstate)
+            u = (r >> 11) * 2.0 ** -53
+            if u < self.p_drop:
+                return
+            if u < self.p_drop + self.p_delay:
+                self.delayed.setdefault(self.t + self.d_ticks, []).append((d, msg))
+                return
+        self._arrive(d, msg)
+
+    def _arrive(self, d, msg):
         c = self.comm[d]
         if c is not None and not c[0]:
             c[0], c[1], c[2] = True, msg, self.t
@@ -311,6 +337,8 @@ class TickEmulator:
         tick = self._ca_tick if self.mode == "ca" else self._pw_tick
         n = len(self.nodes)
         for perm in tick_orders(n, order, ticks):
+            for d, msg in self.delayed.pop(self.t, []):
+                self._arrive(d, msg)
             for i in perm:
                 c = self.comm[i]
                 if c is None:  # CA:73-74

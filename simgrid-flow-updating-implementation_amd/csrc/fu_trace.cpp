@@ -23,6 +23,14 @@
 //
 // Message slots are recycled. A slot consumed at tick t becomes free at the end of tick t,
 // so no slot is both read and written in the same tick batch.
+//
+// Fault injection (not in the reference, which never loses a
+// message). faults = "drop=P,delay=D:Q,seed=S": each put_async (CA:124 / PW:116) is lost
+// with probability P, or is held back D ticks with probability Q. Draws come from a
+// SplitMix64 stream in put order, so the faulty schedule is as deterministic as the clean
+// one. Lost messages exercise the timeouts (CA:87-91, PW:86-91), i.e. Flow Updating's
+// self-healing. The fault model lives entirely in the schedule, so the GPU replay is the
+// same code.
 #include <cstring>
 #include <unordered_map>
 
@@ -30,6 +38,7 @@
 
 struct fu_trace {
   int32_t n = 0, mode = 0, ticks = 0;
+  int64_t dropped = 0, delayed = 0;
   std::vector<int64_t> urowptr;
   std::vector<int32_t> ucol;
   std::vector<int64_t> tick_task_off;
@@ -65,6 +74,11 @@ struct Builder {
   std::vector<int32_t> free_ids, pending_free;
   int64_t first_seq = 0;
   int32_t t = 0;
+  // faults
+  double p_drop = 0.0, p_delay = 0.0;
+  int32_t delay_ticks = 0;
+  uint64_t fstate = 0;
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> delayed;  // due tick -> (dst, id)
 
   Builder(int32_t n_, int32_t mode_, fu_trace &tr_) : n(n_), mode(mode_), tr(tr_) {}
 
@@ -85,6 +99,25 @@ struct Builder {
   }
 
   void deliver(int32_t dst, int32_t id) {
+    if (p_drop > 0.0 || p_delay > 0.0) {
+      const double u = u01(splitmix_next(fstate));
+      if (u < p_drop) {  // lost: the slot is never consumed and frees at the end of the tick
+        pending_free.push_back(id);
+        tr.dropped++;
+        return;
+      }
+      if (u < p_drop + p_delay) {
+        const int32_t due = t + delay_ticks;
+        if (due >= (int32_t)delayed.size()) delayed.resize(due + 1);
+        delayed[due].emplace_back(dst, id);
+        tr.delayed++;
+        return;
+      }
+    }
+    arrive(dst, id);
+  }
+
+  void arrive(int32_t dst, int32_t id) {
     if (cstate[dst] == 1) {  // posted receive: matched now, transfer in flight
       cstate[dst] = 2;
       cmsg[dst] = id;
@@ -189,6 +222,42 @@ struct Builder {
   }
 };
 
+bool parse_faults(const char *f, double &drop, double &delay, int32_t &dticks, uint64_t &seed) {
+  drop = delay = 0.0;
+  dticks = 0;
+  seed = 0;
+  if (!f || !*f) return true;
+  std::string s(f);
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t end = s.find(',', pos);
+    if (end == std::string::npos) end = s.size();
+    std::string kv = s.substr(pos, end - pos);
+    size_t eq = kv.find('=');
+    if (eq == std::string::npos) return false;
+    std::string k = kv.substr(0, eq), v = kv.substr(eq + 1);
+    char *e = nullptr;
+    if (k == "drop") {
+      drop = std::strtod(v.c_str(), &e);
+      if (*e || drop < 0 || drop > 1) return false;
+    } else if (k == "delay") {
+      size_t c = v.find(':');
+      if (c == std::string::npos) return false;
+      dticks = (int32_t)std::strtol(v.substr(0, c).c_str(), &e, 10);
+      if (*e || dticks < 1) return false;
+      delay = std::strtod(v.substr(c + 1).c_str(), &e);
+      if (*e || delay < 0 || delay > 1) return false;
+    } else if (k == "seed") {
+      seed = std::strtoull(v.c_str(), &e, 10);
+      if (*e) return false;
+    } else {
+      return false;
+    }
+    pos = end + 1;
+  }
+  return drop + delay <= 1.0;
+}
+
 bool parse_order(const char *order, int &kind, uint64_t &seed) {
   if (!order || !std::strcmp(order, "fwd")) { kind = 0; return true; }
   if (!std::strcmp(order, "rev")) { kind = 1; return true; }
@@ -208,12 +277,23 @@ extern "C" {
 
 int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                    int32_t mode, int32_t ticks, const char *order, fu_trace **out) {
+  return fu_trace_build_ex(n, decl_rowptr, decl_col, mode, ticks, order, nullptr, out);
+}
+
+int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                      int32_t mode, int32_t ticks, const char *order, const char *faults,
+                      fu_trace **out) {
   FU_TRY_BEGIN
   if (!out || n <= 0 || !decl_rowptr || ticks < 0 || (mode != FU_MODE_COLLECTALL && mode != FU_MODE_PAIRWISE))
     return fail(FU_ERR_ARG, "fu_trace_build: bad arguments");
   int okind = 0;
   uint64_t oseed = 0;
   if (!parse_order(order, okind, oseed)) return fail(FU_ERR_ARG, std::string("fu_trace_build: bad order '") + (order ? order : "") + "'");
+  double p_drop, p_delay;
+  int32_t dticks;
+  uint64_t fseed;
+  if (!parse_faults(faults, p_drop, p_delay, dticks, fseed))
+    return fail(FU_ERR_ARG, std::string("fu_trace_build: bad faults '") + (faults ? faults : "") + "' (drop=P,delay=D:Q,seed=S)");
   auto *tr = new fu_trace();
   tr->n = n;
   tr->mode = mode;
@@ -221,6 +301,10 @@ int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_co
   tr->first_avg_seq.assign(n, -1);
   tr->fires.assign(n, 0);
   Builder B(n, mode, *tr);
+  B.p_drop = p_drop;
+  B.p_delay = p_delay;
+  B.delay_ticks = dticks;
+  B.fstate = fseed;
   B.nbrs.resize(n);
   for (int32_t i = 0; i < n; ++i) {
     for (int64_t k = decl_rowptr[i]; k < decl_rowptr[i + 1]; ++k) {
@@ -252,6 +336,10 @@ int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_co
   tr->tick_task_off.push_back(0);
   for (int32_t t = 0; t < ticks; ++t) {
     B.t = t;
+    if (t < (int32_t)B.delayed.size()) {  // held-back messages reach their mailbox now
+      for (auto &m : B.delayed[t]) B.arrive(m.first, m.second);
+      B.delayed[t].clear();
+    }
     if (okind == 2) {  // per-tick Fisher-Yates, j = r % (i+1) (same as oracle.tick_orders)
       for (int32_t i = 0; i < n; ++i) perm[i] = i;
       for (int32_t i = n - 1; i > 0; --i) {
@@ -288,6 +376,13 @@ int fu_trace_info(const fu_trace *t, int64_t info[8]) {
   info[5] = t->ticks;
   info[6] = t->dyn_adds;
   info[7] = t->msgs_sent;
+  return FU_OK;
+}
+
+int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed) {
+  if (!t) return fail(FU_ERR_ARG, "fu_trace_fault_stats: NULL trace");
+  if (dropped) *dropped = t->dropped;
+  if (delayed) *delayed = t->delayed;
   return FU_OK;
 }
 

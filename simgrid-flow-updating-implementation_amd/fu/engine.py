@@ -127,7 +127,8 @@ class Trace:
     order. mode: 'collectall' | 'pairwise'. order: 'fwd' | 'rev' | 'rand:<seed>'.
     """
 
-    def __init__(self, decl_rowptr, decl_col, mode: str, ticks: int, order: str = "fwd"):
+    def __init__(self, decl_rowptr, decl_col, mode: str, ticks: int, order: str = "fwd",
+                 faults: str | None = None):
         rp = np.ascontiguousarray(decl_rowptr, dtype=np.int64)
         c = np.ascontiguousarray(decl_col, dtype=np.int32)
         self.n = len(rp) - 1
@@ -136,9 +137,14 @@ class Trace:
         self.ticks = int(ticks)
         self.order = order
         out = L.vp()
-        L.call("fu_trace_build", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
-               self.ticks, order.encode(), ctypes.byref(out))
+        L.call("fu_trace_build_ex", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
+               self.ticks, order.encode(), faults.encode() if faults else None,
+               ctypes.byref(out))
         self._h = out
+        self.faults = faults
+        dr, dl = L.i64(), L.i64()
+        L.call("fu_trace_fault_stats", self._h, ctypes.byref(dr), ctypes.byref(dl))
+        self.dropped, self.delayed = int(dr.value), int(dl.value)
         info = np.zeros(8, dtype=np.int64)
         L.call("fu_trace_info", self._h, L.ptr(info))
         (self.n_union_edges, self.n_tasks, self.n_events, self.n_out_ids, self.n_msgs,

@@ -101,3 +101,42 @@ def test_trace_bad_inputs():
         fu.Trace(rp, np.array([1, 5], dtype=np.int32), "pairwise", 10)  # out of range
     with pytest.raises(fu.FuError):
         fu.Trace(rp, np.array([1, 0], dtype=np.int32), "pairwise", 10, "sideways")
+
+
+@pytest.mark.parametrize("mode", ["collectall", "pairwise"])
+@pytest.mark.parametrize("faults", ["drop=0.1,seed=5", "delay=3:0.2,seed=9", "drop=0.05,delay=7:0.1,seed=1"])
+def test_fault_injection_matches_emulator(mode, faults):
+    """Fault injection (§8(f)): the native trace and the oracle emulator draw the same faults
+    in put order; events and per-tick estimates agree exactly, and the run still converges
+    through the timeouts (CA:87-91, PW:86-91)."""
+    d = load_json("tick_small_platform_ca_fwd.json")
+    names, vals, rp, col = fixture_decl_csr(d)
+    em = oracle.TickEmulator(d["actors"], "ca" if mode == "collectall" else "pw", faults=faults)
+    snaps = {}
+
+    def cb(t, e):
+        if t % 50 == 0 or t == 1999:
+            snaps[t] = dict(e.last_avg_items())
+
+    em.run(2000, "fwd", on_tick=cb)
+    tr = fu.Trace(rp, col, mode, 2000, "fwd", faults=faults)
+    a = tr.arrays()
+    assert trace_events_as_log(a) == [list(x) for x in em.events]
+    assert tr.dropped + tr.delayed > 0
+    ticks = sorted(snaps)
+    last, flow, est, s2 = coracle.replay(a["rowptr"], vals, a["tick_task_off"], a["tasks"], a["events"],
+                                         a["out_ids"], tr.n_msgs, ticks)
+    for t in ticks:
+        for i, v in snaps[t].items():
+            assert s2[t][i] == v
+    # self-healing: still converges to the mean despite lost messages
+    mean = sum(vals) / len(vals)
+    assert max(abs(x - mean) for x in snaps[1999].values()) / mean < 1e-6
+
+
+def test_fault_spec_errors():
+    rp = np.array([0, 1, 2], dtype=np.int64)
+    col = np.array([1, 0], dtype=np.int32)
+    for bad in ("drop=2", "delay=0:0.1", "junk=1", "drop=0.6,delay=1:0.6"):
+        with pytest.raises(fu.FuError, match="faults"):
+            fu.Trace(rp, col, "pairwise", 10, faults=bad)
