@@ -796,6 +796,110 @@ __global__ __launch_bounds__(kBlock) void k_replay_tick(
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Persistent replay: one launch for all ticks, dataflow order. Each thread owns nodes
+// {gtid, gtid + G, ...} and walks each node's events in program order (events regrouped
+// per node on the host). A RECV waits until its message exists. Messages have unique slots
+// (no recycling), so a slot is written once: it starts as a signalling-NaN sentinel that
+// arithmetic never produces, and each 8-byte half is its own readiness tag (data-tagged
+// granule: agent-scope relaxed sc1 store, sc1 load; MI355X_MICROARCH.md "hand-off"). Per-node
+// order + produce-before-consume is exactly the dependence structure of the tick batches,
+// so the results are the same bits. A thread never blocks on one node: it polls once and
+// moves on. The globally earliest pending event is always ready, so a fully resident grid
+// always makes progress. The grid is sized below the occupancy bound.
+// ------------------------------------------------------------------------------------
+constexpr unsigned long long kMsgSentinel = 0x7FF7A5A5A5A5A5A5ull;
+
+__device__ inline unsigned long long ld_tag(const unsigned long long *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void st_tag(unsigned long long *p, double v) {
+  __hip_atomic_store(p, (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__global__ __launch_bounds__(kBlock) void k_replay_persist(
+    int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_ev,
+    const int *__restrict__ node_tick, const int *__restrict__ out_uid,
+    const long long *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ flow,
+    double *__restrict__ est, double *__restrict__ last, unsigned long long *__restrict__ pay,
+    long long *__restrict__ cursor, int *__restrict__ scur, int n_snap,
+    const int *__restrict__ snap_ticks, double *__restrict__ snaps, int *__restrict__ status,
+    long long max_iters) {
+  const int G = gridDim.x * kBlock;
+  const int g = blockIdx.x * kBlock + threadIdx.x;
+  long long it = 0;
+  bool left = true;
+  while (left) {
+    left = false;
+    bool progressed = false;
+    for (int node = g; node < n; node += G) {
+      long long p = cursor[node];
+      const long long pe = node_off[node + 1];
+      int sc = scur[node];
+      double *fl = flow + rowptr[node];
+      double *es = est + rowptr[node];
+      const double val = v[node];
+      double lst = last[node];
+      while (p < pe) {
+        const int tk = node_tick[p];
+        if (tk >= tick_end) break;
+        while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
+        const int4 ev = node_ev[p];
+        if (ev.x == FU_EV_RECV) {
+          const unsigned long long fx = ld_tag(pay + 2 * (long long)ev.z);
+          const unsigned long long fy = ld_tag(pay + 2 * (long long)ev.z + 1);
+          if (fx == kMsgSentinel || fy == kMsgSentinel) break;  // not sent yet
+          es[ev.y] = __longlong_as_double((long long)fy);
+          fl[ev.y] = -__longlong_as_double((long long)fx);
+        } else if (ev.x == FU_EV_FIRE_CA) {
+          const int k = ev.y;
+          double S = 0.0, T = 0.0;
+          for (int j = 0; j < k; ++j) S = S + fl[j];
+          const double estimate = val - S;
+          for (int j = 0; j < k; ++j) T = T + es[j];
+          const double avg = (estimate + T) / (double)(k + 1);
+          lst = avg;
+          for (int j = 0; j < k; ++j) {
+            const double nf = (fl[j] + avg) - es[j];
+            fl[j] = nf;
+            es[j] = avg;
+            const long long m = out_uid[ev.z + j];
+            st_tag(pay + 2 * m, nf);
+            st_tag(pay + 2 * m + 1, avg);
+          }
+        } else {
+          const int sl = ev.y, k = ev.z;
+          double S = 0.0;
+          for (int j = 0; j < k; ++j) S = S + fl[j];
+          const double estimate = val - S;
+          const double avg = (es[sl] + estimate) / 2.0;
+          lst = avg;
+          const double nf = (fl[sl] + avg) - es[sl];
+          fl[sl] = nf;
+          es[sl] = avg;
+          st_tag(pay + 2 * (long long)ev.w, nf);
+          st_tag(pay + 2 * (long long)ev.w + 1, avg);
+        }
+        ++p;
+        progressed = true;
+      }
+      const bool done = p == pe || node_tick[p] >= tick_end;
+      if (done)
+        while (sc < n_snap && snap_ticks[sc] < tick_end) snaps[(long long)sc++ * n + node] = lst;
+      cursor[node] = p;
+      scur[node] = sc;
+      last[node] = lst;
+      if (!done) left = true;
+    }
+    if (left && !progressed) __builtin_amdgcn_s_sleep(2);
+    if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
+      atomicExch(status, 1);
+      break;
+    }
+  }
+}
+
 template <typename T>
 int dmalloc(T **p, size_t count) {
   if (count == 0) count = 1;
@@ -1445,7 +1549,80 @@ struct fu_replay {
   int *tasks = nullptr, *events = nullptr, *out_ids = nullptr;
   double *v = nullptr, *flow = nullptr, *est = nullptr, *last = nullptr;
   double2 *msg = nullptr;
+  // persistent mode (built on first use)
+  int persistent = 0;
+  std::vector<int32_t> h_tasks, h_events, h_out_ids;
+  long long *node_off = nullptr, *cursor = nullptr;
+  int4 *node_ev = nullptr;
+  int *node_tick = nullptr, *out_uid = nullptr, *scur = nullptr, *status = nullptr;
+  unsigned long long *pay = nullptr;
+  int64_t n_uid = 0;
+  bool pers_ready = false;
 };
+
+static int replay_build_persistent(fu_replay *r) {
+  if (r->pers_ready) return FU_OK;
+  const int32_t n = r->n;
+  const int64_t nt = (int64_t)r->h_tasks.size() / 3, ne = (int64_t)r->h_events.size() / 4;
+  std::vector<int64_t> off(n + 1, 0);
+  for (int64_t q = 0; q < nt; ++q) off[r->h_tasks[3 * q] + 1] += r->h_tasks[3 * q + 2] - r->h_tasks[3 * q + 1];
+  for (int32_t i = 0; i < n; ++i) off[i + 1] += off[i];
+  std::vector<int64_t> pos(off.begin(), off.end() - 1);
+  std::vector<int4> nev(ne > 0 ? ne : 1);
+  std::vector<int32_t> ntick(ne > 0 ? ne : 1);
+  std::vector<int32_t> ouid(r->h_out_ids.size() > 0 ? r->h_out_ids.size() : 1);
+  std::vector<int64_t> slot_uid(r->n_msgs > 0 ? r->n_msgs : 1, -1);
+  int64_t U = 0;
+  for (int32_t t = 0; t < r->ticks; ++t) {
+    for (int64_t q = r->h_tto[t]; q < r->h_tto[t + 1]; ++q) {
+      const int32_t node = r->h_tasks[3 * q];
+      for (int32_t p = r->h_tasks[3 * q + 1]; p < r->h_tasks[3 * q + 2]; ++p) {
+        const int32_t *e = &r->h_events[4 * (int64_t)p];
+        int4 o = make_int4(e[0], e[1], e[2], e[3]);
+        if (e[0] == FU_EV_RECV) {
+          const int64_t u = slot_uid[e[2]];
+          if (u < 0) return fail(FU_ERR_ARG, "replay: RECV of a message slot never written");
+          o.z = (int)u;
+        } else if (e[0] == FU_EV_FIRE_CA) {
+          for (int32_t j = 0; j < e[1]; ++j) {
+            slot_uid[r->h_out_ids[e[2] + j]] = U;
+            ouid[e[2] + j] = (int32_t)U++;
+          }
+        } else {
+          slot_uid[e[3]] = U;
+          o.w = (int)U++;
+        }
+        if (U >= (int64_t)INT32_MAX) return fail(FU_ERR_ALLOC, "replay: more than 2^31 messages");
+        nev[pos[node]] = o;
+        ntick[pos[node]++] = t;
+      }
+    }
+  }
+  r->n_uid = U;
+  if (int rc = dmalloc(&r->node_off, n + 1)) return rc;
+  if (int rc = dmalloc(&r->node_ev, nev.size())) return rc;
+  if (int rc = dmalloc(&r->node_tick, ntick.size())) return rc;
+  if (int rc = dmalloc(&r->out_uid, ouid.size())) return rc;
+  if (int rc = dmalloc(&r->pay, 2 * (size_t)std::max<int64_t>(U, 1))) return rc;
+  if (int rc = dmalloc(&r->cursor, n)) return rc;
+  if (int rc = dmalloc(&r->scur, n)) return rc;
+  if (int rc = dmalloc(&r->status, 1)) return rc;
+  HIP_TRY(hipMemcpy(r->node_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->node_ev, nev.data(), sizeof(int4) * nev.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->node_tick, ntick.data(), sizeof(int32_t) * ntick.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->out_uid, ouid.data(), sizeof(int32_t) * ouid.size(), hipMemcpyHostToDevice));
+  std::vector<long long> cur(off.begin(), off.end() - 1);
+  HIP_TRY(hipMemcpy(r->cursor, cur.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemset(r->scur, 0, sizeof(int) * n));
+  double sentinel;
+  std::memcpy(&sentinel, &kMsgSentinel, sizeof(double));
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(2 * std::max<int64_t>(U, 1))), dim3(kBlock), 0, r->stream,
+                     (long long)(2 * std::max<int64_t>(U, 1)), sentinel, reinterpret_cast<double *>(r->pay));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(r->stream));
+  r->pers_ready = true;
+  return FU_OK;
+}
 
 int fu_replay_create(int32_t n, const int64_t *rowptr, const double *value, int32_t ticks,
                      const int64_t *tick_task_off, int64_t n_tasks, const int32_t *tasks,
@@ -1486,6 +1663,9 @@ int fu_replay_create(int32_t n, const int64_t *rowptr, const double *value, int3
   r->E = E;
   r->n_msgs = n_msgs;
   r->h_tto.assign(tick_task_off, tick_task_off + ticks + 1);
+  r->h_tasks.assign(tasks, tasks + 3 * n_tasks);
+  r->h_events.assign(events, events + 4 * n_events);
+  r->h_out_ids.assign(out_ids, out_ids + n_out_ids);
   if (hipSetDevice(device) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipSetDevice failed"));
   if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
   if (hipEventCreate(&r->ev0) != hipSuccess || hipEventCreate(&r->ev1) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
@@ -1530,6 +1710,35 @@ int fu_replay_create_from_trace(const fu_trace *t, const double *value, int32_t 
 
 static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
                         double *snaps_dev) {
+  if (r->persistent) {
+    if (r->cur_tick > 0 && !r->pers_ready) return fail(FU_ERR_STATE, "replay: cannot switch to persistent mode mid-run");
+    if (int rc = replay_build_persistent(r)) return rc;
+    int32_t *d_st = nullptr;
+    if (n_snap > 0) {
+      if (int rc = dmalloc(&d_st, n_snap)) return rc;
+      HIP_TRY(hipMemcpyAsync(d_st, snap_ticks, sizeof(int32_t) * n_snap, hipMemcpyHostToDevice, r->stream));
+    }
+    HIP_TRY(hipMemsetAsync(r->scur, 0, sizeof(int) * r->n, r->stream));
+    HIP_TRY(hipMemsetAsync(r->status, 0, sizeof(int), r->stream));
+    int per_cu = 0, ncu = 0;
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_persist, kBlock, 0));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, r->device));
+    // stay below the occupancy bound (the API can over-report by one block per CU)
+    const long long cap = std::max(1LL, (long long)std::max(1, per_cu - 1) * ncu);
+    const unsigned blocks = (unsigned)std::min<long long>(cap, grid_for(r->n));
+    hipLaunchKernelGGL(k_replay_persist, dim3(blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
+                       r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v, r->flow,
+                       r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
+                       (long long)1 << 28);
+    HIP_TRY(hipGetLastError());
+    int st = 0;
+    HIP_TRY(hipMemcpyAsync(&st, r->status, sizeof(int), hipMemcpyDeviceToHost, r->stream));
+    HIP_TRY(hipStreamSynchronize(r->stream));
+    if (d_st) hipFree(d_st);
+    if (st) return fail(FU_ERR_STATE, "replay: persistent kernel hit its iteration bound");
+    r->cur_tick = tick_end;
+    return FU_OK;
+  }
   int32_t si = 0;
   while (si < n_snap && snap_ticks[si] < r->cur_tick) ++si;
   for (int32_t t = r->cur_tick; t < tick_end; ++t) {
@@ -1594,11 +1803,22 @@ int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est) {
   return FU_OK;
 }
 
+int fu_replay_set_option(fu_replay *r, const char *key, int64_t value) {
+  if (!r || !key) return fail(FU_ERR_ARG, "fu_replay_set_option: NULL argument");
+  if (!std::strcmp(key, "persistent")) {
+    if (r->cur_tick != 0) return fail(FU_ERR_STATE, "fu_replay_set_option: persistent must be set before the first tick");
+    r->persistent = value != 0;
+    return FU_OK;
+  }
+  return fail(FU_ERR_ARG, std::string("fu_replay_set_option: unknown key '") + key + "'");
+}
+
 int fu_replay_destroy(fu_replay *r) {
   if (!r) return FU_OK;
   hipSetDevice(r->device);
   if (r->stream) hipStreamSynchronize(r->stream);
-  void *ptrs[] = {r->rowptr, r->tasks, r->events, r->out_ids, r->v, r->flow, r->est, r->last, r->msg};
+  void *ptrs[] = {r->rowptr, r->tasks, r->events, r->out_ids, r->v, r->flow, r->est, r->last, r->msg,
+                  r->node_off, r->cursor, r->node_ev, r->node_tick, r->out_uid, r->scur, r->status, r->pay};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (r->ev0) hipEventDestroy(r->ev0);

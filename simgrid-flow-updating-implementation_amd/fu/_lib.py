@@ -81,6 +81,7 @@ _SIGS = {
     "fu_replay_run_timed": ([vp, i32, P(f32)], ctypes.c_int),
     "fu_replay_get": ([vp, vp, vp, vp], ctypes.c_int),
     "fu_replay_destroy": ([vp], ctypes.c_int),
+    "fu_replay_set_option": ([vp, cp, i64], ctypes.c_int),
     "fu_dist_unique_id": ([vp], ctypes.c_int),
     "fu_dist_create": ([i32, i64, vp, vp, vp, vp, i32, i64, i32, i32, vp, vp, vp, vp, vp, vp,
                         vp, i32, P(vp)], ctypes.c_int),

@@ -191,7 +191,7 @@ class Trace:
 class Replay:
     """GPU replay of a Trace with node values."""
 
-    def __init__(self, trace: Trace, values, device: int = 0):
+    def __init__(self, trace: Trace, values, device: int = 0, persistent: bool = False):
         self.trace = trace
         self.values = np.ascontiguousarray(values, dtype=np.float64)
         if len(self.values) != trace.n:
@@ -202,6 +202,8 @@ class Replay:
         self._h = out
         self.n = trace.n
         self.E = trace.n_union_edges
+        if persistent:
+            L.call("fu_replay_set_option", self._h, b"persistent", 1)
         self.tick = 0
 
     def run(self, tick_end: int, snapshot_ticks=()):

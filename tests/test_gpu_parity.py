@@ -135,13 +135,14 @@ def test_option_errors():
     eng.run(1)
 
 
+@pytest.mark.parametrize("persistent", [False, True])
 @pytest.mark.parametrize("name,fn", tick_fixtures())
-def test_replay_matches_reference_snapshots(name, fn):
+def test_replay_matches_reference_snapshots(name, fn, persistent):
     d = load_json(fn)
     names, vals, rp, col = fixture_decl_csr(d)
     tr = fu.Trace(rp, col, "collectall" if d["mode"] == "ca" else "pairwise", d["ticks"],
                   d["order"])
-    rep = fu.Replay(tr, vals)
+    rep = fu.Replay(tr, vals, persistent=persistent)
     snaps = rep.run(d["ticks"], snapshot_ticks=range(d["ticks"]))
     for t in range(d["ticks"]):
         keys = d["snap_keys"][t]
@@ -153,14 +154,15 @@ def test_replay_matches_reference_snapshots(name, fn):
         assert list(est[a["rowptr"][i]:a["rowptr"][i + 1]]) == d["estimates"][i]
 
 
+@pytest.mark.parametrize("persistent", [False, True])
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
-def test_replay_rr64k_vs_c_oracle(mode):
+def test_replay_rr64k_vs_c_oracle(mode, persistent):
     """BASELINE config 3: pairwise on a 64K-node random regular graph (and collect-all)."""
     g = fu.Graph.random_regular(65536, 8, seed=1)
     v = fu.uniform_values(g.n, seed=0)
     tr = fu.Trace(g.rowptr, g.col, mode, 160, "rand:3")
     a = tr.arrays()
-    rep = fu.Replay(tr, v)
+    rep = fu.Replay(tr, v, persistent=persistent)
     snaps = rep.run(160, snapshot_ticks=[60, 120, 159])
     last, flows, est = rep.state()
     l_ref, f_ref, e_ref, s_ref = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"],
@@ -237,3 +239,21 @@ def test_dist_single_rank_rccl_matches_engine(kernel):
     tr = d.run(10, err_every=5)
     assert len(tr) == 2 and np.isfinite(tr).all()
     d.close()
+
+
+@pytest.mark.parametrize("persistent", [False, True])
+def test_replay_with_faults_vs_c_oracle(persistent):
+    """Fault-injected pairwise trace (drops + delays) replayed on the GPU == C oracle."""
+    g = fu.Graph.random_regular(4096, 6, seed=2)
+    v = fu.uniform_values(g.n, seed=5)
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", 300, "rand:1", faults="drop=0.1,delay=4:0.1,seed=3")
+    a = tr.arrays()
+    rep = fu.Replay(tr, v, persistent=persistent)
+    snaps = rep.run(150, snapshot_ticks=[60, 149])
+    snaps.update(rep.run(300, snapshot_ticks=[299]))
+    l_ref, f_ref, e_ref, s_ref = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"],
+                                                a["events"], a["out_ids"], tr.n_msgs, [60, 149, 299])
+    last, flows, est = rep.state()
+    assert np.array_equal(last, l_ref) and np.array_equal(flows, f_ref)
+    for t in (60, 149, 299):
+        assert np.array_equal(snaps[t], s_ref[t])

@@ -24,19 +24,25 @@ for mode in ("pairwise", "collectall"):
     a = tr.arrays()
     ev = a["events"]
     upd = int(np.sum(ev[:, 0] == 2) + np.sum(ev[ev[:, 0] == 1, 1]))
-    rep = fu.Replay(tr, v)
-    rep.run(1)
-    ms = rep.run_timed(ticks)
-    last, flows, est = rep.state()
+    res = {}
+    for pers in (False, True):
+        rep = fu.Replay(tr, v, persistent=pers)
+        ms = rep.run_timed(ticks)
+        res[pers] = (ms, rep.state())
+        rep.close()
+    ms, (last, flows, est) = res[False]
+    ms_p, (last_p, flows_p, _) = res[True]
     t0 = time.perf_counter()
     l_ref, f_ref, e_ref, _ = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"], a["events"],
                                             a["out_ids"], tr.n_msgs)
     t_cpu = time.perf_counter() - t0
     print(json.dumps({"mode": mode, "ticks": ticks, "events": tr.n_events, "tasks": tr.n_tasks,
                       "flow_updates": upd, "trace_build_s": t_build, "gpu_ms": ms,
-                      "gpu_us_per_tick": ms * 1e3 / (ticks - 1),
+                      "gpu_us_per_tick": ms * 1e3 / ticks,
                       "gpu_flow_updates_per_s": upd / (ms / 1e3),
                       "cpu_oracle_1thread_s": t_cpu, "cpu_flow_updates_per_s": upd / t_cpu,
-                      "bitwise_equal": bool(np.array_equal(last, l_ref) and np.array_equal(flows, f_ref))}),
+                      "gpu_persistent_ms": ms_p, "gpu_persistent_us_per_tick": ms_p * 1e3 / ticks,
+                      "gpu_persistent_flow_updates_per_s": upd / (ms_p / 1e3),
+                      "bitwise_equal": bool(np.array_equal(last, l_ref) and np.array_equal(flows, f_ref)),
+                      "persistent_bitwise_equal": bool(np.array_equal(last_p, l_ref) and np.array_equal(flows_p, f_ref))}),
           flush=True)
-    rep.close()
