@@ -1729,7 +1729,7 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
     hipLaunchKernelGGL(k_replay_persist, dim3(blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
                        r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v, r->flow,
                        r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
-                       (long long)1 << 28);
+                       (long long)1 << 22);
     HIP_TRY(hipGetLastError());
     int st = 0;
     HIP_TRY(hipMemcpyAsync(&st, r->status, sizeof(int), hipMemcpyDeviceToHost, r->stream));
