@@ -44,9 +44,11 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20, help="untimed rounds first")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--m", type=int, default=4_000_000)
-    ap.add_argument("--workload", default="er", choices=["er", "rgg", "rmat", "rr"],
+    ap.add_argument("--workload", default="er", choices=["er", "rgg", "rmat", "rr", "rgg-dist"],
                     help="er = the headline ER-1M (default); others are exploratory: rgg "
-                         "(--n nodes, avg deg 8), rmat (scale = --n, edge factor 16), rr (d = 8)")
+                         "(--n nodes, avg deg 8), rmat (scale = --n, edge factor 16), rr (d = 8), "
+                         "rgg-dist (ONE random geometric graph of --n nodes per GPU, partitioned "
+                         "into slabs across the ranks, RCCL halo exchange every round)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
@@ -81,6 +83,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
+    if args.workload == "rgg-dist":
+        return run_dist(args, world, rank, local, dist, barrier, allmax)
     t_gen = time.perf_counter()
     if args.workload == "er":
         g = fu.Graph.erdos_renyi(args.n, args.m, seed=1 + rank)
@@ -180,6 +184,73 @@ def main():
             "graph_gen_s": t_gen,
         }
         print(json.dumps(out), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def run_dist(args, world, rank, local, dist, barrier, allmax):
+    """BASELINE config 5 (weak scaling): RGG with --n nodes per GPU, one global graph split
+    into slabs (fu_part_gen_rgg, no rank builds the global graph), kernel 4 with the
+    estimates-only RCCL halo. value = all ranks' edge updates / max-over-ranks time."""
+    import fu  # noqa: F401
+    from fu.dist import DistCollectAll, RggPart, unique_id
+
+    n_total = args.n * world
+    t = time.perf_counter()
+    part = RggPart(n_total, avg_deg=8.0, seed=1, nparts=world, part=rank)
+    v = part.values(seed=0)
+    t_gen = time.perf_counter() - t
+    if world > 1:
+        import torch
+
+        buf = torch.zeros(128, dtype=torch.uint8)
+        if rank == 0:
+            buf = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
+        dist.broadcast(buf, 0)
+        uid = bytes(buf.tolist())
+    else:
+        uid = unique_id()
+    eng = DistCollectAll(part.to_plan(), v, uid, device=local, kernel="auto")
+    eng.run(args.warmup)
+    eng.synchronize()
+    barrier()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    kern_ms = eng.run_timed(args.steps)
+    eng.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    wall = allmax(t1 - t0)
+    kern_ms = allmax(kern_ms)
+    e_tot = part.e_local
+    if dist is not None:
+        import torch
+
+        te = torch.tensor([float(part.e_local), float(part.n_local), float(part.n_ghost_a)],
+                          dtype=torch.float64)
+        dist.all_reduce(te)
+        e_tot = int(te[0].item())
+        n_tot, halo = int(te[1].item()), int(te[2].item())
+    else:
+        n_tot, halo = part.n_local, part.n_ghost_a
+    alg = 24 * e_tot + 28 * n_tot
+    if rank == 0:
+        avg_s = kern_ms / 1e3 / args.steps
+        achieved = alg / avg_s / 1e9 / world  # per GPU, against one GPU's peak
+        print(json.dumps({
+            "metric": "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error",
+            "value": e_tot * args.steps / wall, "unit": "edge-updates/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded RGG, U[0,100) values)",
+            "config": {"workload": f"rgg-dist:n={n_total} ({args.n} per GPU), deg=8, slabs, "
+                                   "RCCL estimates-only halo", "E_directed": e_tot,
+                       "halo_estimates_per_round": halo, "parallelism": f"graph partition x{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "alg_bytes_per_launch": alg // world, "avg_launch_us": avg_s * 1e6},
+            "cpu_baseline": None, "graph_gen_s": t_gen}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()

@@ -198,7 +198,9 @@ int fu_dist_unique_id(uint8_t *id_out /* FU_UNIQUE_ID_BYTES */);
  *   send_f_off[nranks+1] / send_f_idx: local edges whose flow goes to each peer, in the
  *     order that peer stores them in its ghost flow slots;
  *   recv_f_off[nranks+1]: ghost flow slots per peer (contiguous, peer order);
- *   send_a_off / send_a_idx, recv_a_off: the same for estimates of boundary nodes. */
+ *   send_a_off / send_a_idx, recv_a_off: the same for estimates of boundary nodes.
+ * rev == NULL (with n_ghost_f = 0 and an empty flow plan) = estimates-only halo: kernel 4
+ * rebuilds flows locally, so only boundary estimates move; kernels 1-3 are refused. */
 int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                    const int32_t *col, const int32_t *rev, const double *value,
                    int32_t n_ghost_a, int64_t n_ghost_f, int32_t nranks, int32_t rank,
@@ -206,6 +208,23 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                    const int64_t *recv_f_off, const int64_t *send_a_off,
                    const int32_t *send_a_idx, const int64_t *recv_a_off,
                    const uint8_t *unique_id, int32_t device, fu_handle **out);
+
+/* Partition-aware random geometric graph: rank `part` of `nparts` generates only its slab
+ * of cell columns (plus the two halo columns) of the graph fu_graph_gen_rgg(n_total, radius,
+ * seed) would build, with the same global node ids and row order. Output: local CSR in
+ * ghost numbering and the estimates-only halo plan for fu_dist_create (rev = NULL). */
+typedef struct fu_part fu_part;
+int fu_part_gen_rgg(int64_t n_total, double radius, uint64_t seed, int32_t nparts,
+                    int32_t part, fu_part **out);
+/* info[0]=n_local [1]=e_local [2]=lo [3]=hi (global ids) [4]=ghost estimates
+ * [5]=boundary sends [6]=max degree [7]=n_total */
+int fu_part_info(const fu_part *p, int64_t info[8]);
+int fu_part_export(const fu_part *p, int64_t *rowptr, int32_t *col, int64_t *ghost_gid,
+                   int64_t *send_a_off, int32_t *send_a_idx, int64_t *recv_a_off);
+int fu_part_free(fu_part *p);
+/* out[k] = lo + (hi - lo) * U_{first+k}: a slice of the fu_values_uniform stream. */
+int fu_values_uniform_range(int64_t first, int64_t count, uint64_t seed, double lo, double hi,
+                            double *out);
 
 #ifdef __cplusplus
 }

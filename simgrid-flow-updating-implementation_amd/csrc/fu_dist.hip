@@ -153,13 +153,18 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, cons
   if (recv_f_off[0] != 0 || recv_f_off[nranks] != n_ghost_f || recv_a_off[0] != 0 || recv_a_off[nranks] != n_ghost_a ||
       send_f_off[0] != 0 || send_a_off[0] != 0)
     return fail(FU_ERR_ARG, "fu_dist_create: halo offsets inconsistent with ghost counts");
+  // rev == NULL: estimates-only halo (kernel 4); no ghost flows, flows plan must be empty
+  if (!rev && (n_ghost_f != 0 || send_f_off[nranks] != 0))
+    return fail(FU_ERR_ARG, "fu_dist_create: rev == NULL requires an empty flow halo");
   const int64_t nsf = send_f_off[nranks], nsa = send_a_off[nranks];
   for (int64_t q = 0; q < nsf; ++q)
     if (send_f_idx[q] < 0 || send_f_idx[q] >= e_local) return fail(FU_ERR_ARG, "fu_dist_create: send_f_idx out of range");
   for (int64_t q = 0; q < nsa; ++q)
     if (send_a_idx[q] < 0 || send_a_idx[q] >= n_local) return fail(FU_ERR_ARG, "fu_dist_create: send_a_idx out of range");
   fu_handle *h = nullptr;
-  if (int rc = fu__create_common(n_local, e_local, rowptr, col, rev, value, device, n_ghost_f, n_ghost_a, &h)) return rc;
+  if (int rc = fu__create_common(n_local, e_local, rowptr, col, rev, value, device, rev ? n_ghost_f : -1,
+                                 n_ghost_a, &h))
+    return rc;
   auto *d = new DistState();
   fu__handle_set_dist(h, d);
   d->nranks = nranks;

@@ -1255,8 +1255,11 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
                       const int32_t *rev, const double *value, int32_t device,
                       int64_t f_extra, int32_t a_extra, fu_handle **out) {
   FU_TRY_BEGIN
-  if (!out || n <= 0 || e < 0 || !rowptr || !value || (e > 0 && (!col || !rev)))
+  // rev may be NULL only for the estimates-only multi-GPU halo (kernel 4 never reads rev)
+  if (!out || n <= 0 || e < 0 || !rowptr || !value || (e > 0 && !col) || (e > 0 && !rev && f_extra != -1))
     return fail(FU_ERR_ARG, "fu_create: bad arguments");
+  const bool no_rev = f_extra == -1;
+  if (no_rev) f_extra = 0;
   if (e + f_extra >= (int64_t)INT32_MAX) return fail(FU_ERR_ARG, "fu_create: more than 2^31-1 edges");
   if (rowptr[0] != 0 || rowptr[n] != e) return fail(FU_ERR_ARG, "fu_create: rowptr[0] must be 0 and rowptr[n] == e");
   int ndev = 0;
@@ -1282,7 +1285,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   const int32_t na = n + a_extra;
   h->na = na;
   for (int64_t k = 0; k < e; ++k) {
-    if (col[k] < 0 || col[k] >= na || rev[k] < 0 || rev[k] >= fe) {
+    if (col[k] < 0 || col[k] >= na || (!no_rev && (rev[k] < 0 || rev[k] >= fe))) {
       delete h;
       return fail(FU_ERR_ARG, "fu_create: col/rev index out of range at edge " + std::to_string(k));
     }
@@ -1292,7 +1295,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   if ((rc = set_device(h))) return cleanup(rc);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
-  if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (rc = dmalloc(&h->rev, e)) ||
+  if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (!no_rev && (rc = dmalloc(&h->rev, e))) ||
       (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) ||
       (rc = dmalloc(&h->a[0], na)) || (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->target, n)) ||
       (rc = dmalloc(&h->err, 1)))
@@ -1300,7 +1303,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   h->errcap = 1;
   if (hipMemcpy(h->rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
       (e && hipMemcpy(h->col, col, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
-      (e && hipMemcpy(h->rev, rev, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
+      (e && !no_rev && hipMemcpy(h->rev, rev, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(h->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
   if (hipMemset(h->f[0], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
@@ -1349,6 +1352,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     if (value < 0 || value > 5) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..5");
     if (h->dist && value != 0 && value != 2 && value != 4)  // 5: single GPU only
       return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
+    if (!h->rev && h->E > 0 && value >= 1 && value <= 3)
+      return fail(FU_ERR_ARG, "fu_set_option: kernels 1-3 need the reverse-edge index (estimates-only halo)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     h->kernel = value == 0 ? 4 : (int)value;
     if (h->kernel == 3) return ensure_inbox(h);

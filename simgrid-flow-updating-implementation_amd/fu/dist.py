@@ -135,6 +135,60 @@ def ghost_f_gidx_owner_nodes(rowptr, gidx):
     return np.searchsorted(rowptr, gidx, side="right") - 1
 
 
+class RggPart:
+    """One rank's slab of the random geometric graph fu_graph_gen_rgg(n_total, radius, seed),
+    generated natively without the global graph (fu_part_gen_rgg), with the estimates-only
+    halo plan (kernel 4)."""
+
+    def __init__(self, n_total: int, radius: float | None = None, avg_deg: float = 8.0,
+                 seed: int = 1, nparts: int = 1, part: int = 0):
+        if radius is None:
+            radius = float(np.sqrt(avg_deg / (np.pi * n_total)))
+        out = L.vp()
+        L.call("fu_part_gen_rgg", int(n_total), float(radius), int(seed), int(nparts), int(part),
+               ctypes.byref(out))
+        self._h = out
+        info = np.zeros(8, dtype=np.int64)
+        L.call("fu_part_info", self._h, L.ptr(info))
+        (self.n_local, self.e_local, self.lo, self.hi, self.n_ghost_a, _, self.max_deg,
+         self.n_total) = (int(x) for x in info)
+        self.nparts, self.part, self.radius = nparts, part, radius
+        self.rowptr = np.empty(self.n_local + 1, dtype=np.int64)
+        self.col = np.empty(max(self.e_local, 1), dtype=np.int32)
+        self.ghost_gid = np.empty(max(self.n_ghost_a, 1), dtype=np.int64)
+        self.send_a_off = np.empty(nparts + 1, dtype=np.int64)
+        self.send_a_idx = np.empty(max(int(info[5]), 1), dtype=np.int32)
+        self.recv_a_off = np.empty(nparts + 1, dtype=np.int64)
+        L.call("fu_part_export", self._h, L.ptr(self.rowptr), L.ptr(self.col), L.ptr(self.ghost_gid),
+               L.ptr(self.send_a_off), L.ptr(self.send_a_idx), L.ptr(self.recv_a_off))
+        self.col = self.col[:self.e_local]
+        self.ghost_gid = self.ghost_gid[:self.n_ghost_a]
+        self.send_a_idx = self.send_a_idx[:int(info[5])]
+        L.lib.fu_part_free(self._h)
+        self._h = None
+
+    def global_col(self):
+        """Neighbour ids in global numbering (for checks)."""
+        c = self.col.astype(np.int64)
+        ghost = c >= self.n_local
+        out = c + self.lo
+        out[ghost] = self.ghost_gid[c[ghost] - self.n_local]
+        return out
+
+    def values(self, seed: int = 0, lo: float = 0.0, hi: float = 100.0):
+        out = np.empty(self.n_local)
+        L.call("fu_values_uniform_range", self.lo, self.n_local, int(seed), float(lo), float(hi),
+               L.ptr(out))
+        return out
+
+    def to_plan(self) -> Plan:
+        z = np.zeros(self.nparts + 1, dtype=np.int64)
+        return Plan(self.part, self.nparts, self.lo, self.hi, self.rowptr, self.col, None,
+                    self.n_ghost_a, 0, self.ghost_gid, np.zeros(0, dtype=np.int64), z,
+                    np.zeros(0, dtype=np.int32), z.copy(), self.send_a_off, self.send_a_idx,
+                    self.recv_a_off)
+
+
 def unique_id() -> bytes:
     buf = (ctypes.c_uint8 * 128)()
     L.call("fu_dist_unique_id", buf)
@@ -154,11 +208,12 @@ class DistCollectAll:
             raise ValueError("values_local must have n_local entries")
         keep = [plan.rowptr, plan.col, plan.rev, plan.send_f_off, plan.send_f_idx,
                 plan.recv_f_off, plan.send_a_off, plan.send_a_idx, plan.recv_a_off]
-        self._keep = [np.ascontiguousarray(x) for x in keep]
+        self._keep = [None if x is None else np.ascontiguousarray(x) for x in keep]
         (rp, c, r, sfo, sfi, rfo, sao, sai, rao) = self._keep
         idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         out = L.vp()
-        L.call("fu_dist_create", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c), L.ptr(r),
+        L.call("fu_dist_create", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c),
+               None if r is None else L.ptr(r),
                L.ptr(self.values), plan.n_ghost_a, plan.n_ghost_f, plan.nranks, plan.rank,
                L.ptr(sfo), L.ptr(sfi) if len(sfi) else None, L.ptr(rfo), L.ptr(sao),
                L.ptr(sai) if len(sai) else None, L.ptr(rao), idbuf, int(device),

@@ -160,3 +160,28 @@ def test_plan_shapes_and_symmetry():
         # local numbering in range
         assert p.col.max() < p.n_local + p.n_ghost_a
         assert p.rev.max() < p.e_local + p.n_ghost_f
+
+
+@pytest.mark.parametrize("nparts", [1, 2, 3, 5])
+def test_rgg_slab_generator_matches_global_and_partition(nparts):
+    """fu_part_gen_rgg: each rank's slab (built without the global graph) has the global
+    generator's rows, and the same ghost numbering / halo plan as fu.dist.partition with the
+    same node ranges."""
+    import fu
+    from fu.dist import RggPart
+
+    n, avg = 20000, 8.0
+    g = fu.Graph.random_geometric(n, avg_deg=avg, seed=7)
+    parts = [RggPart(n, avg_deg=avg, seed=7, nparts=nparts, part=p) for p in range(nparts)]
+    assert parts[0].lo == 0 and parts[-1].hi == n
+    bounds = [p.lo for p in parts] + [n]
+    for p in parts:
+        assert np.array_equal(p.rowptr, g.rowptr[p.lo:p.hi + 1] - g.rowptr[p.lo])
+        assert np.array_equal(p.global_col(), g.col[g.rowptr[p.lo]:g.rowptr[p.hi]])
+        ref = partition(g.rowptr, g.col, g.rev, nparts, p.part, bounds=bounds)
+        assert np.array_equal(p.col, ref.col)
+        assert np.array_equal(p.ghost_gid, ref.ghost_a_gid)
+        assert np.array_equal(p.send_a_off, ref.send_a_off)
+        assert np.array_equal(p.send_a_idx, ref.send_a_idx)
+        assert np.array_equal(p.recv_a_off, ref.recv_a_off)
+        assert np.array_equal(p.values(seed=3), fu.uniform_values(n, seed=3)[p.lo:p.hi])

@@ -257,3 +257,22 @@ def test_replay_with_faults_vs_c_oracle(persistent):
     assert np.array_equal(last, l_ref) and np.array_equal(flows, f_ref)
     for t in (60, 149, 299):
         assert np.array_equal(snaps[t], s_ref[t])
+
+
+def test_dist_rgg_slab_estimates_only_halo_matches_engine():
+    """The native slab generator + estimates-only halo (rev = NULL) at world size 1 equals
+    the single-GPU engine on the global graph, bitwise; kernels that need rev are refused."""
+    from fu.dist import DistCollectAll, RggPart, unique_id
+
+    n = 200_000
+    part = RggPart(n, avg_deg=8.0, seed=5, nparts=1, part=0)
+    v = part.values(seed=2)
+    d = DistCollectAll(part.to_plan(), v, unique_id())
+    with pytest.raises(fu.FuError, match="reverse-edge"):
+        d2 = DistCollectAll(part.to_plan(), v, unique_id(), kernel="tile")
+    d.run(40)
+    g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=5)
+    eng = fu.CollectAll(g, v)
+    eng.run(40)
+    assert np.array_equal(d.estimates(), eng.estimates())
+    assert np.array_equal(d.flows(), eng.flows())

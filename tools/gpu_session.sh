@@ -29,6 +29,7 @@ for s in $STEPS; do
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;
     rmat)   step bench_rmat 500 python bench.py --workload rmat --n 22 --no-conv --cpu-seconds 0 --steps 100 ;;
     ubench) step ubench 200 tools/bin/ubench_gather ;;
+    rggdist) step bench_rggdist 500 python bench.py --workload rgg-dist --n 8388608 --steps 300 ;;
     pmc)    step pmc 900 bash tools/pmc.sh ;;
     *) echo "unknown step $s" ;;
   esac
