@@ -93,7 +93,8 @@ int fu_create(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
 int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
                          fu_handle **out);
 /* Options: "kernel" (0 = auto = 4, 1 = thread-per-node, 2 = LDS tile (pull), 3 = push/inbox,
- *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch
+ *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch,
+ *          6 = 4 with the low half of each row staged by a gather launch
  *          (rows must be sorted by neighbour id)),
  * "hub_threshold" (degree above which a node gets a block; default 64),
  * "nt" (1 = non-temporal loads/stores for the streamed arrays of kernel 4; default 0). */

@@ -574,18 +574,41 @@ __global__ __launch_bounds__(kBlock) void k_gather_split(const int *__restrict__
   }
 }
 
+// Kernel 6: gather only part 0 (low half of the estimate table), every block, every XCD.
+__global__ __launch_bounds__(kBlock) void k_gather_part0(const int *__restrict__ col_pm,
+                                                         long long e0_count,
+                                                         const double *__restrict__ a_prev,
+                                                         double *__restrict__ G) {
+  constexpr int kPer = kGatherChunk / kBlock;
+  const long long base = (long long)blockIdx.x * kGatherChunk;
+  int c[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long e = base + threadIdx.x + k * kBlock;
+    c[k] = e < e0_count ? ld_stream(col_pm + e) : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long e = base + threadIdx.x + k * kBlock;
+    if (c[k] >= 0) G[e] = a_prev[c[k]];
+  }
+}
+
 // part-major index of canonical edge k (0-based position inside row t of the tile)
 __device__ inline int split_index(int k, int split_t, int p0, int p1) {
   return k < split_t ? p0 + k : p1 + (k - split_t);
 }
 
-template <bool CHECK>
+// GATHER1 (kernel 6): part-1 estimates are gathered here from a_prev (high half of the
+// table, 4 MB for ER-1M) instead of being read from G; only part 0 went through G.
+template <bool CHECK, bool GATHER1 = false>
 __global__ __launch_bounds__(kBlock) void k_round_split(
     const int4 *__restrict__ tiles, const int2 *__restrict__ tiles_g, const int *__restrict__ rowptr,
     const int *__restrict__ rowptr0, long long e0_count, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ G, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err) {
+    unsigned long long *__restrict__ err, const int *__restrict__ col_pm = nullptr,
+    const double *__restrict__ a_prev = nullptr) {
   __shared__ double s_x[kTileEdges];  // f_{r-2} on load, fr after phase B (canonical order)
   __shared__ double s_g[kTileEdges];  // a_{r-1}[col] in part-major order: part 0 | part 1
   __shared__ unsigned char s_own[kTileEdges];
@@ -608,7 +631,8 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     for (int c0 = b; c0 < e; c0 += kTileEdges) {
       const int cn = min(kTileEdges, e - c0);
       for (int q = t; q < cn; q += kBlock) {
-        const double er = G[split_index(c0 - b + q, split_i, p0, p1)];
+        const int gi = split_index(c0 - b + q, split_i, p0, p1);
+        const double er = (GATHER1 && c0 - b + q >= split_i) ? a_prev[col_pm[gi]] : G[gi];
         s_x[q] = recon_fr(F[c0 + q], er, own2);
         s_g[q] = er;
       }
@@ -630,7 +654,8 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     __syncthreads();
     const double a = s_a[0];
     for (int k = b + t; k < e; k += kBlock) {
-      const double er = G[split_index(k - b, split_i, p0, p1)];
+      const int gi = split_index(k - b, split_i, p0, p1);
+      const double er = (GATHER1 && k - b >= split_i) ? a_prev[col_pm[gi]] : G[gi];
       F[k] = (recon_fr(F[k], er, own2) + a) - er;
     }
     if (CHECK) block_max_to(eb, err);
@@ -651,7 +676,8 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     g[k] = 0.0;
     if (q < ne) {
       x[k] = F[e0 + q];
-      g[k] = q < n0 ? G[g0b + q] : G[g1b + (q - n0)];
+      if (GATHER1) g[k] = q < n0 ? G[g0b + q] : a_prev[col_pm[g1b + (q - n0)]];
+      else g[k] = q < n0 ? G[g0b + q] : G[g1b + (q - n0)];
     }
   }
   const int rp = t <= nn ? rowptr[nb + t] : 0;
@@ -1139,6 +1165,22 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
                            h->stream, h->n, h->a[0], h->target, err_slot);
+    } else if (h->kernel == 6) {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+      const unsigned gblocks = (unsigned)((h->e0_count + kGatherChunk - 1) / kGatherChunk);
+      if (gblocks)
+        hipLaunchKernelGGL(k_gather_part0, dim3(gblocks), dim3(kBlock), 0, h->stream, h->colpm,
+                           (long long)h->e0_count, ap, h->G);
+      if (check)
+        hipLaunchKernelGGL((k_round_split<true, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
+                           h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
+                           h->G, ap2, an, h->target, err_slot, h->colpm, ap);
+      else
+        hipLaunchKernelGGL((k_round_split<false, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
+                           h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
+                           h->G, ap2, an, h->target, err_slot, h->colpm, ap);
     } else if (h->kernel == 5) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -1349,8 +1391,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 5) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..5");
-    if (h->dist && value != 0 && value != 2 && value != 4)  // 5: single GPU only
+    if (value < 0 || value > 6) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..6");
+    if (h->dist && value != 0 && value != 2 && value != 4)  // 5, 6: single GPU only
       return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
     if (!h->rev && h->E > 0 && value >= 1 && value <= 3)
       return fail(FU_ERR_ARG, "fu_set_option: kernels 1-3 need the reverse-edge index (estimates-only halo)");
@@ -1358,7 +1400,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->kernel = value == 0 ? 4 : (int)value;
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4) return ensure_a2(h);
-    if (h->kernel == 5) {
+    if (h->kernel == 5 || h->kernel == 6) {
       if (int rc = ensure_a2(h)) return rc;
       if (int rc = ensure_split(h)) {
         h->kernel = 4;

@@ -16,7 +16,7 @@ import numpy as np
 from . import _lib as L
 from .graph import Graph
 
-KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5}
+KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 

@@ -15,7 +15,7 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["thread", "tile", "push", "recon", "split"]
+KERNELS = ["thread", "tile", "push", "recon", "split", "split2"]
 
 
 def _rows_sorted(rowptr, col):
@@ -25,7 +25,7 @@ def _rows_sorted(rowptr, col):
 def _check_fixture(meta, kernel, hub_threshold=None):
     d = load_npz(meta["file"])
     rounds = [int(r) for r in d["rounds"]]
-    if kernel == "split" and not _rows_sorted(d["rowptr"], d["col"]):
+    if kernel in ("split", "split2") and not _rows_sorted(d["rowptr"], d["col"]):
         with pytest.raises(fu.FuError, match="sorted"):
             fu.CollectAll(rowptr=d["rowptr"], col=d["col"], values=d["values"], kernel=kernel)
         return
@@ -46,7 +46,7 @@ def test_ca_sync_fixture_bitwise(name, meta, kernel):
     _check_fixture(meta, kernel)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2"])
 @pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
 def test_ca_sync_fixture_heavy_path(name, kernel):
     """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
@@ -65,7 +65,7 @@ def test_er_vs_c_oracle_bitwise(kernel):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2"])
 def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.rmat(15, 16, seed=2)
     assert g.max_deg > 2048  # exercises chunked heavy tiles

@@ -20,6 +20,7 @@ VARIANTS = {
     "recon": ("recon", {}),
     "recon_nt": ("recon", {"nt": 1}),
     "split": ("split", {}),
+    "split2": ("split2", {}),
     "recon_nobins": ("recon", {"bins": 0}),
     "recon_1024": ("recon", {"tile_edges": 1024}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
