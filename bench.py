@@ -101,8 +101,9 @@ def main():
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
-    eng.run(args.warmup)
+    eng.run(args.warmup)  # with kernel "auto" the first warmup rounds also pick the kernel
     eng.synchronize()
+    kinfo = eng.info()
 
     barrier()
     eng.synchronize()
@@ -164,6 +165,8 @@ def main():
                 "workload": wl,
                 "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
                 "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel,
+                "kernel_selected": kinfo["kernel"] + ("+nt" if kinfo["nt"] else ""),
+                "autotune_us_per_round": kinfo["tune_us_per_round"],
                 "parallelism": "independent graph per GPU" if world > 1 else "single GPU",
             },
             "roofline": {

@@ -117,6 +117,12 @@ int fu_get_estimates(fu_handle *h, double *a_out);
 /* Per-directed-edge flow f[e] = flows[col[e]] of node i (CA:117-118), CSR order. */
 int fu_get_flows(fu_handle *h, double *f_out);
 int fu_get_round(fu_handle *h, int64_t *rounds_done);
+/* info[0] = kernel in use, [1] = nt, [2] = autotune (0 off, 1 pending, 2 done),
+ * [3] = rounds done, [4..7] = tuned candidates' ns per round (4, 4+nt, 6, 5). With kernel
+ * "auto" (the default) the first fu_run_collectall with >= 12 rounds after round 0 times
+ * kernels 4, 4+nt, 6 and 5 on real rounds (they share state and are bitwise identical) and
+ * keeps the fastest. */
+int fu_get_info(fu_handle *h, int64_t info[8]);
 int fu_synchronize(fu_handle *h);
 int fu_destroy(fu_handle *h);
 

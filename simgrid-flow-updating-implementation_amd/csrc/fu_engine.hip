@@ -964,6 +964,9 @@ struct fu_handle {
   int kernel = 4;
   int hub_threshold = 64;
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
+  bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
+  bool tuned = false;
+  float tune_ms[4] = {0, 0, 0, 0};
   int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_col;  // host copy (column-split preparation)
@@ -1398,6 +1401,9 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       return fail(FU_ERR_ARG, "fu_set_option: kernels 1-3 need the reverse-edge index (estimates-only halo)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     h->kernel = value == 0 ? 4 : (int)value;
+    h->autotune = value == 0;
+    h->tuned = false;
+    h->nt = 0;
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4) return ensure_a2(h);
     if (h->kernel == 5 || h->kernel == 6) {
@@ -1467,6 +1473,53 @@ int fu__err_slots(fu_handle *h, int count) {
   return FU_OK;
 }
 
+// Kernels 4, 5 and 6 share the state layout (F[r & 1], A[r % 3]) and are all bitwise
+// exact, so switching between them mid-run changes nothing but speed. "auto" times each
+// candidate on real rounds (1 warm + 2 timed each) once round 0 is done and keeps the
+// fastest. The rounds count toward the caller's total, and the results are unchanged.
+static int autotune_kernel(fu_handle *h, int32_t *budget) {
+  struct Cand {
+    int kernel, nt;
+  };
+  std::vector<Cand> cands = {{4, 0}, {4, 1}};
+  if (!h->dist) {
+    cands.push_back({6, 0});
+    cands.push_back({5, 0});
+  }
+  const int32_t need = 3 * (int32_t)cands.size();
+  if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
+  float best = 1e30f;
+  int bi = -1;
+  for (size_t c = 0; c < cands.size(); ++c) {
+    if (cands[c].kernel >= 5) {
+      if (ensure_split(h) != FU_OK) {  // rows not sorted: column split not applicable
+        set_error("");
+        continue;
+      }
+    }
+    h->kernel = cands[c].kernel;
+    h->nt = cands[c].nt;
+    if (int rc = launch_round(h, nullptr)) return rc;
+    HIP_TRY(hipEventRecord(h->ev0, h->stream));
+    for (int k = 0; k < 2; ++k)
+      if (int rc = launch_round(h, nullptr)) return rc;
+    HIP_TRY(hipEventRecord(h->ev1, h->stream));
+    HIP_TRY(hipEventSynchronize(h->ev1));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
+    if (c < 4) h->tune_ms[c] = ms / 2;
+    *budget -= 3;
+    if (ms < best) {
+      best = ms;
+      bi = (int)c;
+    }
+  }
+  h->kernel = cands[bi].kernel;
+  h->nt = cands[bi].nt;
+  h->tuned = true;
+  return FU_OK;
+}
+
 int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *err_trace) {
   FU_TRY_BEGIN
   if (!h || rounds < 0) return fail(FU_ERR_ARG, "fu_run_collectall: bad arguments");
@@ -1478,6 +1531,13 @@ int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *e
     HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(unsigned long long) * nerr, h->stream));
   }
   for (int32_t r = 0; r < rounds; ++r) {
+    // tune between rounds when no error slot is pending in the rounds it would consume
+    if (h->autotune && !h->tuned && h->kernel >= 4 && h->rounds >= 1 && nerr == 0) {
+      int32_t budget = rounds - r;
+      if (int rc = autotune_kernel(h, &budget)) return rc;
+      r = rounds - budget;
+      if (r >= rounds) break;
+    }
     unsigned long long *slot = nullptr;
     if (nerr > 0 && (r + 1) % err_every == 0) slot = h->err + ((r + 1) / err_every - 1);
     if (int rc = launch_round(h, slot)) return rc;
@@ -1549,6 +1609,16 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   }
   HIP_TRY(hipMemcpyAsync(f_out, src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
+  return FU_OK;
+}
+
+int fu_get_info(fu_handle *h, int64_t info[8]) {
+  if (!h || !info) return fail(FU_ERR_ARG, "fu_get_info: NULL argument");
+  info[0] = h->kernel;
+  info[1] = h->nt;
+  info[2] = h->autotune ? (h->tuned ? 2 : 1) : 0;
+  info[3] = h->rounds;
+  for (int k = 0; k < 4; ++k) info[4 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
   return FU_OK;
 }
 

@@ -96,6 +96,16 @@ class CollectAll:
         L.call("fu_get_flows", self._h, L.ptr(f))
         return f[:self.E]
 
+    def info(self) -> dict:
+        """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
+        a = np.zeros(8, dtype=np.int64)
+        L.call("fu_get_info", self._h, L.ptr(a))
+        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2"}
+        return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
+                "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
+                "tune_us_per_round": {k: a[4 + i] / 1e3 for i, k in
+                                      enumerate(("recon", "recon_nt", "split2", "split"))}}
+
     @property
     def rounds_done(self) -> int:
         r = L.i64()

@@ -276,3 +276,19 @@ def test_dist_rgg_slab_estimates_only_halo_matches_engine():
     eng.run(40)
     assert np.array_equal(d.estimates(), eng.estimates())
     assert np.array_equal(d.flows(), eng.flows())
+
+
+def test_autotune_switches_kernels_bitwise():
+    """kernel="auto" times kernels 4, 4+nt, 6, 5 on real rounds and keeps the fastest; the
+    switch happens mid-run and must not change a single bit."""
+    g = fu.Graph.erdos_renyi(300_000, 1_200_000, seed=8)
+    v = fu.uniform_values(g.n, seed=8)
+    eng = fu.CollectAll(g, v)
+    assert eng.info()["autotune"] == "pending"
+    eng.run(30)
+    info = eng.info()
+    assert info["autotune"] == "done" and info["rounds"] == 30
+    assert all(t > 0 for t in info["tune_us_per_round"].values())
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=8)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
