@@ -1668,6 +1668,7 @@ struct fu_replay {
   double2 *msg = nullptr;
   // persistent mode (built on first use)
   int persistent = 0;
+  unsigned pers_blocks = 1;
   std::vector<int32_t> h_tasks, h_events, h_out_ids;
   long long *node_off = nullptr, *cursor = nullptr;
   int4 *node_ev = nullptr;
@@ -1737,6 +1738,12 @@ static int replay_build_persistent(fu_replay *r) {
                      (long long)(2 * std::max<int64_t>(U, 1)), sentinel, reinterpret_cast<double *>(r->pay));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(r->stream));
+  int per_cu = 0, ncu = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_persist, kBlock, 0));
+  HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, r->device));
+  // stay below the occupancy bound (the API can over-report by one block per CU)
+  const long long cap = std::max(1LL, (long long)std::max(1, per_cu - 1) * ncu);
+  r->pers_blocks = (unsigned)std::min<long long>(cap, grid_for(r->n));
   r->pers_ready = true;
   return FU_OK;
 }
@@ -1837,13 +1844,7 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
     }
     HIP_TRY(hipMemsetAsync(r->scur, 0, sizeof(int) * r->n, r->stream));
     HIP_TRY(hipMemsetAsync(r->status, 0, sizeof(int), r->stream));
-    int per_cu = 0, ncu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_replay_persist, kBlock, 0));
-    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, r->device));
-    // stay below the occupancy bound (the API can over-report by one block per CU)
-    const long long cap = std::max(1LL, (long long)std::max(1, per_cu - 1) * ncu);
-    const unsigned blocks = (unsigned)std::min<long long>(cap, grid_for(r->n));
-    hipLaunchKernelGGL(k_replay_persist, dim3(blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
+    hipLaunchKernelGGL(k_replay_persist, dim3(r->pers_blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
                        r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v, r->flow,
                        r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
                        (long long)1 << 22);
@@ -1925,7 +1926,10 @@ int fu_replay_set_option(fu_replay *r, const char *key, int64_t value) {
   if (!std::strcmp(key, "persistent")) {
     if (r->cur_tick != 0) return fail(FU_ERR_STATE, "fu_replay_set_option: persistent must be set before the first tick");
     r->persistent = value != 0;
-    return FU_OK;
+    if (!r->persistent) return FU_OK;
+    // build the per-node event lists now, so that no host work lands inside a timed run
+    HIP_TRY(hipSetDevice(r->device));
+    return replay_build_persistent(r);
   }
   return fail(FU_ERR_ARG, std::string("fu_replay_set_option: unknown key '") + key + "'");
 }

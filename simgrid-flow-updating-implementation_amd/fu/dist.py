@@ -199,7 +199,7 @@ class DistCollectAll:
     """One rank of a partitioned collect-all run (RCCL halo exchange every round)."""
 
     def __init__(self, plan: Plan, values_local, uid: bytes, device: int = 0,
-                 kernel: str = "tile"):
+                 kernel: str = "auto"):
         from .engine import KERNELS
 
         self.plan = plan
