@@ -102,18 +102,30 @@ def main():
     t_gen = time.perf_counter() - t_gen
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
     eng.run(args.warmup)  # with kernel "auto" the first warmup rounds also pick the kernel
+    eng.reset()           # the timed region is rounds 0 .. steps-1 from the zero state
     eng.synchronize()
-    kinfo = eng.info()
 
+    # Timed in <= 10 chunks (HIP events on the engine's own stream) to show how the round
+    # time evolves: the packed estimate table engages as the estimates converge, and the
+    # autotuner re-runs (on real rounds, inside the timed region) when its width changes.
+    nchunk = min(10, args.steps)
+    bounds = [args.steps * k // nchunk for k in range(nchunk + 1)]
     barrier()
     eng.synchronize()
     t0 = time.perf_counter()
-    kern_ms = eng.run_timed(args.steps)  # HIP events on the engine's own stream
+    chunk_ms, chunk_pack = [], []
+    for k in range(nchunk):
+        chunk_ms.append(eng.run_timed(bounds[k + 1] - bounds[k]))
+        chunk_pack.append(eng.pack_widths()[2])
     eng.synchronize()
     t1 = time.perf_counter()
     barrier()
     wall = allmax(t1 - t0)
-    kern_ms = allmax(kern_ms)
+    kern_ms = allmax(sum(chunk_ms))
+    kinfo = eng.info()
+    phases = [{"rounds": [bounds[k], bounds[k + 1]],
+               "us_per_round": chunk_ms[k] * 1e3 / max(1, bounds[k + 1] - bounds[k]),
+               "pack_width_after": chunk_pack[k]} for k in range(nchunk)]
 
     edges_total = g.E * world
     value = edges_total * args.steps / wall
@@ -166,7 +178,10 @@ def main():
                 "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
                 "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel,
                 "kernel_selected": kinfo["kernel"] + ("+nt" if kinfo["nt"] else ""),
+                "tile_selected": kinfo["tile"],
+                "autotune_passes": kinfo["tune_passes"],
                 "autotune_us_per_round": kinfo["tune_us_per_round"],
+                "phases": phases,
                 "parallelism": "independent graph per GPU" if world > 1 else "single GPU",
             },
             "roofline": {
@@ -178,6 +193,7 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_us": avg_launch_s * 1e6,
+                "last_phase_frac": alg_bytes / (phases[-1]["us_per_round"] * 1e-6) / 1e9 / HBM_PEAK_GBS,
             },
             "cpu_baseline": cpu,
             "rounds_to_1e-9": rounds_to,

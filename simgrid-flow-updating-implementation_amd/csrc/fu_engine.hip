@@ -280,6 +280,116 @@ __global__ __launch_bounds__(kBlock) void k_round_push(
 }
 
 // ------------------------------------------------------------------------------------
+// Packed estimate table (kernel 4). Once the estimates have converged into a narrow
+// cluster, the neighbour gather reads a W-bit code per node (W = 8, 16 or 32) instead of
+// the 8-byte double: a 1-4 MB table instead of 8 MB for ER-1M, so the random gathers hit
+// the XCD's L2. The code is a LOSSLESS offset of the double's order-preserving 64-bit key
+// from a per-table base: key(x) - base in [0, 2^W - 2]. Any estimate outside that window
+// is stored as the escape code 2^W - 1, and its reader gathers the double instead. Every
+// decoded value is the exact bit pattern, so the results are unchanged. Each round writes
+// the doubles (coalesced, always) and, when packing is on, the codes under the parameters
+// pack_plan chose from a sample of gather targets. Slots: ctl[r & 1] describes the code
+// table written in round r (copied by block 0 from ctl[2], the current encoding plan);
+// width 0 = no codes (the reader gathers the doubles).
+// ------------------------------------------------------------------------------------
+struct PackCtl {
+  unsigned long long base;
+  int width;
+  int pad;
+};
+
+__device__ inline unsigned long long dkey(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+__device__ inline double dkey_inv(unsigned long long k) {
+  const unsigned long long b = (k >> 63) ? (k & ~(1ull << 63)) : ~k;
+  return __longlong_as_double((long long)b);
+}
+template <int W>
+__device__ inline unsigned ld_code(const void *tab, int i) {
+  if constexpr (W == 8) return reinterpret_cast<const unsigned char *>(tab)[i];
+  else if constexpr (W == 16) return reinterpret_cast<const unsigned short *>(tab)[i];
+  else return reinterpret_cast<const unsigned *>(tab)[i];
+}
+__device__ inline void put_code(const PackCtl &pc, void *tab, int i, double a) {
+  const unsigned long long off = dkey(a) - pc.base;
+  const unsigned esc = pc.width == 32 ? 0xFFFFFFFFu : (1u << pc.width) - 1u;
+  const unsigned cd = off < (unsigned long long)esc ? (unsigned)off : esc;
+  if (pc.width == 8) reinterpret_cast<unsigned char *>(tab)[i] = (unsigned char)cd;
+  else if (pc.width == 16) reinterpret_cast<unsigned short *>(tab)[i] = (unsigned short)cd;
+  else reinterpret_cast<unsigned *>(tab)[i] = cd;
+}
+template <int W>
+__device__ inline double decode_or(unsigned cd, unsigned long long base, const double *a_prev, int j) {
+  constexpr unsigned esc = W == 32 ? 0xFFFFFFFFu : (1u << W) - 1u;
+  return cd == esc ? a_prev[j] : dkey_inv(base + cd);
+}
+// One neighbour estimate a_{r-1}[j] under the table's packing (uniform branch).
+__device__ inline double ld_est(const PackCtl &pp, const void *codes, const double *a_prev, int j) {
+  if (pp.width == 8) return decode_or<8>(ld_code<8>(codes, j), pp.base, a_prev, j);
+  if (pp.width == 16) return decode_or<16>(ld_code<16>(codes, j), pp.base, a_prev, j);
+  if (pp.width == 32) return decode_or<32>(ld_code<32>(codes, j), pp.base, a_prev, j);
+  return a_prev[j];
+}
+// The light tile's kPer neighbour estimates: all code loads first, then decode (escapes
+// gather the double).
+template <int W, int KP>
+__device__ inline void gather_packed(const int (&c)[KP], double (&g)[KP], int t, int ne,
+                                     const void *codes, unsigned long long base,
+                                     const double *a_prev) {
+  unsigned cd[KP];
+#pragma unroll
+  for (int k = 0; k < KP; ++k) cd[k] = t + k * kBlock < ne ? ld_code<W>(codes, c[k]) : 0u;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) g[k] = t + k * kBlock < ne ? decode_or<W>(cd[k], base, a_prev, c[k]) : 0.0;
+}
+// Encoding plan from the estimates a_r of a fixed sample of gather targets: the centre is
+// the median of the first 64 sampled keys; the width is the smallest W whose window
+// [centre - 2^(W-1), centre + 2^(W-1) - 2] holds >= 99.5 % of the sample; else 0 (off).
+__global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__ a,
+                                                      const int *__restrict__ sample, int ns,
+                                                      PackCtl *__restrict__ ctl) {
+  __shared__ unsigned long long s_centre;
+  __shared__ int s_cnt[3];
+  const int t = threadIdx.x;
+  if (t < 3) s_cnt[t] = 0;
+  if (t < 64) {
+    const int m = min(ns, 64);
+    const unsigned long long k = t < m ? dkey(a[sample[t]]) : ~0ull;
+    int below = 0;
+    for (int l = 0; l < m; ++l) {
+      const unsigned long long o = __shfl(k, l, 64);
+      below += (o < k) || (o == k && l < t);
+    }
+    if (t < m && below == m / 2) s_centre = k;
+  }
+  __syncthreads();
+  const unsigned long long c = s_centre;
+  int n8 = 0, n16 = 0, n32 = 0;
+  for (int i = t; i < ns; i += kBlock) {
+    const unsigned long long k = dkey(a[sample[i]]);
+    const unsigned long long d = k >= c ? k - c : c - k;
+    n8 += d + 2 <= (1ull << 7);
+    n16 += d + 2 <= (1ull << 15);
+    n32 += d + 2 <= (1ull << 31);
+  }
+  atomicAdd(&s_cnt[0], n8);
+  atomicAdd(&s_cnt[1], n16);
+  atomicAdd(&s_cnt[2], n32);
+  __syncthreads();
+  if (t == 0) {
+    const int need = ns - ns / 200;
+    const int w = s_cnt[0] >= need ? 8 : s_cnt[1] >= need ? 16 : s_cnt[2] >= need ? 32 : 0;
+    PackCtl p;
+    p.base = w ? c - (1ull << (w - 1)) : 0;
+    p.width = w;
+    p.pad = 0;
+    ctl[2] = p;
+  }
+}
+
+// ------------------------------------------------------------------------------------
 // Variant 4: flow reconstruction ("recon"). Node j computed, in round r-1,
 //     f_{r-1}[j->i] = ((-f_{r-2}[i->j]) + a_{r-1}[j]) - a_{r-2}[i]        (CA:99, CA:117)
 // from three operands that node i also holds: its own previous flow f_{r-2}[i->j] (its
@@ -312,8 +422,13 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
     const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, const int *__restrict__ perm) {
+    unsigned long long *__restrict__ err, const int *__restrict__ perm,
+    const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
+    int rslot) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
+  const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
+  const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
   __shared__ double s_x[TE];   // f_{r-2} on load, fr after phase B
   __shared__ double s_er[TE];  // a_{r-1}[col e]
   __shared__ unsigned char s_own[TE];
@@ -358,7 +473,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         const int r = q >> lgC, k = q & (C - 1);
         if (c0 + k < s_deg[r]) {
           const int e = s_rb[r] + c0 + k;
-          const double er = a_prev[col[e]];
+          const double er = ld_est(pp, code_prev, a_prev, col[e]);
           const int slot = (r << lgC) + (k ^ sw(r));
           s_x[slot] = recon_fr(F[e], er, s_own2[r]);
           s_er[slot] = er;
@@ -380,6 +495,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const int node = s_node[t];
       a_mine = ((v[node] - S) + T) / (double)(my_deg + 1);
       a_new[node] = a_mine;
+      if (pc.width) put_code(pc, code_new, node, a_mine);
       if (CHECK) eb = err_bits(a_mine, target[node]);
     }
     __syncthreads();  // every read of s_own2 (aliases s_a) is done
@@ -398,7 +514,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         const int rb = s_rb[r], d = s_deg[r];
         const double own2 = a_prev2[s_node[r]], a = s_a[r];
         for (int k = t; k < d; k += kBlock) {
-          const double er = a_prev[col[rb + k]];
+          const double er = ld_est(pp, code_prev, a_prev, col[rb + k]);
           F[rb + k] = (recon_fr(F[rb + k], er, own2) + a) - er;
         }
       }
@@ -417,7 +533,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     for (int c0 = b; c0 < e; c0 += TE) {
       const int cn = min(TE, e - c0);
       for (int q = t; q < cn; q += kBlock) {
-        const double er = a_prev[col[c0 + q]];
+        const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
         s_x[q] = recon_fr(F[c0 + q], er, own2);
         s_er[q] = er;
       }
@@ -434,12 +550,13 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const double a = ((v[i] - S) + T) / (double)(e - b + 1);
       s_a[0] = a;
       a_new[i] = a;
+      if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
     __syncthreads();
     const double a = s_a[0];
     for (int k = b + t; k < e; k += kBlock) {
-      const double er = a_prev[col[k]];
+      const double er = ld_est(pp, code_prev, a_prev, col[k]);
       F[k] = (recon_fr(F[k], er, own2) + a) - er;
     }
     if (CHECK) block_max_to(eb, err);
@@ -474,14 +591,22 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
   const double vv = t < nn ? v[nb + t] : 0.0;
   const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
+  if (DIAG != 0 || pp.width == 0) {
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    g[k] = 0.0;
-    if (q < ne) {
-      const int gi = DIAG == 1 ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
-      g[k] = a_prev[gi];
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      g[k] = 0.0;
+      if (q < ne) {
+        const int gi = DIAG == 1 ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
+        g[k] = a_prev[gi];
+      }
     }
+  } else if (pp.width == 8) {
+    gather_packed<8>(c, g, t, ne, code_prev, pp.base, a_prev);
+  } else if (pp.width == 16) {
+    gather_packed<16>(c, g, t, ne, code_prev, pp.base, a_prev);
+  } else {
+    gather_packed<32>(c, g, t, ne, code_prev, pp.base, a_prev);
   }
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
@@ -511,6 +636,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
     a_new[nb + t] = a;
+    if (pc.width) put_code(pc, code_new, nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
   __syncthreads();
@@ -607,8 +733,9 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     const int *__restrict__ rowptr0, long long e0_count, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ G, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, const int *__restrict__ col_pm = nullptr,
-    const double *__restrict__ a_prev = nullptr) {
+    unsigned long long *__restrict__ err, PackCtl *__restrict__ ctl, int rslot,
+    const int *__restrict__ col_pm = nullptr, const double *__restrict__ a_prev = nullptr) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot].width = 0;  // a_r is not packed
   __shared__ double s_x[kTileEdges];  // f_{r-2} on load, fr after phase B (canonical order)
   __shared__ double s_g[kTileEdges];  // a_{r-1}[col] in part-major order: part 0 | part 1
   __shared__ unsigned char s_own[kTileEdges];
@@ -945,7 +1072,8 @@ int dmalloc(T **p, size_t count) {
 struct fu_handle {
   int device = 0;
   hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
+  hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
@@ -966,7 +1094,12 @@ struct fu_handle {
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
   bool tuned = false;
-  float tune_ms[4] = {0, 0, 0, 0};
+  float tune_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
+  int tuned_width = 0;    // packing width the last pass ran under
+  int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
+  hipEvent_t ev_pw = nullptr;
+  bool pw_pending = false;
   int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_col;  // host copy (column-split preparation)
@@ -979,10 +1112,20 @@ struct fu_handle {
   int64_t e0_count = 0;
   int4 *tiles = nullptr;  // 2048-edge tiles (kernels 2, 3)
   int ntiles = 0;
-  int4 *tiles_r = nullptr;  // kernel 4 tiles (geometry: tile_edges)
-  int ntiles_r = 0;
+  // kernel 4 tiles per geometry (0 = 2048x256, 1 = 1024x128, 2 = 1024x256, 3 = 512x64 edges x
+  // nodes); all four are built up front so autotuning can switch geometry between rounds
+  int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
+  int ntiles_geo[4] = {0, 0, 0, 0};
+  int geo = 0;
   int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
-  int bins = 1;         // kernel 4: degree bins for rows above hub_threshold
+  int bins = 0;         // kernel 4 (geometry 0): degree bins for rows above hub_threshold
+  // kernel 4 packed estimate table (see PackCtl): code[r & 1] = codes of a_r
+  unsigned char *code[2] = {nullptr, nullptr};
+  PackCtl *pctl = nullptr;  // [0], [1]: per code table; [2]: current encoding plan
+  int *psample = nullptr;   // gather targets sampled for the plan
+  int n_psample = 0;
+  int pack = 1;             // 0 = off
+  int pack_every = 8;       // rounds between encoding plans
   int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
   int tile_nodes = 0;
   bool has_target = false;
@@ -1061,23 +1204,31 @@ int build_tiles_binned(fu_handle *h) {
     light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
   all.insert(all.end(), light.begin(), light.end());
-  if (h->tiles_r) hipFree(h->tiles_r);
+  if (h->tiles_geo[0]) hipFree(h->tiles_geo[0]);
   if (h->perm) hipFree(h->perm);
-  h->tiles_r = nullptr;
+  h->tiles_geo[0] = nullptr;
   h->perm = nullptr;
-  h->ntiles_r = (int)all.size();
-  if (int rc = dmalloc(&h->tiles_r, all.size())) return rc;
+  h->ntiles_geo[0] = (int)all.size();
+  if (int rc = dmalloc(&h->tiles_geo[0], all.size())) return rc;
   if (int rc = dmalloc(&h->perm, std::max<size_t>(1, heavy.size()))) return rc;
-  HIP_TRY(hipMemcpy(h->tiles_r, all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->tiles_geo[0], all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
   if (!heavy.empty()) HIP_TRY(hipMemcpy(h->perm, heavy.data(), sizeof(int32_t) * heavy.size(), hipMemcpyHostToDevice));
   return FU_OK;
 }
 
+constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
+constexpr int kGeoNodes[4] = {256, 128, 256, 64};
+
 int build_tiles(fu_handle *h) {
   if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
-  if (h->bins && h->tile_edges == 2048) return build_tiles_binned(h);
-  const int te = h->tile_edges, tn = te == 2048 ? 256 : te == 1024 ? (h->tile_nodes ? h->tile_nodes : 128) : 64;
-  return build_tiles_geom(h, te, tn, &h->tiles_r, &h->ntiles_r);
+  for (int g = 0; g < 4; ++g) {
+    if (g == 0 && h->bins) {
+      if (int rc = build_tiles_binned(h)) return rc;
+      continue;
+    }
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g])) return rc;
+  }
+  return FU_OK;
 }
 
 // Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
@@ -1165,6 +1316,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         hipLaunchKernelGGL(k_fill, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
                            -0.0, h->f[1]);
       HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
+      HIP_TRY(hipMemsetAsync(h->pctl, 0, sizeof(PackCtl) * 3, h->stream));      // no codes yet
       if (check)
         hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
                            h->stream, h->n, h->a[0], h->target, err_slot);
@@ -1179,11 +1331,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL((k_round_split<true, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
                            h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
-                           h->G, ap2, an, h->target, err_slot, h->colpm, ap);
+                           h->G, ap2, an, h->target, err_slot, h->pctl, (int)(r & 1), h->colpm, ap);
       else
         hipLaunchKernelGGL((k_round_split<false, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
                            h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
-                           h->G, ap2, an, h->target, err_slot, h->colpm, ap);
+                           h->G, ap2, an, h->target, err_slot, h->pctl, (int)(r & 1), h->colpm, ap);
     } else if (h->kernel == 5) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -1197,23 +1349,24 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL(k_round_split<true>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
                            h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
-                           h->target, err_slot);
+                           h->target, err_slot, h->pctl, (int)(r & 1));
       else
         hipLaunchKernelGGL(k_round_split<false>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
                            h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
-                           h->target, err_slot);
+                           h->target, err_slot, h->pctl, (int)(r & 1));
     } else {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
-  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_r), dim3(kBlock), 0, h->stream, \
-                     h->tiles_r, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm)
+  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_geo[h->geo]), dim3(kBlock), 0, \
+                     h->stream, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
+                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1))
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
-    if (h->tile_edges == 2048) FU_RECON_G(C, N, D, 2048, 256);                              \
-    else if (h->tile_edges == 1024 && h->tile_nodes == 256) FU_RECON_G(C, N, D, 1024, 256); \
-    else if (h->tile_edges == 1024) FU_RECON_G(C, N, D, 1024, 128);                         \
+    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
+    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                   \
+    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                   \
     else FU_RECON_G(C, N, D, 512, 64);                                                      \
   } while (0)
       if (h->diag == 1) FU_RECON(false, false, 1);
@@ -1272,6 +1425,17 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   HIP_TRY(hipGetLastError());
   h->cur = dst;
   h->rounds++;
+  // refresh the packing plan from a_r (kernel 4 encodes with it from the next round on)
+  if (h->kernel >= 4 && h->pack && !h->dist && h->n_psample > 0 && h->rounds % h->pack_every == 0) {
+    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample,
+                       h->n_psample, h->pctl);
+    HIP_TRY(hipGetLastError());
+    if (!h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
+      HIP_TRY(hipMemcpyAsync(h->h_pw, &h->pctl[2].width, sizeof(int), hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(hipEventRecord(h->ev_pw, h->stream));
+      h->pw_pending = true;
+    }
+  }
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 1)) return rc;
   }
@@ -1339,7 +1503,13 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   auto cleanup = [&](int code) { fu_destroy(h); return code; };
   if ((rc = set_device(h))) return cleanup(rc);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
-  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
+  if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
+      hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
+  if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
+    return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
+  *h->h_pw = 0;
   if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (!no_rev && (rc = dmalloc(&h->rev, e))) ||
       (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) ||
       (rc = dmalloc(&h->a[0], na)) || (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->target, n)) ||
@@ -1358,6 +1528,19 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
   if ((rc = build_tiles(h))) return cleanup(rc);
   if ((rc = ensure_a2(h))) return cleanup(rc);
+  if ((rc = dmalloc(&h->pctl, 3)) || (rc = dmalloc(&h->code[0], 4 * (size_t)na)) ||
+      (rc = dmalloc(&h->code[1], 4 * (size_t)na)))
+    return cleanup(rc);
+  if (hipMemset(h->pctl, 0, sizeof(PackCtl) * 3) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
+  if (e > 0) {  // plan sample: the targets of 4096 pseudo-random edges (degree-weighted)
+    const int ns = 4096;
+    std::vector<int32_t> smp(ns);
+    for (int q = 0; q < ns; ++q) smp[q] = col[splitmix_at(0x9ac4u, (uint64_t)q) % (uint64_t)e];
+    if ((rc = dmalloc(&h->psample, ns))) return cleanup(rc);
+    if (hipMemcpy(h->psample, smp.data(), sizeof(int32_t) * ns, hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
+    h->n_psample = ns;
+  }
   *out = h;
   return FU_OK;
   FU_TRY_END
@@ -1423,6 +1606,16 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->nt = value != 0;
     return FU_OK;
   }
+  if (!std::strcmp(key, "pack")) {
+    h->pack = value != 0;
+    if (!h->pack) HIP_TRY(hipMemsetAsync(h->pctl + 2, 0, sizeof(PackCtl), h->stream));  // stop encoding
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "pack_every")) {
+    if (value < 1 || value > (1 << 20)) return fail(FU_ERR_ARG, "fu_set_option: pack_every must be in [1, 2^20]");
+    h->pack_every = (int)value;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "bins")) {
     h->bins = value != 0;
     return build_tiles(h);
@@ -1430,12 +1623,14 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!std::strcmp(key, "tile_edges")) {
     if (value != 2048 && value != 1024 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: tile_edges must be 2048, 1024 or 512");
     h->tile_edges = (int)value;
-    return build_tiles(h);
+    h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
+    return FU_OK;
   }
   if (!std::strcmp(key, "tile_nodes")) {
     if (value != 0 && value != 128 && value != 256) return fail(FU_ERR_ARG, "fu_set_option: tile_nodes must be 0, 128 or 256");
     h->tile_nodes = (int)value;
-    return build_tiles(h);
+    h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
+    return FU_OK;
   }
   if (!std::strcmp(key, "hub_threshold")) {
     if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: hub_threshold must be >= 1");
@@ -1474,23 +1669,28 @@ int fu__err_slots(fu_handle *h, int count) {
 }
 
 // Kernels 4, 5 and 6 share the state layout (F[r & 1], A[r % 3]) and are all bitwise
-// exact, so switching between them mid-run changes nothing but speed. "auto" times each
-// candidate on real rounds (1 warm + 2 timed each) once round 0 is done and keeps the
-// fastest. The rounds count toward the caller's total, and the results are unchanged.
+// exact, so switching between them (or between kernel 4's tile geometries) mid-run changes
+// nothing but speed. "auto" times each candidate on real rounds (1 warm + 2 timed each)
+// once round 0 is done and keeps the fastest. The rounds count toward the caller's total,
+// and the results are unchanged. The pass re-runs when the packing plan changes width (the
+// packed gather shifts the balance between the candidates), at most kMaxTunes times.
+constexpr int kMaxTunes = 4;
+
 static int autotune_kernel(fu_handle *h, int32_t *budget) {
   struct Cand {
-    int kernel, nt;
+    int kernel, nt, geo;
   };
-  std::vector<Cand> cands = {{4, 0}, {4, 1}};
+  std::vector<Cand> cands = {{4, 0, 0}, {4, 1, 0}, {4, 0, 2}, {4, 0, 3}};
   if (!h->dist) {
-    cands.push_back({6, 0});
-    cands.push_back({5, 0});
+    cands.push_back({6, 0, 0});
+    cands.push_back({5, 0, 0});
   }
   const int32_t need = 3 * (int32_t)cands.size();
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
   int bi = -1;
   for (size_t c = 0; c < cands.size(); ++c) {
+    h->tune_ms[c] = 0.f;
     if (cands[c].kernel >= 5) {
       if (ensure_split(h) != FU_OK) {  // rows not sorted: column split not applicable
         set_error("");
@@ -1499,6 +1699,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
     }
     h->kernel = cands[c].kernel;
     h->nt = cands[c].nt;
+    h->geo = cands[c].geo;
     if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     for (int k = 0; k < 2; ++k)
@@ -1507,7 +1708,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
     HIP_TRY(hipEventSynchronize(h->ev1));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-    if (c < 4) h->tune_ms[c] = ms / 2;
+    h->tune_ms[c] = ms / 2;
     *budget -= 3;
     if (ms < best) {
       best = ms;
@@ -1516,7 +1717,37 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   }
   h->kernel = cands[bi].kernel;
   h->nt = cands[bi].nt;
+  h->geo = cands[bi].geo;
   h->tuned = true;
+  h->n_tunes++;
+  return FU_OK;
+}
+
+// After each packing plan the host keeps an asynchronous copy of its width; a changed width
+// re-arms the autotuner (checked without blocking).
+static void poll_pack_width(fu_handle *h) {
+  if (!h->pw_pending || hipEventQuery(h->ev_pw) != hipSuccess) return;
+  h->pw_pending = false;
+  if (h->autotune && h->tuned && *h->h_pw != h->tuned_width && h->n_tunes < kMaxTunes) h->tuned = false;
+}
+
+// The round loop shared by fu_run_collectall and fu_run_collectall_timed.
+static int run_rounds(fu_handle *h, int32_t rounds, int32_t err_every, int nerr) {
+  for (int32_t r = 0; r < rounds; ++r) {
+    poll_pack_width(h);
+    // tune between rounds when no error slot is pending in the rounds it would consume
+    if (h->autotune && !h->tuned && h->kernel >= 4 && h->rounds >= 1 && nerr == 0) {
+      int32_t budget = rounds - r;
+      const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
+      if (int rc = autotune_kernel(h, &budget)) return rc;
+      if (h->tuned) h->tuned_width = w;
+      r = rounds - budget;
+      if (r >= rounds) break;
+    }
+    unsigned long long *slot = nullptr;
+    if (nerr > 0 && (r + 1) % err_every == 0) slot = h->err + ((r + 1) / err_every - 1);
+    if (int rc = launch_round(h, slot)) return rc;
+  }
   return FU_OK;
 }
 
@@ -1530,18 +1761,7 @@ int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *e
     if (int rc = fu__err_slots(h, nerr)) return rc;
     HIP_TRY(hipMemsetAsync(h->err, 0, sizeof(unsigned long long) * nerr, h->stream));
   }
-  for (int32_t r = 0; r < rounds; ++r) {
-    // tune between rounds when no error slot is pending in the rounds it would consume
-    if (h->autotune && !h->tuned && h->kernel >= 4 && h->rounds >= 1 && nerr == 0) {
-      int32_t budget = rounds - r;
-      if (int rc = autotune_kernel(h, &budget)) return rc;
-      r = rounds - budget;
-      if (r >= rounds) break;
-    }
-    unsigned long long *slot = nullptr;
-    if (nerr > 0 && (r + 1) % err_every == 0) slot = h->err + ((r + 1) / err_every - 1);
-    if (int rc = launch_round(h, slot)) return rc;
-  }
+  if (int rc = run_rounds(h, rounds, err_every, nerr)) return rc;
   if (nerr > 0) {
     if (h->dist) {
       if (int rc = fu__dist_round_hook(h, 100 + nerr)) return rc;  // all-reduce max, in place
@@ -1556,15 +1776,16 @@ int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *e
 }
 
 int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
+  FU_TRY_BEGIN
   if (!h || !ms || rounds < 0) return fail(FU_ERR_ARG, "fu_run_collectall_timed: bad arguments");
   if (int rc = set_device(h)) return rc;
-  HIP_TRY(hipEventRecord(h->ev0, h->stream));
-  for (int32_t r = 0; r < rounds; ++r)
-    if (int rc = launch_round(h, nullptr)) return rc;
-  HIP_TRY(hipEventRecord(h->ev1, h->stream));
-  HIP_TRY(hipEventSynchronize(h->ev1));
-  HIP_TRY(hipEventElapsedTime(ms, h->ev0, h->ev1));
+  HIP_TRY(hipEventRecord(h->ev2, h->stream));
+  if (int rc = run_rounds(h, rounds, 0, 0)) return rc;
+  HIP_TRY(hipEventRecord(h->ev3, h->stream));
+  HIP_TRY(hipEventSynchronize(h->ev3));
+  HIP_TRY(hipEventElapsedTime(ms, h->ev2, h->ev3));
   return FU_OK;
+  FU_TRY_END
 }
 
 int fu_max_err(fu_handle *h, double *out) {
@@ -1612,13 +1833,27 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   return FU_OK;
 }
 
-int fu_get_info(fu_handle *h, int64_t info[8]) {
+int fu_get_info(fu_handle *h, int64_t info[16]) {
   if (!h || !info) return fail(FU_ERR_ARG, "fu_get_info: NULL argument");
   info[0] = h->kernel;
   info[1] = h->nt;
   info[2] = h->autotune ? (h->tuned ? 2 : 1) : 0;
   info[3] = h->rounds;
-  for (int k = 0; k < 4; ++k) info[4 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  info[4] = kGeoEdges[h->geo];
+  info[5] = kGeoNodes[h->geo];
+  info[6] = h->n_tunes;
+  info[7] = h->tuned_width;
+  for (int k = 0; k < 8; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  return FU_OK;
+}
+
+int fu_get_pack(fu_handle *h, int32_t width[3]) {
+  if (!h || !width) return fail(FU_ERR_ARG, "fu_get_pack: NULL argument");
+  if (int rc = set_device(h)) return rc;
+  PackCtl p[3];
+  HIP_TRY(hipMemcpyAsync(p, h->pctl, sizeof(p), hipMemcpyDeviceToHost, h->stream));
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  for (int k = 0; k < 3; ++k) width[k] = p[k].width;
   return FU_OK;
 }
 
@@ -1641,12 +1876,18 @@ int fu_destroy(fu_handle *h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->dist) fu__dist_free(h);
   void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
-                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_r,
-                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm};
+                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_geo[0],
+                  h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
+                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm,
+                  h->code[0], h->code[1], h->pctl, h->psample};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
   if (h->ev1) hipEventDestroy(h->ev1);
+  if (h->ev2) hipEventDestroy(h->ev2);
+  if (h->ev3) hipEventDestroy(h->ev3);
+  if (h->ev_pw) hipEventDestroy(h->ev_pw);
+  if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   delete h;
   return FU_OK;

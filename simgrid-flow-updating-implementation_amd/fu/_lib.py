@@ -67,6 +67,7 @@ _SIGS = {
     "fu_get_flows": ([vp, vp], ctypes.c_int),
     "fu_get_round": ([vp, P(i64)], ctypes.c_int),
     "fu_get_info": ([vp, vp], ctypes.c_int),
+    "fu_get_pack": ([vp, vp], ctypes.c_int),
     "fu_synchronize": ([vp], ctypes.c_int),
     "fu_destroy": ([vp], ctypes.c_int),
     "fu_trace_build": ([i32, vp, vp, i32, i32, cp, P(vp)], ctypes.c_int),

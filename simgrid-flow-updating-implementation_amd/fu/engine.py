@@ -98,13 +98,23 @@ class CollectAll:
 
     def info(self) -> dict:
         """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
-        a = np.zeros(8, dtype=np.int64)
+        a = np.zeros(16, dtype=np.int64)
         L.call("fu_get_info", self._h, L.ptr(a))
         names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2"}
         return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
                 "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
-                "tune_us_per_round": {k: a[4 + i] / 1e3 for i, k in
-                                      enumerate(("recon", "recon_nt", "split2", "split"))}}
+                "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
+                "tuned_pack_width": int(a[7]),
+                "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
+                                      enumerate(("recon", "recon_nt", "recon_1024x256", "recon_512",
+                                                 "split2", "split"))}}
+
+    def pack_widths(self) -> tuple:
+        """Packed estimate table widths (0 = doubles): the last even / odd round's code
+        table and the current encoding plan."""
+        w = np.zeros(3, dtype=np.int32)
+        L.call("fu_get_pack", self._h, L.ptr(w))
+        return tuple(int(x) for x in w)
 
     @property
     def rounds_done(self) -> int:

@@ -292,3 +292,64 @@ def test_autotune_switches_kernels_bitwise():
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=8)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+def _er_with_outlier_pairs(n, m, pairs, seed):
+    """ER(n, m) plus `pairs` disjoint 2-node components whose values are far from the giant
+    component's mean: their estimates never enter the packed window, so every gather of
+    them goes through the escape code."""
+    g = fu.Graph.erdos_renyi(n, m, seed=seed)
+    src = np.repeat(np.arange(g.n), np.diff(g.rowptr))
+    keep = src < g.col
+    ps = n + 2 * np.arange(pairs)
+    s = np.concatenate([src[keep], ps])
+    d = np.concatenate([g.col[keep], ps + 1])
+    v = np.concatenate([fu.uniform_values(n, seed=seed), 1e6 + np.arange(2 * pairs, dtype=np.float64)])
+    return fu.Graph.from_edges(n + 2 * pairs, s, d), v
+
+
+@pytest.mark.parametrize("kind", ["er", "rmat", "rmat_bins_off"])
+def test_packed_gather_long_run_bitwise(kind):
+    """The packed estimate table (8/16/32-bit lossless codes + escapes) switches on as the
+    estimates converge; 300 rounds must still equal the C oracle bit for bit, and equal the
+    same run with packing off."""
+    if kind == "er":
+        g, v = _er_with_outlier_pairs(100_000, 400_000, 64, seed=3)
+    else:
+        g = fu.Graph.rmat(13, 16, seed=3)
+        v = fu.uniform_values(g.n, seed=3)
+    rounds = 300
+    eng = fu.CollectAll(g, v, kernel="recon", hub_threshold=16)
+    eng.set_option("pack_every", 4)
+    if kind == "rmat_bins_off":
+        eng.set_option("bins", 0)
+    seen = set()
+    for _ in range(rounds // 25):
+        eng.run(25)
+        seen.update(eng.pack_widths())
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    assert seen & {8, 16, 32}, seen  # packing was actually exercised
+    off = fu.CollectAll(g, v, kernel="recon", hub_threshold=16)
+    off.set_option("pack", 0)
+    off.run(rounds)
+    assert off.pack_widths() == (0, 0, 0)
+    assert np.array_equal(off.estimates(), a_ref)
+
+
+def test_packed_gather_with_kernel_switches():
+    """Kernel 6 rounds mark their estimate table unpacked (width 0), so a kernel-4 round after
+    them gathers the doubles. recon, split2 and auto (which switches kernels mid-run) give
+    the same bits over a run long enough for packing to engage."""
+    g = fu.Graph.erdos_renyi(50_000, 200_000, seed=9)
+    v = fu.uniform_values(g.n, seed=9)
+    ref = None
+    for kernel in ("recon", "split2", "auto"):
+        eng = fu.CollectAll(g, v, kernel=kernel)
+        eng.set_option("pack_every", 2)
+        eng.run(260)
+        got = (eng.estimates(), eng.flows())
+        if ref is None:
+            ref = got
+        assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), kernel

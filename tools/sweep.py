@@ -19,6 +19,8 @@ VARIANTS = {
     "push": ("push", {}),
     "recon": ("recon", {}),
     "recon_nt": ("recon", {"nt": 1}),
+    "recon_nopack": ("recon", {"pack": 0}),
+    "recon_nt_nopack": ("recon", {"nt": 1, "pack": 0}),
     "split": ("split", {}),
     "split2": ("split2", {}),
     "recon_nobins": ("recon", {"bins": 0}),
@@ -39,6 +41,8 @@ VARIANTS = {
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
 opts = [a for a in sys.argv[1:] if a.startswith("--variants=")]
 names = opts[0].split("=", 1)[1].split(",") if opts else list(VARIANTS)
+warm = [int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--warm=")]
+warm = warm[0] if warm else 10  # rounds before timing (packing engages after ~100-300)
 specs = args or ["er:n=1000000,m=4000000"]
 for spec in specs:
     g = fu.Graph.from_spec(spec, seed=1)
@@ -50,7 +54,7 @@ for spec in specs:
         for k, val in o.items():
             if k != "diag":
                 e.set_option(k, val)
-        e.run(10)
+        e.run(warm)
         if "diag" in o:
             e.set_option("diag", o["diag"])
         engs[nm] = e
@@ -59,11 +63,12 @@ for spec in specs:
         for k, e in engs.items():
             res[k].append(e.run_timed(200) / 200 * 1e3)
     alg = 24 * g.E + 28 * g.n
-    out = {"spec": spec, "n": g.n, "E": g.E, "max_deg": g.max_deg}
+    out = {"spec": spec, "n": g.n, "E": g.E, "max_deg": g.max_deg, "warm": warm}
     for k, ts in res.items():
         med = sorted(ts)[len(ts) // 2]
         out[k] = {"us_per_round_med": med, "us_min": min(ts),
-                  "alg_GBs": alg / (med * 1e-6) / 1e9, "edge_updates_per_s": g.E / (med * 1e-6)}
+                  "alg_GBs": alg / (med * 1e-6) / 1e9, "edge_updates_per_s": g.E / (med * 1e-6),
+                  "pack": engs[k].pack_widths()}
     print(json.dumps(out), flush=True)
     for e in engs.values():
         e.close()
