@@ -95,12 +95,12 @@ int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
 /* Options: "kernel" (0 = auto = 4, 1 = thread-per-node, 2 = LDS tile (pull), 3 = push/inbox,
  *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch,
  *          6 = 4 with the low half of each row staged by a gather launch
- *          (rows must be sorted by neighbour id)),
+ *          (rows must be sorted by neighbour id), 7 = 4 with one tile per wave),
  * "hub_threshold" (degree above which a node gets a block; default 64),
  * "nt" (1 = non-temporal loads/stores for the streamed arrays of kernel 4; default 0),
  * "pack" (kernel 4: gather lossless 8/16/32-bit codes of the estimates once they have
  *          converged into a narrow cluster; default 1), "pack_every" (rounds between
- *          encoding plans; default 8), "bins" (degree bins for kernel 4's heavy rows). */
+ *          encoding plans; default 16), "bins" (degree bins for kernel 4's heavy rows). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);
@@ -124,7 +124,7 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done);
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
  * passes, [7] = packing width of the last pass, [8..13] = the last pass's ns per round for
  * its candidates (4, 4+nt, 4 at 1024x256, 4 at 512x64, 6, 5; 0 = not run). With kernel
- * "auto" (the default) a fu_run_collectall(_timed) with >= 18 rounds left after round 0
+ * "auto" (the default) a fu_run_collectall(_timed) with >= 30 rounds left after round 0
  * times the candidates on real rounds (they share state and are bitwise identical) and keeps
  * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */
 int fu_get_info(fu_handle *h, int64_t info[16]);

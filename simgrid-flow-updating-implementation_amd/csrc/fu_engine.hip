@@ -55,7 +55,10 @@ __device__ inline void block_max_to(unsigned long long x, unsigned long long *ds
   if (threadIdx.x == 0) {
     unsigned long long m = s_w[0];
     for (int k = 1; k < kBlock / 64; ++k) m = m > s_w[k] ? m : s_w[k];
-    if (m) atomicMax(dst, m);
+    // a plain read first: only blocks that raise the running max issue the atomic (a stale
+    // read only costs an extra atomic, never a wrong max). Without it 16K blocks serialise
+    // on one address.
+    if (m && m > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMax(dst, m);
   }
 }
 
@@ -344,32 +347,39 @@ __device__ inline void gather_packed(const int (&c)[KP], double (&g)[KP], int t,
 #pragma unroll
   for (int k = 0; k < KP; ++k) g[k] = t + k * kBlock < ne ? decode_or<W>(cd[k], base, a_prev, c[k]) : 0.0;
 }
-// Encoding plan from the estimates a_r of a fixed sample of gather targets: the centre is
-// the median of the first 64 sampled keys; the width is the smallest W whose window
-// [centre - 2^(W-1), centre + 2^(W-1) - 2] holds >= 99.5 % of the sample; else 0 (off).
+// Encoding plan from the estimates a_r of a fixed sample of kPlanSamples gather targets:
+// the centre is the median of the first 64 sampled keys; the width is the smallest W whose
+// window [centre - 2^(W-1), centre + 2^(W-1) - 2] holds >= 99.5 % of the sample; else 0.
+constexpr int kPlanSamples = 4096;
+
 __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__ a,
-                                                      const int *__restrict__ sample, int ns,
+                                                      const int *__restrict__ sample,
                                                       PackCtl *__restrict__ ctl) {
+  constexpr int kPer = kPlanSamples / kBlock;
   __shared__ unsigned long long s_centre;
   __shared__ int s_cnt[3];
   const int t = threadIdx.x;
   if (t < 3) s_cnt[t] = 0;
-  if (t < 64) {
-    const int m = min(ns, 64);
-    const unsigned long long k = t < m ? dkey(a[sample[t]]) : ~0ull;
+  int idx[kPer];
+  unsigned long long key[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) idx[k] = sample[t + k * kBlock];  // all loads in flight
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) key[k] = dkey(a[idx[k]]);
+  if (t < 64) {  // median of samples 0..63: rank by comparison against every lane
     int below = 0;
-    for (int l = 0; l < m; ++l) {
-      const unsigned long long o = __shfl(k, l, 64);
-      below += (o < k) || (o == k && l < t);
+    for (int l = 0; l < 64; ++l) {
+      const unsigned long long o = __shfl(key[0], l, 64);
+      below += (o < key[0]) || (o == key[0] && l < t);
     }
-    if (t < m && below == m / 2) s_centre = k;
+    if (below == 32) s_centre = key[0];
   }
   __syncthreads();
   const unsigned long long c = s_centre;
   int n8 = 0, n16 = 0, n32 = 0;
-  for (int i = t; i < ns; i += kBlock) {
-    const unsigned long long k = dkey(a[sample[i]]);
-    const unsigned long long d = k >= c ? k - c : c - k;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const unsigned long long d = key[k] >= c ? key[k] - c : c - key[k];
     n8 += d + 2 <= (1ull << 7);
     n16 += d + 2 <= (1ull << 15);
     n32 += d + 2 <= (1ull << 31);
@@ -379,7 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
   atomicAdd(&s_cnt[2], n32);
   __syncthreads();
   if (t == 0) {
-    const int need = ns - ns / 200;
+    const int need = kPlanSamples - kPlanSamples / 200;
     const int w = s_cnt[0] >= need ? 8 : s_cnt[1] >= need ? 16 : s_cnt[2] >= need ? 32 : 0;
     PackCtl p;
     p.base = w ? c - (1ull << (w - 1)) : 0;
@@ -415,7 +425,8 @@ __device__ inline T ld_stream(const T *p) {
 //   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
 //   2 = no flow load/store (prices the flow stream);
 //   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
-//   5 = hub chains skipped (prices the exact sequential hub sums).
+//   5 = hub chains skipped (prices the exact sequential hub sums);
+//   12 = 1 and 2 together (prices col + the per-node arrays alone).
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
@@ -579,10 +590,10 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (q < ne) {
       if (NT) {
         c[k] = ld_stream(col + e0 + q);
-        x[k] = DIAG == 2 ? 0.0 : ld_stream(F + e0 + q);
+        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_stream(F + e0 + q);
       } else {
         c[k] = col[e0 + q];
-        x[k] = DIAG == 2 ? 0.0 : F[e0 + q];
+        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : F[e0 + q];
       }
     }
   }
@@ -597,7 +608,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const int q = t + k * kBlock;
       g[k] = 0.0;
       if (q < ne) {
-        const int gi = DIAG == 1 ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
+        const int gi = (DIAG == 1 || DIAG == 12) ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
         g[k] = a_prev[gi];
       }
     }
@@ -646,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int q = t + k * kBlock;
     if (q < ne) {
       const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
-      if (DIAG == 2) {
+      if (DIAG == 2 || DIAG == 12) {
         if (fnew == 12345.678) F[e0 + q] = fnew;  // keep the value live, store ~never
       } else if (NT) {
         __builtin_nontemporal_store(fnew, F + e0 + q);
@@ -656,6 +667,131 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     }
   }
   if (CHECK) block_max_to(eb, err);
+}
+
+// ------------------------------------------------------------------------------------
+// Variant 7: kernel 4's light tiles at WAVE granularity ("wave"). Same arithmetic and
+// state as kernel 4 (flow reconstruction, packed gathers); each 64-lane wave owns one tile
+// of <= TN nodes / <= TE edges and its own LDS slice, so there is no block barrier: a wave
+// that finishes its loads proceeds without waiting for the other three, and more tiles are
+// in flight per CU. Phase C keeps each edge's er and f_{r-2} in the registers that loaded
+// them. Heavy rows (degree > min(hub_threshold, TE)) run through kernel 4's heavy path in
+// a separate launch before this one.
+// ------------------------------------------------------------------------------------
+__device__ inline void wave_sync() {
+  // LDS traffic of one wave is processed in order; this only stops the compiler from moving
+  // LDS accesses across the hand-off between lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline void wave_max_to(unsigned long long x, unsigned long long *dst) {
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long y = __shfl_xor(x, off, 64);
+    x = x > y ? x : y;
+  }
+  if ((threadIdx.x & 63) == 0 && x && x > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(dst, x);
+}
+
+template <bool CHECK, int TE, int TN>
+__global__ __launch_bounds__(kBlock) void k_round_wave(
+    const int4 *__restrict__ wtiles, int nwt, const int *__restrict__ rowptr,
+    const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
+    const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
+    double *__restrict__ a_new, const double *__restrict__ target,
+    unsigned long long *__restrict__ err, const void *__restrict__ code_prev,
+    void *__restrict__ code_new, PackCtl *__restrict__ ctl, int rslot) {
+  static_assert(TE % 64 == 0 && TN <= 64 && TE <= 512, "wave tile geometry");
+  constexpr int kW = kBlock / 64;
+  constexpr int kPer = TE / 64;
+  __shared__ double s_x[kW][TE];   // f_{r-2}, then fr after phase B
+  __shared__ double s_er[kW][TE];  // a_{r-1}[col e]
+  __shared__ unsigned short s_own[kW][TE];
+  __shared__ int s_rp[kW][TN + 1];
+  __shared__ double s_a[kW][TN];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const PackCtl pp = ctl[rslot ^ 1];
+  const PackCtl pc = ctl[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
+  const int tile = blockIdx.x * kW + w;
+  if (tile >= nwt) return;  // no block barrier below: waves are independent
+  const int4 tl = wtiles[tile];
+  const int nb = tl.x, nn = tl.y - tl.x;
+  const int e0 = tl.z, ne = tl.w - tl.z;
+  int c[kPer];
+  double x[kPer], g[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = lane + k * 64;
+    c[k] = q < ne ? col[e0 + q] : 0;
+    x[k] = q < ne ? F[e0 + q] : 0.0;
+  }
+  const int rp = lane <= nn ? rowptr[nb + lane] : 0;
+  const int rp_last = (TN == 64 && lane == 0 && nn == 64) ? rowptr[nb + 64] : 0;
+  const double vv = lane < nn ? v[nb + lane] : 0.0;
+  const double own2 = lane < nn ? a_prev2[nb + lane] : 0.0;
+  if (pp.width == 0) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? a_prev[c[k]] : 0.0;
+  } else {
+    unsigned cd[kPer];
+    if (pp.width == 8) {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<8>(code_prev, c[k]) : 0u;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<8>(cd[k], pp.base, a_prev, c[k]) : 0.0;
+    } else if (pp.width == 16) {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<16>(code_prev, c[k]) : 0u;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<16>(cd[k], pp.base, a_prev, c[k]) : 0.0;
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<32>(code_prev, c[k]) : 0u;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<32>(cd[k], pp.base, a_prev, c[k]) : 0.0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = lane + k * 64;
+    if (q < ne) {
+      s_x[w][q] = x[k];
+      s_er[w][q] = g[k];
+    }
+  }
+  if (lane <= nn && lane <= TN) s_rp[w][lane] = rp;
+  if (TN == 64 && lane == 0 && nn == 64) s_rp[w][64] = rp_last;
+  wave_sync();
+  // phase B: one lane per node, its row in order (CA:106-113)
+  unsigned long long eb = 0;
+  if (lane < nn) {
+    const int qb = s_rp[w][lane] - e0, qe = s_rp[w][lane + 1] - e0;
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double er = s_er[w][q];
+      const double fr = recon_fr(s_x[w][q], er, own2);
+      s_x[w][q] = fr;
+      s_own[w][q] = (unsigned short)lane;
+      S = S + fr;
+      T = T + er;
+    }
+    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
+    s_a[w][lane] = a;
+    a_new[nb + lane] = a;
+    if (pc.width) put_code(pc, code_new, nb + lane, a);
+    if (CHECK) eb = err_bits(a, target[nb + lane]);
+  }
+  wave_sync();
+  // phase C: new flows, coalesced, in place (CA:117-118); er from the loading registers
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = lane + k * 64;
+    if (q < ne) F[e0 + q] = (s_x[w][q] + s_a[w][s_own[w][q]]) - g[k];
+  }
+  if (CHECK) wave_max_to(eb, err);
 }
 
 __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
@@ -1094,7 +1230,7 @@ struct fu_handle {
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
   bool tuned = false;
-  float tune_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  float tune_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per candidate (autotune_kernel order)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
   int tuned_width = 0;    // packing width the last pass ran under
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
@@ -1117,6 +1253,13 @@ struct fu_handle {
   int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
   int ntiles_geo[4] = {0, 0, 0, 0};
   int geo = 0;
+  // kernel 7 (wave tiles): per wave geometry (0 = 256 edges x 32 nodes, 1 = 512 x 64) the
+  // light wave tiles and the heavy rows (kernel 4 heavy-path tiles) of that geometry
+  int4 *wtiles[2] = {nullptr, nullptr};
+  int nwtiles[2] = {0, 0};
+  int4 *wheavy[2] = {nullptr, nullptr};
+  int nwheavy[2] = {0, 0};
+  int wgeo = 1;
   int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
   int bins = 0;         // kernel 4 (geometry 0): degree bins for rows above hub_threshold
   // kernel 4 packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -1125,7 +1268,7 @@ struct fu_handle {
   int *psample = nullptr;   // gather targets sampled for the plan
   int n_psample = 0;
   int pack = 1;             // 0 = off
-  int pack_every = 8;       // rounds between encoding plans
+  int pack_every = 16;      // rounds between encoding plans
   int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
   int tile_nodes = 0;
   bool has_target = false;
@@ -1219,8 +1362,50 @@ int build_tiles_binned(fu_handle *h) {
 constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
 constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 
+constexpr int kWaveEdges[2] = {256, 512};
+constexpr int kWaveNodes[2] = {32, 64};
+
+// Kernel 7 tiles: light rows (degree <= min(hub_threshold, TE)) in contiguous wave tiles of
+// <= TN nodes / <= TE edges; the other rows as kernel 4 heavy-path tiles {i, -1, b, e}.
+int build_wave_tiles(fu_handle *h, int wg) {
+  const int te = kWaveEdges[wg], tn = kWaveNodes[wg];
+  const int64_t lim = std::min<int64_t>(h->hub_threshold, te);
+  std::vector<int4> light, heavy;
+  const int32_t n = h->n;
+  int32_t i = 0;
+  while (i < n) {
+    const int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
+    if (d > lim) {
+      heavy.push_back(make_int4(i, -1, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
+      ++i;
+      continue;
+    }
+    const int32_t b = i;
+    const int64_t eb = h->h_rowptr[b];
+    while (i < n && i - b < tn) {
+      const int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
+      if (di > lim || h->h_rowptr[i + 1] - eb > te) break;
+      ++i;
+    }
+    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
+  }
+  for (int4 **p : {&h->wtiles[wg], &h->wheavy[wg]}) {
+    if (*p) hipFree(*p);
+    *p = nullptr;
+  }
+  h->nwtiles[wg] = (int)light.size();
+  h->nwheavy[wg] = (int)heavy.size();
+  if (int rc = dmalloc(&h->wtiles[wg], std::max<size_t>(1, light.size()))) return rc;
+  if (int rc = dmalloc(&h->wheavy[wg], std::max<size_t>(1, heavy.size()))) return rc;
+  if (!light.empty()) HIP_TRY(hipMemcpy(h->wtiles[wg], light.data(), sizeof(int4) * light.size(), hipMemcpyHostToDevice));
+  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->wheavy[wg], heavy.data(), sizeof(int4) * heavy.size(), hipMemcpyHostToDevice));
+  return FU_OK;
+}
+
 int build_tiles(fu_handle *h) {
   if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
+  for (int wg = 0; wg < 2; ++wg)
+    if (int rc = build_wave_tiles(h, wg)) return rc;
   for (int g = 0; g < 4; ++g) {
     if (g == 0 && h->bins) {
       if (int rc = build_tiles_binned(h)) return rc;
@@ -1354,6 +1539,34 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         hipLaunchKernelGGL(k_round_split<false>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
                            h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
                            h->target, err_slot, h->pctl, (int)(r & 1));
+    } else if (h->kernel == 7) {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+      const int wg = h->wgeo;
+      if (h->nwheavy[wg]) {
+        if (check)
+          hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
+                             h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1));
+        else
+          hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
+                             h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1));
+      }
+      if (h->nwtiles[wg]) {
+        const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
+#define FU_WAVE(C, TE, TN)                                                                          \
+  hipLaunchKernelGGL((k_round_wave<C, TE, TN>), dim3(blocks), dim3(kBlock), 0, h->stream, h->wtiles[wg], \
+                     h->nwtiles[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,         \
+                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1))
+        if (wg == 0) {
+          if (check) FU_WAVE(true, 256, 32); else FU_WAVE(false, 256, 32);
+        } else {
+          if (check) FU_WAVE(true, 512, 64); else FU_WAVE(false, 512, 64);
+        }
+#undef FU_WAVE
+      }
     } else {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -1374,6 +1587,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       else if (h->diag == 3) FU_RECON(false, false, 3);
       else if (h->diag == 4) FU_RECON(false, false, 4);
       else if (h->diag == 5) FU_RECON(false, false, 5);
+      else if (h->diag == 12) FU_RECON(false, false, 12);
       else if (check) {
         if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
       } else {
@@ -1427,8 +1641,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   h->rounds++;
   // refresh the packing plan from a_r (kernel 4 encodes with it from the next round on)
   if (h->kernel >= 4 && h->pack && !h->dist && h->n_psample > 0 && h->rounds % h->pack_every == 0) {
-    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample,
-                       h->n_psample, h->pctl);
+    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample, h->pctl);
     HIP_TRY(hipGetLastError());
     if (!h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
       HIP_TRY(hipMemcpyAsync(h->h_pw, &h->pctl[2].width, sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -1533,7 +1746,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     return cleanup(rc);
   if (hipMemset(h->pctl, 0, sizeof(PackCtl) * 3) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
   if (e > 0) {  // plan sample: the targets of 4096 pseudo-random edges (degree-weighted)
-    const int ns = 4096;
+    const int ns = kPlanSamples;
     std::vector<int32_t> smp(ns);
     for (int q = 0; q < ns; ++q) smp[q] = col[splitmix_at(0x9ac4u, (uint64_t)q) % (uint64_t)e];
     if ((rc = dmalloc(&h->psample, ns))) return cleanup(rc);
@@ -1577,7 +1790,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 6) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..6");
+    if (value < 0 || value > 7) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..7");
     if (h->dist && value != 0 && value != 2 && value != 4)  // 5, 6: single GPU only
       return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
     if (!h->rev && h->E > 0 && value >= 1 && value <= 3)
@@ -1588,7 +1801,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->tuned = false;
     h->nt = 0;
     if (h->kernel == 3) return ensure_inbox(h);
-    if (h->kernel == 4) return ensure_a2(h);
+    if (h->kernel == 4 || h->kernel == 7) return ensure_a2(h);
     if (h->kernel == 5 || h->kernel == 6) {
       if (int rc = ensure_a2(h)) return rc;
       if (int rc = ensure_split(h)) {
@@ -1619,6 +1832,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!std::strcmp(key, "bins")) {
     h->bins = value != 0;
     return build_tiles(h);
+  }
+  if (!std::strcmp(key, "wave_edges")) {  // kernel 7 wave tile: 256 (x32 nodes) or 512 (x64)
+    if (value != 256 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: wave_edges must be 256 or 512");
+    h->wgeo = value == 512;
+    return FU_OK;
   }
   if (!std::strcmp(key, "tile_edges")) {
     if (value != 2048 && value != 1024 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: tile_edges must be 2048, 1024 or 512");
@@ -1670,7 +1888,7 @@ int fu__err_slots(fu_handle *h, int count) {
 
 // Kernels 4, 5 and 6 share the state layout (F[r & 1], A[r % 3]) and are all bitwise
 // exact, so switching between them (or between kernel 4's tile geometries) mid-run changes
-// nothing but speed. "auto" times each candidate on real rounds (1 warm + 2 timed each)
+// nothing but speed. "auto" times each candidate on real rounds (1 warm + 4 timed each)
 // once round 0 is done and keeps the fastest. The rounds count toward the caller's total,
 // and the results are unchanged. The pass re-runs when the packing plan changes width (the
 // packed gather shifts the balance between the candidates), at most kMaxTunes times.
@@ -1680,12 +1898,15 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   struct Cand {
     int kernel, nt, geo;
   };
+  // kernel 7 (wave tiles) is not a candidate: slower than kernel 4 at 512x64 everywhere
+  // measured; it stays selectable as an option
   std::vector<Cand> cands = {{4, 0, 0}, {4, 1, 0}, {4, 0, 2}, {4, 0, 3}};
   if (!h->dist) {
     cands.push_back({6, 0, 0});
     cands.push_back({5, 0, 0});
   }
-  const int32_t need = 3 * (int32_t)cands.size();
+  constexpr int kTimed = 4;
+  const int32_t need = (1 + kTimed) * (int32_t)cands.size();
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
   int bi = -1;
@@ -1699,17 +1920,18 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
     }
     h->kernel = cands[c].kernel;
     h->nt = cands[c].nt;
-    h->geo = cands[c].geo;
+    if (h->kernel == 7) h->wgeo = cands[c].geo;
+    else h->geo = cands[c].geo;
     if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
-    for (int k = 0; k < 2; ++k)
+    for (int k = 0; k < kTimed; ++k)
       if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
     HIP_TRY(hipEventSynchronize(h->ev1));
     float ms = 0.f;
     HIP_TRY(hipEventElapsedTime(&ms, h->ev0, h->ev1));
-    h->tune_ms[c] = ms / 2;
-    *budget -= 3;
+    h->tune_ms[c] = ms / kTimed;
+    *budget -= 1 + kTimed;
     if (ms < best) {
       best = ms;
       bi = (int)c;
@@ -1717,7 +1939,8 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   }
   h->kernel = cands[bi].kernel;
   h->nt = cands[bi].nt;
-  h->geo = cands[bi].geo;
+  if (h->kernel == 7) h->wgeo = cands[bi].geo;
+  else h->geo = cands[bi].geo;
   h->tuned = true;
   h->n_tunes++;
   return FU_OK;
@@ -1877,7 +2100,8 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
                   h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_geo[0],
-                  h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
+                  h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3], h->wtiles[0], h->wtiles[1],
+                  h->wheavy[0], h->wheavy[1],
                   h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm,
                   h->code[0], h->code[1], h->pctl, h->psample};
   for (void *p : ptrs)

@@ -16,7 +16,7 @@ import numpy as np
 from . import _lib as L
 from .graph import Graph
 
-KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6}
+KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6, "wave": 7}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
@@ -100,7 +100,7 @@ class CollectAll:
         """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
         a = np.zeros(16, dtype=np.int64)
         L.call("fu_get_info", self._h, L.ptr(a))
-        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2"}
+        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave"}
         return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
                 "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
                 "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),

@@ -15,7 +15,7 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["thread", "tile", "push", "recon", "split", "split2"]
+KERNELS = ["thread", "tile", "push", "recon", "split", "split2", "wave"]
 
 
 def _rows_sorted(rowptr, col):
@@ -46,7 +46,7 @@ def test_ca_sync_fixture_bitwise(name, meta, kernel):
     _check_fixture(meta, kernel)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave"])
 @pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
 def test_ca_sync_fixture_heavy_path(name, kernel):
     """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
@@ -65,7 +65,7 @@ def test_er_vs_c_oracle_bitwise(kernel):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave"])
 def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.rmat(15, 16, seed=2)
     assert g.max_deg > 2048  # exercises chunked heavy tiles
@@ -279,17 +279,17 @@ def test_dist_rgg_slab_estimates_only_halo_matches_engine():
 
 
 def test_autotune_switches_kernels_bitwise():
-    """kernel="auto" times kernels 4, 4+nt, 6, 5 on real rounds and keeps the fastest; the
-    switch happens mid-run and must not change a single bit."""
+    """kernel="auto" times kernel 4 (three tile geometries, +nt), 6 and 5 on real rounds and
+    keeps the fastest; the switch happens mid-run and must not change a single bit."""
     g = fu.Graph.erdos_renyi(300_000, 1_200_000, seed=8)
     v = fu.uniform_values(g.n, seed=8)
     eng = fu.CollectAll(g, v)
     assert eng.info()["autotune"] == "pending"
-    eng.run(30)
+    eng.run(50)
     info = eng.info()
-    assert info["autotune"] == "done" and info["rounds"] == 30
+    assert info["autotune"] == "done" and info["rounds"] == 50
     assert all(t > 0 for t in info["tune_us_per_round"].values())
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=8)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 50, nthreads=8)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
 
@@ -308,8 +308,9 @@ def _er_with_outlier_pairs(n, m, pairs, seed):
     return fu.Graph.from_edges(n + 2 * pairs, s, d), v
 
 
-@pytest.mark.parametrize("kind", ["er", "rmat", "rmat_bins_off"])
-def test_packed_gather_long_run_bitwise(kind):
+@pytest.mark.parametrize("kind,kernel", [("er", "recon"), ("rmat", "recon"), ("rmat_bins", "recon"),
+                                         ("er", "wave"), ("rmat", "wave")])
+def test_packed_gather_long_run_bitwise(kind, kernel):
     """The packed estimate table (8/16/32-bit lossless codes + escapes) switches on as the
     estimates converge; 300 rounds must still equal the C oracle bit for bit, and equal the
     same run with packing off."""
@@ -319,10 +320,10 @@ def test_packed_gather_long_run_bitwise(kind):
         g = fu.Graph.rmat(13, 16, seed=3)
         v = fu.uniform_values(g.n, seed=3)
     rounds = 300
-    eng = fu.CollectAll(g, v, kernel="recon", hub_threshold=16)
+    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=16)
     eng.set_option("pack_every", 4)
-    if kind == "rmat_bins_off":
-        eng.set_option("bins", 0)
+    if kind == "rmat_bins":
+        eng.set_option("bins", 1)
     seen = set()
     for _ in range(rounds // 25):
         eng.run(25)
@@ -345,7 +346,7 @@ def test_packed_gather_with_kernel_switches():
     g = fu.Graph.erdos_renyi(50_000, 200_000, seed=9)
     v = fu.uniform_values(g.n, seed=9)
     ref = None
-    for kernel in ("recon", "split2", "auto"):
+    for kernel in ("recon", "split2", "wave", "auto"):
         eng = fu.CollectAll(g, v, kernel=kernel)
         eng.set_option("pack_every", 2)
         eng.run(260)
@@ -353,3 +354,26 @@ def test_packed_gather_with_kernel_switches():
         if ref is None:
             ref = got
         assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), kernel
+
+
+@pytest.mark.parametrize("kernel,opts", [("recon", {"tile_edges": 1024}),
+                                         ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
+                                         ("recon", {"tile_edges": 512}),
+                                         ("wave", {"wave_edges": 256}),
+                                         ("wave", {"wave_edges": 512})])
+@pytest.mark.parametrize("kind", ["er", "rmat"])
+def test_tile_geometries_bitwise(kernel, opts, kind):
+    """Every kernel 4 / kernel 7 tile geometry the autotuner may pick, incl. the heavy-row
+    launch of kernel 7 (hub_threshold 16 on R-MAT), against the C oracle."""
+    if kind == "er":
+        g = fu.Graph.erdos_renyi(200_000, 800_000, seed=6)
+    else:
+        g = fu.Graph.rmat(14, 16, seed=6)
+    v = fu.uniform_values(g.n, seed=6)
+    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=16 if kind == "rmat" else None)
+    for k, val in opts.items():
+        eng.set_option(k, val)
+    eng.run(30)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)

@@ -1,5 +1,7 @@
 #!/usr/bin/env python3
-"""Small profiling target: ER-1M, `rounds` rounds of one kernel variant (for rocprofv3)."""
+"""Profiling target (for rocprofv3): the bench's timed region without the bench around it.
+ER-1M, kernel "auto": `warm` rounds (autotune), reset, then `rounds` rounds from the zero
+state, exactly as bench.py times them."""
 import argparse
 import os
 import sys
@@ -10,17 +12,25 @@ import fu  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--spec", default="er:n=1000000,m=4000000")
-ap.add_argument("--kernel", default="recon")
-ap.add_argument("--rounds", type=int, default=50)
-ap.add_argument("--nt", type=int, default=0)
+ap.add_argument("--kernel", default="auto")
+ap.add_argument("--warm", type=int, default=20)
+ap.add_argument("--rounds", type=int, default=1000)
+ap.add_argument("--nt", type=int, default=-1)
+ap.add_argument("--pack", type=int, default=1)
+ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1024/512); 0 = default")
 ap.add_argument("--diag", type=int, default=0)
 a = ap.parse_args()
 g = fu.Graph.from_spec(a.spec, seed=1)
 v = fu.uniform_values(g.n, seed=0)
 eng = fu.CollectAll(g, v, kernel=a.kernel)
-eng.set_option("nt", a.nt)
-eng.run(2)
+if a.nt >= 0:
+    eng.set_option("nt", a.nt)
+eng.set_option("pack", a.pack)
+if a.tile:
+    eng.set_option("tile_edges", a.tile)
+eng.run(a.warm)
+eng.reset()
 eng.set_option("diag", a.diag)
 eng.run(a.rounds)
 eng.synchronize()
-print("n", g.n, "E", g.E, "alg_bytes", 24 * g.E + 28 * g.n)
+print("n", g.n, "E", g.E, "alg_bytes", 24 * g.E + 28 * g.n, "info", eng.info(), "pack", eng.pack_widths())

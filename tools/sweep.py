@@ -23,6 +23,8 @@ VARIANTS = {
     "recon_nt_nopack": ("recon", {"nt": 1, "pack": 0}),
     "split": ("split", {}),
     "split2": ("split2", {}),
+    "wave256": ("wave", {"wave_edges": 256}),
+    "wave512": ("wave", {"wave_edges": 512}),
     "recon_nobins": ("recon", {"bins": 0}),
     "recon_1024": ("recon", {"tile_edges": 1024}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
@@ -31,6 +33,9 @@ VARIANTS = {
     "diag1_gather_free": ("recon", {"diag": 1}),
     "diag2_flow_free": ("recon", {"diag": 2}),
     "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
+    "diag1_512": ("recon", {"tile_edges": 512, "diag": 1}),
+    "diag2_512": ("recon", {"tile_edges": 512, "diag": 2}),
+    "diag12_512": ("recon", {"tile_edges": 512, "diag": 12}),
     "diag3_half_table": ("recon", {"diag": 3}),
     "diag4_quarter_table": ("recon", {"diag": 4}),
     "diag5_no_hub_chain": ("recon", {"diag": 5}),
