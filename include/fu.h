@@ -95,12 +95,16 @@ int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
 /* Options: "kernel" (0 = auto = 4, 1 = thread-per-node, 2 = LDS tile (pull), 3 = push/inbox,
  *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch,
  *          6 = 4 with the low half of each row staged by a gather launch
- *          (rows must be sorted by neighbour id), 7 = 4 with one tile per wave),
+ *          (rows must be sorted by neighbour id), 7 = 4 with one tile per wave,
+ *          8 = LDS-staged slices: a stage launch turns the estimate gather into streams,
+ *          9 = persistent software-pipelined tiles, 10 = 9 reading 8's staged estimates),
  * "hub_threshold" (degree above which a node gets a block; default 64),
  * "nt" (1 = non-temporal loads/stores for the streamed arrays of kernel 4; default 0),
  * "pack" (kernel 4: gather lossless 8/16/32-bit codes of the estimates once they have
  *          converged into a narrow cluster; default 1), "pack_every" (rounds between
- *          encoding plans; default 16), "bins" (degree bins for kernel 4's heavy rows). */
+ *          encoding plans; default 16), "bins" (degree bins for kernel 4's heavy rows),
+ * "pipe_bpc" (kernels 9/10: persistent blocks per CU; default 6), "stage_layout" (kernels
+ *          8/10, tests: -1 = by packing width, 0..3 = slice layout of 1/2/4/8-byte elements). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);
@@ -122,12 +126,12 @@ int fu_get_flows(fu_handle *h, double *f_out);
 int fu_get_round(fu_handle *h, int64_t *rounds_done);
 /* info[0] = kernel in use, [1] = nt, [2] = autotune (0 off, 1 pending, 2 done),
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
- * passes, [7] = packing width of the last pass, [8..13] = the last pass's ns per round for
- * its candidates (4, 4+nt, 4 at 1024x256, 4 at 512x64, 6, 5; 0 = not run). With kernel
- * "auto" (the default) a fu_run_collectall(_timed) with >= 30 rounds left after round 0
+ * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
+ * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run). With kernel
+ * "auto" (the default) a fu_run_collectall(_timed) with >= 25 rounds left after round 0
  * times the candidates on real rounds (they share state and are bitwise identical) and keeps
  * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */
-int fu_get_info(fu_handle *h, int64_t info[16]);
+int fu_get_info(fu_handle *h, int64_t info[32]);  /* ABI 2: 32 entries */
 /* Packed estimate table widths (0 = doubles): [0]/[1] = the code tables of the last
  * even/odd round, [2] = the current encoding plan (synchronises). */
 int fu_get_pack(fu_handle *h, int32_t width[3]);

@@ -794,6 +794,502 @@ __global__ __launch_bounds__(kBlock) void k_round_wave(
   if (CHECK) wave_max_to(eb, err);
 }
 
+// ------------------------------------------------------------------------------------
+// Variant 8: LDS-staged slices ("stage"). The a_{r-1}[col e] gather is the part of a round
+// that does not stream: on ER every gather is a random L2 request (8 M per round), and the
+// fp64 table (8 MB) does not fit an XCD's 4 MB L2. Kernel 8 splits it into two launches:
+//   * k_stage: the estimate table (codes, or doubles while unpacked) is cut into slices of
+//     64 KB; a block copies slice s into LDS, then streams the slice-s column offsets of its
+//     edge groups (u16) and writes the looked-up table elements to G, in the same
+//     (group, slice, tile, position) order: coalesced reads and writes, gathers from LDS.
+//   * k_round_staged: kernel 4's light tile (flow reconstruction, CA:98-99 + CA:105-128),
+//     where each edge's estimate comes from G (contiguous runs of the tile) through a u32
+//     {index in the group's G region, position in the tile} instead of col + gather.
+// The layout depends on the table's element width (slice = 65536 / bytes nodes). The host
+// builds it for the width it last saw; a table wider than the layout is still handled (the
+// stage launch gathers it from global memory), so correctness never depends on the host's
+// view of the device-side packing plan. Rows above the tile limit run as kernel 4 heavy
+// tiles in a launch of their own. Results are bitwise those of kernel 4.
+// ------------------------------------------------------------------------------------
+constexpr int kStageThreads = 512;
+constexpr int kStageLds = 65536;  // bytes of table per slice
+constexpr int kStageTE = 512, kStageTN = 64;
+
+constexpr int kStageMaxItems = 513;  // per stage block: <= 512 group segments + sentinel
+constexpr int kStageU = 8;           // elements per thread per pass (all loads issued first)
+
+// LDS: the table slice is in s_tab (ds_read); else it is read from global memory (the
+// two are separate instantiations, so no load goes through the generic address space).
+template <typename T, bool LDS>
+__device__ inline void stage_pass(const int2 *s_item, int nit, int total, int j0,
+                                  const unsigned short *__restrict__ colS,
+                                  const unsigned char *s_tab, const T *__restrict__ gtab,
+                                  T *__restrict__ G) {
+  int kk[kStageU];
+  unsigned o[kStageU];
+#pragma unroll
+  for (int u = 0; u < kStageU; ++u) {  // flat index -> element: last item with pre <= j
+    const int j = j0 + u * kStageThreads;
+    int lo = 0, hi = nit - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (s_item[mid].y <= j) lo = mid; else hi = mid - 1;
+    }
+    kk[u] = j < total ? s_item[lo].x + (j - s_item[lo].y) : -1;
+  }
+#pragma unroll
+  for (int u = 0; u < kStageU; ++u) o[u] = kk[u] >= 0 ? colS[kk[u]] : 0u;
+  T val[kStageU];
+#pragma unroll
+  for (int u = 0; u < kStageU; ++u) {
+    if constexpr (LDS) val[u] = reinterpret_cast<const T *>(s_tab)[o[u]];
+    else val[u] = kk[u] >= 0 ? gtab[o[u]] : T(0);
+  }
+#pragma unroll
+  for (int u = 0; u < kStageU; ++u)
+    if (kk[u] >= 0) G[kk[u]] = val[u];
+}
+
+template <int LB>  // bytes per element the layout was built for (1, 2, 4, 8)
+__global__ __launch_bounds__(kStageThreads) void k_stage(
+    int P, int n, const int *__restrict__ aoff, const int2 *__restrict__ aitem,
+    const unsigned short *__restrict__ colS, const double *__restrict__ a_prev,
+    const void *__restrict__ code_prev, const PackCtl *__restrict__ ctl, int rslot,
+    void *__restrict__ G) {
+  constexpr int SN = kStageLds / LB;
+  __shared__ __align__(16) unsigned char s_tab[kStageLds];
+  __shared__ int2 s_item[kStageMaxItems];
+  const PackCtl pp = ctl[rslot ^ 1];
+  const int wb = pp.width ? pp.width / 8 : 8;  // bytes per element of the table gathered
+  const int s = blockIdx.x % P;
+  const int nb = s * SN;
+  const int cnt = min(SN, n - nb);
+  const unsigned char *src = pp.width ? reinterpret_cast<const unsigned char *>(code_prev)
+                                      : reinterpret_cast<const unsigned char *>(a_prev);
+  const bool lds = wb <= LB;
+  // this block's segments: {first element, flat prefix}, then a sentinel {-, total}
+  const int ib = aoff[blockIdx.x], nit = aoff[blockIdx.x + 1] - ib;
+  for (int i = threadIdx.x; i < nit; i += kStageThreads) s_item[i] = aitem[ib + i];
+  if (lds) {  // slice -> LDS: every 16-byte load issued before the stores, byte tail
+    const int bytes = cnt * wb;
+    const uint4 *s16 = reinterpret_cast<const uint4 *>(src + (size_t)nb * wb);
+    uint4 *d16 = reinterpret_cast<uint4 *>(s_tab);
+    constexpr int kW = kStageLds / 16 / kStageThreads;
+    const int w16 = bytes >> 4;
+    uint4 buf[kW];
+#pragma unroll
+    for (int u = 0; u < kW; ++u) {
+      const int k = threadIdx.x + u * kStageThreads;
+      buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < kW; ++u) {
+      const int k = threadIdx.x + u * kStageThreads;
+      if (k < w16) d16[k] = buf[u];
+    }
+    const int tb = w16 << 4;
+    if ((int)threadIdx.x < bytes - tb) s_tab[tb + threadIdx.x] = src[(size_t)nb * wb + tb + threadIdx.x];
+  }
+  __syncthreads();
+  const int items = nit - 1, total = s_item[nit - 1].y;
+  for (int j0 = threadIdx.x; j0 < total; j0 += kStageU * kStageThreads) {
+#define FU_PASS(T)                                                                                   \
+  do {                                                                                               \
+    if (lds) stage_pass<T, true>(s_item, items, total, j0, colS, s_tab, nullptr, reinterpret_cast<T *>(G)); \
+    else stage_pass<T, false>(s_item, items, total, j0, colS, s_tab,                                \
+                              reinterpret_cast<const T *>(src) + nb, reinterpret_cast<T *>(G));      \
+  } while (0)
+    if (wb == 1) FU_PASS(unsigned char);
+    else if (wb == 2) FU_PASS(unsigned short);
+    else if (wb == 4) FU_PASS(unsigned);
+    else FU_PASS(unsigned long long);
+#undef FU_PASS
+  }
+}
+
+// DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
+// 2 = no stage launch and G read as in 1 (prices the round without staging).
+template <bool CHECK, int TE, int TN, int DIAG = 0>
+__global__ __launch_bounds__(kBlock) void k_round_staged(
+    const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
+    const int *__restrict__ rowptr, const int *__restrict__ col,
+    const unsigned *__restrict__ sidx, const void *__restrict__ G, const double *__restrict__ v,
+    double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
+    double *__restrict__ a_new, const double *__restrict__ target,
+    unsigned long long *__restrict__ err, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
+    int rslot) {
+  static_assert(TE % kBlock == 0 && TN <= kBlock, "tile geometry");
+  const PackCtl pp = ctl[rslot ^ 1];
+  const PackCtl pc = ctl[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
+  __shared__ double s_x[TE];
+  __shared__ double s_er[TE];
+  __shared__ unsigned char s_own[TE];
+  __shared__ int s_rp[TN + 1];
+  __shared__ double s_a[TN];
+  const int t = threadIdx.x;
+  unsigned long long eb = 0;
+  // XCD-aware order: block b runs on XCD b % 8; consecutive tiles (one edge group, whose G
+  // region the tiles share) go to the same XCD, so that region is fetched into one L2
+  const int xcd = blockIdx.x & 7, per = ntl >> 3, rem = ntl & 7;
+  const int tile = DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3);
+  const int4 tl = tiles[tile];
+  const int gb = tgbase[tile];
+  const int nb = tl.x, nn = tl.y - tl.x;
+  const int e0 = tl.z, ne = tl.w - tl.z;
+  constexpr int kPer = TE / kBlock;
+  unsigned si[kPer];
+  double x[kPer], g[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    si[k] = q < ne ? sidx[e0 + q] : 0u;
+    x[k] = q < ne ? F[e0 + q] : 0.0;
+  }
+  const int rp = t <= nn ? rowptr[nb + t] : 0;
+  const double vv = t < nn ? v[nb + t] : 0.0;
+  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
+  int gi[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) gi[k] = t + k * kBlock < ne ? (DIAG ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
+  // every G load of the tile first, then decode (escapes gather the double via col)
+  if (pp.width == 0) {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) g[k] = gi[k] >= 0 ? reinterpret_cast<const double *>(G)[gi[k]] : 0.0;
+  } else {
+    unsigned cd[kPer];
+    unsigned esc;
+    if (pp.width == 8) {
+      esc = 0xFFu;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = gi[k] >= 0 ? reinterpret_cast<const unsigned char *>(G)[gi[k]] : 0u;
+    } else if (pp.width == 16) {
+      esc = 0xFFFFu;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = gi[k] >= 0 ? reinterpret_cast<const unsigned short *>(G)[gi[k]] : 0u;
+    } else {
+      esc = 0xFFFFFFFFu;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cd[k] = gi[k] >= 0 ? reinterpret_cast<const unsigned *>(G)[gi[k]] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      g[k] = gi[k] < 0 ? 0.0 : cd[k] == esc ? a_prev[col[e0 + (int)(si[k] & 0xFFFFu)]] : dkey_inv(pp.base + cd[k]);
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) {
+      s_x[q] = x[k];
+      s_er[si[k] & 0xFFFFu] = g[k];
+    }
+  }
+  if (t <= nn) s_rp[t] = rp;
+  __syncthreads();
+  if (t < nn) {  // phase B (CA:106-113)
+    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double er = s_er[q];
+      const double fr = recon_fr(s_x[q], er, own2);
+      s_x[q] = fr;
+      s_own[q] = (unsigned char)t;
+      S = S + fr;
+      T = T + er;
+    }
+    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
+    s_a[t] = a;
+    a_new[nb + t] = a;
+    if (pc.width) put_code(pc, code_new, nb + t, a);
+    if (CHECK) eb = err_bits(a, target[nb + t]);
+  }
+  __syncthreads();
+  // phase C: new flows, coalesced, in place (CA:117-118)
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = t + k * kBlock;
+    if (q < ne) F[e0 + q] = (s_x[q] + s_a[s_own[q]]) - s_er[q];
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
+// ------------------------------------------------------------------------------------
+// Variant 9: persistent, software-pipelined round ("pipe"). Kernels 4 and 8 run one tile
+// per block through load -> gather -> LDS -> row chains -> store, so a block's memory
+// latency is exposed once per tile and the chip runs short of bytes in flight (kernel 4
+// without its gather still only streams 5.4 TB/s). Here a block owns a list of light tiles
+// (512 edges / 64 nodes, on its XCD) and keeps two of them ahead of the one it computes:
+// while tile i is staged in LDS and summed, the estimate loads of tile i+1 and the stream
+// loads (edges, flows, node arrays) of tile i+2 are in flight. LDS is double-buffered by
+// tile parity, so two barriers per tile suffice. Rows above the tile limit (hubs) get
+// blocks of their own at the front of the grid (kernel 4's exact chunked chain).
+// MODE 0: per edge col -> a_{r-1}[col] (or its packed code); MODE 1: the staged runs of
+// kernel 8 (sidx -> G). Arithmetic identical to kernel 4 (CA:98-99, CA:105-128).
+// ------------------------------------------------------------------------------------
+constexpr int kPipeTE = 512, kPipeTN = 64, kPipeKP = kPipeTE / kBlock;
+constexpr int kPipeChunk = 64;  // max tiles per block (host sizes the grid accordingly)
+
+struct PipeStream {
+  int nb, nn, e0, ne, gb;
+  unsigned c[kPipeKP];  // MODE 0: col; MODE 1: sidx
+  double x[kPipeKP];    // f_{r-2}
+  int rp;
+  double vv, own2;
+};
+
+// Every load of the pipeline is unconditional, with indices clamped into the arrays, so
+// the loop body is straight-line code and the compiler can wait for exactly the loads an
+// instruction consumes (a guarded load makes it fall back to waiting for all of them,
+// prefetches included). Lanes past the tile read valid but unused elements.
+template <int MODE>
+__device__ inline void pipe_load(PipeStream &s, int it, int m, const int4 *s_tl, const int *s_gb,
+                                 const int *__restrict__ rowptr, const unsigned *__restrict__ cidx,
+                                 const double *__restrict__ F, const double *__restrict__ v,
+                                 const double *__restrict__ a_prev2, int elast) {
+  const int t = threadIdx.x;
+  const int itc = it < m ? it : 0;
+  const int4 tl = s_tl[itc];
+  const bool live = it < m;
+  s.nb = tl.x;
+  s.nn = live ? tl.y - tl.x : -1;
+  s.e0 = tl.z;
+  s.ne = live ? tl.w - tl.z : 0;
+  s.gb = MODE ? s_gb[itc] : 0;
+#pragma unroll
+  for (int k = 0; k < kPipeKP; ++k) {
+    const int e = min(s.e0 + t + k * kBlock, elast);
+    s.c[k] = cidx[e];
+    s.x[k] = F[e];
+  }
+  const int nn = tl.y - tl.x;
+  s.rp = rowptr[s.nb + min(t, nn)];
+  const int i = s.nb + min(t, max(nn - 1, 0));
+  s.vv = v[i];
+  s.own2 = a_prev2[i];
+}
+
+// raw estimate words of one tile (W = 0: the double's bits; else the W-bit code)
+template <int MODE, int W>
+__device__ inline void pipe_gather(unsigned long long (&raw)[kPipeKP], const PipeStream &s,
+                                   const void *__restrict__ tab, const double *__restrict__ a_prev) {
+#pragma unroll
+  for (int k = 0; k < kPipeKP; ++k) {
+    const int gi = MODE ? s.gb + (int)(s.c[k] >> 16) : (int)s.c[k];
+    if constexpr (W == 0) raw[k] = reinterpret_cast<const unsigned long long *>(MODE ? tab : a_prev)[gi];
+    else if constexpr (W == 8) raw[k] = reinterpret_cast<const unsigned char *>(tab)[gi];
+    else if constexpr (W == 16) raw[k] = reinterpret_cast<const unsigned short *>(tab)[gi];
+    else raw[k] = reinterpret_cast<const unsigned *>(tab)[gi];
+  }
+}
+
+struct PipeLds {
+  double x[2][kPipeTE];
+  double er[2][kPipeTE];
+  unsigned char own[2][kPipeTE];
+  int rp[2][kPipeTN + 1];
+  double a[2][kPipeTN];
+  int4 tl[kPipeChunk];
+  int gb[kPipeChunk];
+};
+
+// One pipeline step: compute tile `it` (stream registers sa, estimate words ga) while the
+// estimates of tile it+1 (stream sb, into gb) and the stream of tile it+2 (into sc) load.
+// The caller unrolls the step over the 3 x 2 register sets (period 6), so no register is
+// ever copied while a load into it is in flight (a copy would wait for that load).
+template <bool CHECK, int MODE, int W>
+__device__ inline void pipe_step(
+    PipeLds &L, int it, int m, PipeStream &sa, const PipeStream &sb, PipeStream &sc,
+    unsigned long long (&ga)[kPipeKP], unsigned long long (&gb)[kPipeKP], unsigned long long &eb,
+    const int *__restrict__ rowptr, const int *__restrict__ col, const unsigned *__restrict__ cidx,
+    const void *__restrict__ tab, const double *__restrict__ v, double *__restrict__ F,
+    const double *__restrict__ a_prev, const double *__restrict__ a_prev2, double *__restrict__ a_new,
+    const double *__restrict__ target, void *__restrict__ code_new, const PackCtl &pp,
+    const PackCtl &pc, int elast) {
+  constexpr int KP = kPipeKP;
+  const int t = threadIdx.x;
+  const int bf = it & 1;
+  pipe_gather<MODE, W>(gb, sb, tab, a_prev);                                       // tile it+1
+  pipe_load<MODE>(sc, it + 2, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);  // tile it+2
+  bool any_esc = false;
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {
+    const int q = t + k * kBlock;
+    double er;
+    if constexpr (W == 0) {
+      er = __longlong_as_double((long long)ga[k]);
+    } else {
+      constexpr unsigned long long esc = W == 32 ? 0xFFFFFFFFull : (1ull << W) - 1ull;
+      er = dkey_inv(pp.base + ga[k]);
+      any_esc |= q < sa.ne && ga[k] == esc;
+    }
+    if (q < sa.ne) {
+      L.x[bf][q] = sa.x[k];
+      L.er[bf][MODE ? (int)(sa.c[k] & 0xFFFFu) : q] = er;
+    }
+  }
+  if constexpr (W != 0) {
+    // escapes (rare): the double, through the edge's column, written over the LDS slot. The
+    // load completes inside the branch (explicit wait), so the common path never waits for
+    // it, and with it for every prefetch issued before it.
+    if (__builtin_expect(__any(any_esc), 0)) {
+      constexpr unsigned long long esc = W == 32 ? 0xFFFFFFFFull : (1ull << W) - 1ull;
+#pragma unroll
+      for (int k = 0; k < KP; ++k) {
+        const int q = t + k * kBlock;
+        if (q < sa.ne && ga[k] == esc) {
+          const int pos = MODE ? (int)(sa.c[k] & 0xFFFFu) : q;
+          L.er[bf][pos] = a_prev[MODE ? col[sa.e0 + pos] : (int)sa.c[k]];
+        }
+      }
+      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
+    }
+  }
+  if (t <= sa.nn) L.rp[bf][t] = sa.rp;
+  __syncthreads();
+  if (t < sa.nn) {  // phase B (CA:106-113)
+    const int qb = L.rp[bf][t] - sa.e0, qe = L.rp[bf][t + 1] - sa.e0;
+    double S = 0.0, T = 0.0;
+    for (int q = qb; q < qe; ++q) {
+      const double e_ = L.er[bf][q];
+      const double fr = recon_fr(L.x[bf][q], e_, sa.own2);
+      L.x[bf][q] = fr;
+      L.own[bf][q] = (unsigned char)t;
+      S = S + fr;
+      T = T + e_;
+    }
+    const double a = ((sa.vv - S) + T) / (double)(qe - qb + 1);
+    L.a[bf][t] = a;
+    a_new[sa.nb + t] = a;
+    if (pc.width) put_code(pc, code_new, sa.nb + t, a);
+    if (CHECK) {
+      const unsigned long long b2 = err_bits(a, target[sa.nb + t]);
+      eb = b2 > eb ? b2 : eb;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < KP; ++k) {  // phase C (CA:117-118)
+    const int q = t + k * kBlock;
+    if (q < sa.ne) {
+      F[sa.e0 + q] = (L.x[bf][q] + L.a[bf][L.own[bf][q]]) - L.er[bf][q];
+    }
+  }
+}
+
+template <bool CHECK, int MODE, int W>
+__device__ inline unsigned long long pipe_tiles(
+    PipeLds &L, int m, const int *__restrict__ rowptr, const int *__restrict__ col,
+    const unsigned *__restrict__ cidx, const void *__restrict__ tab, const double *__restrict__ v,
+    double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
+    double *__restrict__ a_new, const double *__restrict__ target, void *__restrict__ code_new,
+    const PackCtl &pp, const PackCtl &pc, int elast) {
+  unsigned long long eb = 0;
+  PipeStream s0, s1, s2;
+  unsigned long long g0[kPipeKP], g1[kPipeKP];
+  pipe_load<MODE>(s0, 0, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);
+  pipe_load<MODE>(s1, 1, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);
+  pipe_gather<MODE, W>(g0, s0, tab, a_prev);
+#define FU_STEP(K, SA, SB, SC, GA, GB)                                                             \
+  if (it + K >= m) break;                                                                          \
+  pipe_step<CHECK, MODE, W>(L, it + K, m, SA, SB, SC, GA, GB, eb, rowptr, col, cidx, tab, v, F,    \
+                            a_prev, a_prev2, a_new, target, code_new, pp, pc, elast)
+  for (int it = 0; it < m; it += 6) {
+    FU_STEP(0, s0, s1, s2, g0, g1);
+    FU_STEP(1, s1, s2, s0, g1, g0);
+    FU_STEP(2, s2, s0, s1, g0, g1);
+    FU_STEP(3, s0, s1, s2, g1, g0);
+    FU_STEP(4, s1, s2, s0, g0, g1);
+    FU_STEP(5, s2, s0, s1, g1, g0);
+  }
+#undef FU_STEP
+  return eb;
+}
+
+template <bool CHECK, int MODE>
+__global__ __launch_bounds__(kBlock) void k_round_pipe(
+    const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
+    const int4 *__restrict__ heavy, int nheavy, const int *__restrict__ rowptr,
+    const int *__restrict__ col, const unsigned *__restrict__ sidx, const void *__restrict__ G,
+    const double *__restrict__ v, double *__restrict__ F, const double *__restrict__ a_prev,
+    const double *__restrict__ a_prev2, double *__restrict__ a_new,
+    const double *__restrict__ target, unsigned long long *__restrict__ err,
+    const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
+    int rslot, int elast) {
+  constexpr int TE = kPipeTE;
+  __shared__ PipeLds L;
+  const PackCtl pp = ctl[rslot ^ 1];
+  const PackCtl pc = ctl[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
+  const int t = threadIdx.x;
+  unsigned long long eb = 0;
+
+  if ((int)blockIdx.x < nheavy) {
+    // ---------------- heavy row: kernel 4's exact chunked chain ----------------
+    const int4 tl = heavy[blockIdx.x];
+    const int i = tl.x, b = tl.z, e = tl.w;
+    const double own2 = a_prev2[i];
+    double S = 0.0, T = 0.0;
+    for (int c0 = b; c0 < e; c0 += TE) {
+      const int cn = min(TE, e - c0);
+      for (int q = t; q < cn; q += kBlock) {
+        const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
+        L.x[0][q] = recon_fr(F[c0 + q], er, own2);
+        L.er[0][q] = er;
+      }
+      __syncthreads();
+      if (t < 64) {
+        for (int q = 0; q < cn; ++q) {
+          S = S + L.x[0][q];
+          T = T + L.er[0][q];
+        }
+      }
+      __syncthreads();
+    }
+    if (t == 0) {
+      const double a = ((v[i] - S) + T) / (double)(e - b + 1);
+      L.a[0][0] = a;
+      a_new[i] = a;
+      if (pc.width) put_code(pc, code_new, i, a);
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = L.a[0][0];
+    for (int k = b + t; k < e; k += kBlock) {
+      const double er = ld_est(pp, code_prev, a_prev, col[k]);
+      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
+
+  // ---------------- light tiles: this block's list (XCD-aware) ----------------
+  const int bid = (int)blockIdx.x - nheavy, nbl = (int)gridDim.x - nheavy;  // nbl % 8 == 0
+  const int x = bid & 7, j = bid >> 3, nbx = nbl >> 3;
+  const int per = ntl >> 3, rem = ntl & 7;
+  const int lo = x * per + min(x, rem), hi = lo + per + (x < rem ? 1 : 0);
+  const int m = j < hi - lo ? (hi - lo - j + nbx - 1) / nbx : 0;
+  if (t < m) {
+    L.tl[t] = tiles[lo + j + t * nbx];
+    if (MODE) L.gb[t] = tgbase[lo + j + t * nbx];
+  }
+  if (t == 0 && m == 0) {  // keep the clamped prefetch of an empty list in bounds
+    L.tl[0] = make_int4(0, 0, 0, 0);
+    L.gb[0] = 0;
+  }
+  __syncthreads();
+  const unsigned *cidx = MODE ? sidx : reinterpret_cast<const unsigned *>(col);
+  const void *tab = MODE ? G : code_prev;
+#define FU_TILES(W_)                                                                                  \
+  pipe_tiles<CHECK, MODE, W_>(L, m, rowptr, col, cidx, tab, v, F, a_prev, a_prev2, a_new, target,     \
+                              code_new, pp, pc, elast)
+  if (pp.width == 0) eb = FU_TILES(0);
+  else if (pp.width == 8) eb = FU_TILES(8);
+  else if (pp.width == 16) eb = FU_TILES(16);
+  else eb = FU_TILES(32);
+#undef FU_TILES
+  if (CHECK) block_max_to(eb, err);
+}
+
 __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) p[q] = val;
@@ -1230,7 +1726,7 @@ struct fu_handle {
   int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
   bool tuned = false;
-  float tune_ms[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // per candidate (autotune_kernel order)
+  float tune_ms[12] = {};  // per candidate (autotune_kernel order)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
   int tuned_width = 0;    // packing width the last pass ran under
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
@@ -1272,6 +1768,30 @@ struct fu_handle {
   int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
   int tile_nodes = 0;
   bool has_target = false;
+  // kernel 8 (LDS-staged slices): light tiles of kStageTE x kStageTN in edge groups, heavy
+  // rows as kernel 4 heavy tiles, and one slice layout per table element width
+  struct StageLayout {
+    int P = 0, Q = 0;              // slices, blocks per slice
+    int *aoff = nullptr;           // per stage block: first entry in aitem
+    int2 *aitem = nullptr;         // per stage block: {segment start, flat prefix}..., {0, total}
+    unsigned short *colS = nullptr;  // per staged element: column offset within its slice
+    unsigned *sidx = nullptr;      // per tile edge (slice order): G index in group << 16 | position
+  };
+  StageLayout st[4];            // element bytes 1, 2, 4, 8
+  bool st_ready = false;
+  int st_ngroups = 0;
+  int4 *st_tiles = nullptr;     // light tiles
+  int *st_gbase = nullptr;      // per light tile: first edge of its group
+  int st_ntiles = 0;
+  int4 *st_heavy = nullptr;     // rows above the tile limit ({i, -1, b, e})
+  int st_nheavy = 0;
+  void *stG = nullptr;          // staged estimates, 8 B per light edge
+  int seen_width = 0;           // packing width the host last saw (layout choice)
+  int st_force = -1;            // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
+  std::vector<int4> h_light;    // host copies (layout construction)
+  std::vector<int32_t> h_gstart;
+  int n_cu = 256;               // compute units (kernel 9 grid)
+  int pipe_bpc = 6;             // kernel 9/10: persistent blocks per CU
   // multi-GPU (fu_dist.hip)
   void *dist = nullptr;
 };
@@ -1469,6 +1989,161 @@ int ensure_split(fu_handle *h) {
   return FU_OK;
 }
 
+// Kernel 8 preparation: light tiles, edge groups and the four slice layouts.
+constexpr int kStageMaxP = 512;      // slices per layout (more: layout not built)
+constexpr int kStageGroupEdges = 65536;  // G index within a group is u16
+
+// Light tiles (kStageTE x kStageTN), their edge groups and the heavy rows (kernels 8-10).
+int ensure_light(fu_handle *h) {
+  if (h->st_tiles) return FU_OK;
+  const int32_t n = h->n;
+  const auto &rp = h->h_rowptr;
+  const int64_t lim = std::min<int64_t>(h->hub_threshold, kStageTE);
+  std::vector<int4> light, heavy;
+  std::vector<int32_t> gstart;  // per group: first light tile
+  int64_t gedges = 0;
+  bool prev_light = false;
+  for (int32_t i = 0; i < n;) {
+    const int64_t d = rp[i + 1] - rp[i];
+    if (d > lim) {
+      heavy.push_back(make_int4(i, -1, (int)rp[i], (int)rp[i + 1]));
+      ++i;
+      prev_light = false;
+      continue;
+    }
+    const int32_t b = i;
+    while (i < n && i - b < kStageTN) {
+      const int64_t di = rp[i + 1] - rp[i];
+      if (di > lim || rp[i + 1] - rp[b] > kStageTE) break;
+      ++i;
+    }
+    const int64_t te = rp[i] - rp[b];
+    if (!prev_light || gedges + te > kStageGroupEdges) {
+      gstart.push_back((int32_t)light.size());
+      gedges = 0;
+    }
+    light.push_back(make_int4(b, i, (int)rp[b], (int)rp[i]));
+    gedges += te;
+    prev_light = true;
+  }
+  const int ng = (int)gstart.size();
+  gstart.push_back((int32_t)light.size());
+  std::vector<int32_t> gbase(light.size());
+  for (int g = 0; g < ng; ++g)
+    for (int t = gstart[g]; t < gstart[g + 1]; ++t) gbase[t] = light[gstart[g]].z;
+  auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
+    if (int rc = dmalloc(dst, std::max<size_t>(1, cnt))) return rc;
+    if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
+    return FU_OK;
+  };
+  h->h_light = light;
+  h->h_gstart = gstart;
+  if (int rc = up(&h->st_tiles, light.data(), light.size())) return rc;
+  if (int rc = up(&h->st_gbase, gbase.data(), gbase.size())) return rc;
+  if (int rc = up(&h->st_heavy, heavy.data(), heavy.size())) return rc;
+  h->st_ntiles = (int)light.size();
+  h->st_nheavy = (int)heavy.size();
+  h->st_ngroups = ng;
+  return FU_OK;
+}
+
+// Kernel 8 / 10: the staged-estimate buffer and the four slice layouts.
+int ensure_stage(fu_handle *h) {
+  if (h->st_ready) return FU_OK;
+  if (int rc = ensure_light(h)) return rc;
+  const int32_t n = h->n;
+  const int ng = h->st_ngroups;
+  const std::vector<int4> &light = h->h_light;
+  const std::vector<int32_t> &gstart = h->h_gstart;
+  auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
+    if (int rc = dmalloc(dst, std::max<size_t>(1, cnt))) return rc;
+    if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
+    return FU_OK;
+  };
+  if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)h->E)) return rc;
+  HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long)));
+  for (int li = 0; li < 4; ++li) {
+    const int64_t SN = kStageLds >> li;
+    const int64_t P = (n + SN - 1) / SN;
+    auto &L = h->st[li];
+    if (P > kStageMaxP) continue;
+    std::vector<int32_t> segs((size_t)ng * (P + 1));
+    std::vector<uint16_t> colS(h->E > 0 ? h->E : 1);
+    std::vector<uint32_t> sidx(h->E > 0 ? h->E : 1);
+    std::vector<int32_t> cur(P + 1);
+    std::vector<int32_t> kpos;
+    for (int g = 0; g < ng; ++g) {
+      const int t0 = gstart[g], t1 = gstart[g + 1];
+      const int32_t ge0 = light[t0].z, ge1 = light[t1 - 1].w;
+      std::fill(cur.begin(), cur.end(), 0);
+      for (int32_t e = ge0; e < ge1; ++e) cur[h->h_col[e] / SN + 1]++;
+      for (int64_t s = 0; s < P; ++s) cur[s + 1] += cur[s];
+      for (int64_t s = 0; s <= P; ++s) segs[(size_t)g * (P + 1) + s] = ge0 + cur[s];
+      kpos.assign(ge1 - ge0, 0);
+      for (int32_t e = ge0; e < ge1; ++e) {  // stable: (slice, tile, position) order
+        const int32_t c = h->h_col[e];
+        const int32_t k = cur[c / SN]++;
+        colS[ge0 + k] = (uint16_t)(c % SN);
+        kpos[e - ge0] = k;
+      }
+      for (int t = t0; t < t1; ++t) {  // tile elements in slice order (stable in position)
+        const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
+        std::vector<int32_t> ord(ne);
+        for (int32_t m = 0; m < ne; ++m) ord[m] = m;
+        std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
+          return h->h_col[e0 + x] / SN < h->h_col[e0 + y] / SN;
+        });
+        for (int32_t m = 0; m < ne; ++m)
+          sidx[e0 + m] = ((uint32_t)kpos[e0 + ord[m] - ge0] << 16) | (uint32_t)ord[m];
+      }
+    }
+    // stage blocks (s, q), blockIdx = s + P * q (slice s on XCD s % 8 when 8 | P): q takes
+    // groups [ng q / Q, ng (q+1) / Q), at most kStageMaxItems - 1 of them
+    int64_t Q = std::max<int64_t>(1, std::min<int64_t>(ng, 512 / P));
+    Q = std::max<int64_t>(Q, (ng + kStageMaxItems - 2) / (kStageMaxItems - 1));
+    std::vector<int32_t> aoff(P * Q + 1, 0);
+    std::vector<int2> aitem;
+    for (int64_t q = 0; q < Q; ++q)
+      for (int64_t s = 0; s < P; ++s) {
+        const int64_t b = s + P * q;
+        const int64_t g0 = ng * q / Q, g1 = ng * (q + 1) / Q;
+        aoff[b] = (int32_t)aitem.size();
+        int32_t pre = 0;
+        for (int64_t g = g0; g < g1; ++g) {
+          const int32_t kb = segs[g * (P + 1) + s], ke = segs[g * (P + 1) + s + 1];
+          if (ke > kb) aitem.push_back(make_int2(kb, pre));
+          pre += ke - kb;
+        }
+        aitem.push_back(make_int2(0, pre));
+      }
+    aoff[P * Q] = (int32_t)aitem.size();  // q outer, s inner: b = s + P q in order
+    L.P = (int)P;
+    L.Q = (int)Q;
+    if (int rc = up(&L.aoff, aoff.data(), aoff.size())) return rc;
+    if (int rc = up(&L.aitem, aitem.data(), aitem.size())) return rc;
+    if (int rc = up(&L.colS, colS.data(), (size_t)h->E)) return rc;
+    if (int rc = up(&L.sidx, sidx.data(), (size_t)h->E)) return rc;
+    if (h->E == 0) HIP_TRY(hipMemset(L.sidx, 0, sizeof(unsigned)));  // kernel 10 reads sidx[0]
+  }
+  bool any = false;
+  for (int li = 0; li < 4; ++li) any |= h->st[li].P > 0;
+  if (!any) return fail(FU_ERR_GRAPH, "kernel 8 (staged slices): graph has too many nodes for a slice layout");
+  h->st_ready = true;
+  return FU_OK;
+}
+
+// Layout for the packing width the host last saw: the narrowest built layout that holds
+// the table's elements in LDS, else the widest built one (the stage launch then gathers).
+inline int stage_layout(fu_handle *h) {
+  if (h->st_force >= 0 && h->st[h->st_force].P) return h->st_force;
+  const int want = h->seen_width == 8 ? 0 : h->seen_width == 16 ? 1 : h->seen_width == 32 ? 2 : 3;
+  for (int li = want; li < 4; ++li)
+    if (h->st[li].P) return li;
+  for (int li = want; li >= 0; --li)
+    if (h->st[li].P) return li;
+  return -1;
+}
+
 int ensure_a2(fu_handle *h) {
   if (h->a[2]) return FU_OK;
   if (int rc = dmalloc(&h->a[2], (size_t)h->na)) return rc;
@@ -1539,6 +2214,81 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         hipLaunchKernelGGL(k_round_split<false>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
                            h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
                            h->target, err_slot, h->pctl, (int)(r & 1));
+    } else if (h->kernel == 9 || h->kernel == 10) {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+      const void *cp = h->code[(r - 1) & 1];
+      const bool staged = h->kernel == 10;
+      const int li = staged ? stage_layout(h) : 0;
+      const fu_handle::StageLayout &L = h->st[li < 0 ? 0 : li];
+      if (staged && h->st_ngroups) {
+        const dim3 grid((unsigned)(L.P * L.Q));
+#define FU_STAGE(LB)                                                                              \
+  hipLaunchKernelGGL(k_stage<LB>, grid, dim3(kStageThreads), 0, h->stream, L.P, h->n, L.aoff, L.aitem, \
+                     L.colS, ap, cp, h->pctl, (int)(r & 1), h->stG)
+        if (li == 0) FU_STAGE(1); else if (li == 1) FU_STAGE(2); else if (li == 2) FU_STAGE(4); else FU_STAGE(8);
+#undef FU_STAGE
+      }
+      long long nbl = std::max<long long>((h->st_ntiles + kPipeChunk - 1) / kPipeChunk, (long long)h->pipe_bpc * h->n_cu);
+      nbl = std::min<long long>(nbl, ((long long)h->st_ntiles + 7) / 8 * 8);
+      nbl = std::max<long long>(8, (nbl + 7) / 8 * 8);
+      const dim3 grid((unsigned)(nbl + h->st_nheavy));
+#define FU_PIPE(C, M)                                                                                  \
+  hipLaunchKernelGGL((k_round_pipe<C, M>), grid, dim3(kBlock), 0, h->stream, h->st_tiles, h->st_gbase,       \
+                     h->st_ntiles, h->st_heavy, h->st_nheavy, h->rowptr, h->col, L.sidx, h->stG, h->v, F, ap, \
+                     ap2, an, h->target, err_slot, cp, h->code[r & 1], h->pctl, (int)(r & 1),           \
+                     (int)std::max<int64_t>(0, h->E - 1))
+      if (check) {
+        if (staged) FU_PIPE(true, 1); else FU_PIPE(true, 0);
+      } else {
+        if (staged) FU_PIPE(false, 1); else FU_PIPE(false, 0);
+      }
+#undef FU_PIPE
+    } else if (h->kernel == 8) {
+      double *F = h->f[r & 1];
+      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+      double *an = h->a[r % 3];
+      const int li = stage_layout(h);
+      const fu_handle::StageLayout &L = h->st[li];
+      const void *cp = h->code[(r - 1) & 1];
+      if (h->st_ngroups && h->diag < 2) {
+        const dim3 grid((unsigned)(L.P * L.Q));
+#define FU_STAGE(LB)                                                                              \
+  hipLaunchKernelGGL(k_stage<LB>, grid, dim3(kStageThreads), 0, h->stream, L.P, h->n, L.aoff, L.aitem, \
+                     L.colS, ap, cp, h->pctl, (int)(r & 1), h->stG)
+        if (li == 0) FU_STAGE(1); else if (li == 1) FU_STAGE(2); else if (li == 2) FU_STAGE(4); else FU_STAGE(8);
+#undef FU_STAGE
+      }
+      if (h->st_nheavy) {
+        if (check)
+          hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
+                             h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1));
+        else
+          hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
+                             h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1));
+      }
+      if (h->st_ntiles && h->diag) {
+        if (h->diag == 3)
+          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 3>), dim3(h->st_ntiles), dim3(kBlock), 0,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
+        else
+          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 1>), dim3(h->st_ntiles), dim3(kBlock), 0,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
+      } else if (h->st_ntiles) {
+        if (check)
+          hipLaunchKernelGGL((k_round_staged<true, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
+        else
+          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
+      }
     } else if (h->kernel == 7) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -1716,6 +2466,10 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   auto cleanup = [&](int code) { fu_destroy(h); return code; };
   if ((rc = set_device(h))) return cleanup(rc);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) h->n_cu = cus;
+  }
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess)
@@ -1734,7 +2488,8 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       (e && !no_rev && hipMemcpy(h->rev, rev, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(h->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
-  if (hipMemset(h->f[0], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
+  if ((e == 0 && hipMemset(h->col, 0, sizeof(int)) != hipSuccess) ||  // kernels 9/10 read col[0]
+      hipMemset(h->f[0], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
       hipMemset(h->f[1], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
       hipMemset(h->a[0], 0, sizeof(double) * na) != hipSuccess ||
       hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess)
@@ -1790,7 +2545,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 7) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..7");
+    if (value < 0 || value > 10) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..10");
     if (h->dist && value != 0 && value != 2 && value != 4)  // 5, 6: single GPU only
       return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
     if (!h->rev && h->E > 0 && value >= 1 && value <= 3)
@@ -1802,6 +2557,20 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->nt = 0;
     if (h->kernel == 3) return ensure_inbox(h);
     if (h->kernel == 4 || h->kernel == 7) return ensure_a2(h);
+    if (h->kernel == 9) {
+      if (int rc = ensure_a2(h)) return rc;
+      if (int rc = ensure_light(h)) {
+        h->kernel = 4;
+        return rc;
+      }
+    }
+    if (h->kernel == 8 || h->kernel == 10) {
+      if (int rc = ensure_a2(h)) return rc;
+      if (int rc = ensure_stage(h)) {
+        h->kernel = 4;
+        return rc;
+      }
+    }
     if (h->kernel == 5 || h->kernel == 6) {
       if (int rc = ensure_a2(h)) return rc;
       if (int rc = ensure_split(h)) {
@@ -1809,6 +2578,16 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
         return rc;
       }
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "stage_layout")) {  // kernel 8: -1 = by packing width, 0..3 forced
+    if (value < -1 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: stage_layout must be -1..3");
+    h->st_force = (int)value;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "pipe_bpc")) {  // kernels 9/10: persistent blocks per CU
+    if (value < 1 || value > 64) return fail(FU_ERR_ARG, "fu_set_option: pipe_bpc must be in [1, 64]");
+    h->pipe_bpc = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "diag")) {
@@ -1864,6 +2643,9 @@ int fu_reset(fu_handle *h) {
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
   h->cur = 0;
+  h->pw_pending = false;  // the stream is idle: no plan copy in flight
+  *h->h_pw = 0;           // round 0 clears the packing plan
+  h->seen_width = 0;
   return FU_OK;
 }
 
@@ -1900,10 +2682,12 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   };
   // kernel 7 (wave tiles) is not a candidate: slower than kernel 4 at 512x64 everywhere
   // measured; it stays selectable as an option
-  std::vector<Cand> cands = {{4, 0, 0}, {4, 1, 0}, {4, 0, 2}, {4, 0, 3}};
+  // measured on ER-1M / R-MAT: 4+nt, 4 at 1024x256, 5 and 9 never win; they stay options
+  std::vector<Cand> cands = {{4, 0, 0}, {4, 0, 3}};
   if (!h->dist) {
     cands.push_back({6, 0, 0});
-    cands.push_back({5, 0, 0});
+    cands.push_back({8, 0, 0});
+    cands.push_back({10, 0, 0});
   }
   constexpr int kTimed = 4;
   const int32_t need = (1 + kTimed) * (int32_t)cands.size();
@@ -1912,7 +2696,17 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   int bi = -1;
   for (size_t c = 0; c < cands.size(); ++c) {
     h->tune_ms[c] = 0.f;
-    if (cands[c].kernel >= 5) {
+    if (cands[c].kernel == 9) {
+      if (ensure_light(h) != FU_OK) {
+        set_error("");
+        continue;
+      }
+    } else if (cands[c].kernel == 8 || cands[c].kernel == 10) {
+      if (ensure_stage(h) != FU_OK) {  // too many nodes for a slice layout
+        set_error("");
+        continue;
+      }
+    } else if (cands[c].kernel >= 5) {
       if (ensure_split(h) != FU_OK) {  // rows not sorted: column split not applicable
         set_error("");
         continue;
@@ -1951,6 +2745,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
 static void poll_pack_width(fu_handle *h) {
   if (!h->pw_pending || hipEventQuery(h->ev_pw) != hipSuccess) return;
   h->pw_pending = false;
+  h->seen_width = *h->h_pw;
   if (h->autotune && h->tuned && *h->h_pw != h->tuned_width && h->n_tunes < kMaxTunes) h->tuned = false;
 }
 
@@ -2056,7 +2851,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   return FU_OK;
 }
 
-int fu_get_info(fu_handle *h, int64_t info[16]) {
+int fu_get_info(fu_handle *h, int64_t info[32]) {
   if (!h || !info) return fail(FU_ERR_ARG, "fu_get_info: NULL argument");
   info[0] = h->kernel;
   info[1] = h->nt;
@@ -2066,7 +2861,7 @@ int fu_get_info(fu_handle *h, int64_t info[16]) {
   info[5] = kGeoNodes[h->geo];
   info[6] = h->n_tunes;
   info[7] = h->tuned_width;
-  for (int k = 0; k < 8; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  for (int k = 0; k < 12; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
   return FU_OK;
 }
 
@@ -2103,7 +2898,11 @@ int fu_destroy(fu_handle *h) {
                   h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3], h->wtiles[0], h->wtiles[1],
                   h->wheavy[0], h->wheavy[1],
                   h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm,
-                  h->code[0], h->code[1], h->pctl, h->psample};
+                  h->code[0], h->code[1], h->pctl, h->psample, h->st_tiles, h->st_gbase, h->st_heavy,
+                  h->stG, h->st[0].aoff, h->st[0].aitem, h->st[0].colS, h->st[0].sidx, h->st[1].aoff,
+                  h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
+                  h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
+                  h->st[3].sidx};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

@@ -134,7 +134,7 @@ using namespace fu;
 extern "C" {
 
 const char *fu_last_error(void) { return fu::g_err.c_str(); }
-int fu_version(void) { return 1; }
+int fu_version(void) { return 2; }
 
 int fu_graph_from_edges(int32_t n, int64_t m, const int32_t *src, const int32_t *dst,
                         fu_graph **out) {

@@ -16,7 +16,8 @@ import numpy as np
 from . import _lib as L
 from .graph import Graph
 
-KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6, "wave": 7}
+KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6, "wave": 7, "stage": 8, "pipe": 9,
+           "pipe_stage": 10}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
@@ -98,16 +99,17 @@ class CollectAll:
 
     def info(self) -> dict:
         """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
-        a = np.zeros(16, dtype=np.int64)
+        a = np.zeros(32, dtype=np.int64)
         L.call("fu_get_info", self._h, L.ptr(a))
-        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave"}
+        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave", 8: "stage", 9: "pipe",
+                 10: "pipe_stage"}
         return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
                 "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
                 "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
                 "tuned_pack_width": int(a[7]),
                 "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
-                                      enumerate(("recon", "recon_nt", "recon_1024x256", "recon_512",
-                                                 "split2", "split"))}}
+                                      enumerate(("recon", "recon_512", "split2", "stage",
+                                                 "pipe_stage"))}}
 
     def pack_widths(self) -> tuple:
         """Packed estimate table widths (0 = doubles): the last even / odd round's code

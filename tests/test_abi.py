@@ -30,7 +30,7 @@ def test_every_declared_symbol_is_exported():
 
 
 def test_version_and_device_count():
-    assert L.lib.fu_version() == 1
+    assert L.lib.fu_version() == 2
     assert fu.device_count() >= 0
 
 

@@ -15,7 +15,7 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["thread", "tile", "push", "recon", "split", "split2", "wave"]
+KERNELS = ["thread", "tile", "push", "recon", "split", "split2", "wave", "stage", "pipe", "pipe_stage"]
 
 
 def _rows_sorted(rowptr, col):
@@ -46,7 +46,8 @@ def test_ca_sync_fixture_bitwise(name, meta, kernel):
     _check_fixture(meta, kernel)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave", "stage", "pipe",
+                                    "pipe_stage"])
 @pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
 def test_ca_sync_fixture_heavy_path(name, kernel):
     """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
@@ -65,7 +66,8 @@ def test_er_vs_c_oracle_bitwise(kernel):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave"])
+@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave", "stage", "pipe",
+                                    "pipe_stage"])
 def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.rmat(15, 16, seed=2)
     assert g.max_deg > 2048  # exercises chunked heavy tiles
@@ -122,7 +124,7 @@ def test_option_errors():
     g = fu.Graph.random_regular(64, 4, seed=1)
     eng = fu.CollectAll(g, np.ones(g.n))
     with pytest.raises(fu.FuError):
-        eng.set_option("kernel", 9)
+        eng.set_option("kernel", 11)
     with pytest.raises(fu.FuError):
         eng.set_option("nope", 1)
     with pytest.raises(fu.FuError):
@@ -309,7 +311,9 @@ def _er_with_outlier_pairs(n, m, pairs, seed):
 
 
 @pytest.mark.parametrize("kind,kernel", [("er", "recon"), ("rmat", "recon"), ("rmat_bins", "recon"),
-                                         ("er", "wave"), ("rmat", "wave")])
+                                         ("er", "wave"), ("rmat", "wave"), ("er", "stage"),
+                                         ("rmat", "stage"), ("er", "pipe"), ("rmat", "pipe"),
+                                         ("er", "pipe_stage"), ("rmat", "pipe_stage")])
 def test_packed_gather_long_run_bitwise(kind, kernel):
     """The packed estimate table (8/16/32-bit lossless codes + escapes) switches on as the
     estimates converge; 300 rounds must still equal the C oracle bit for bit, and equal the
@@ -346,7 +350,7 @@ def test_packed_gather_with_kernel_switches():
     g = fu.Graph.erdos_renyi(50_000, 200_000, seed=9)
     v = fu.uniform_values(g.n, seed=9)
     ref = None
-    for kernel in ("recon", "split2", "wave", "auto"):
+    for kernel in ("recon", "split2", "wave", "stage", "pipe", "pipe_stage", "auto"):
         eng = fu.CollectAll(g, v, kernel=kernel)
         eng.set_option("pack_every", 2)
         eng.run(260)
@@ -375,5 +379,42 @@ def test_tile_geometries_bitwise(kernel, opts, kind):
         eng.set_option(k, val)
     eng.run(30)
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
+@pytest.mark.parametrize("kernel", ["stage", "pipe_stage"])
+@pytest.mark.parametrize("layout", [0, 1, 2, 3])
+def test_stage_forced_layouts_bitwise(layout, kernel):
+    """Kernel 8 with each slice layout forced (1/2/4/8-byte elements) over a run in which the
+    table goes from doubles to 32/16/8-bit codes: a table wider than the layout is gathered
+    from global memory by the stage launch, a narrower one sits in LDS; escapes (far-off
+    2-node components) read the double through the edge's column. Heavy rows (R-MAT part)
+    run as kernel 4 heavy tiles."""
+    g, v = _er_with_outlier_pairs(60_000, 240_000, 32, seed=11)
+    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=16)
+    eng.set_option("stage_layout", layout)
+    eng.set_option("pack_every", 4)
+    seen = set()
+    for _ in range(12):
+        eng.run(25)
+        seen.update(eng.pack_widths())
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 300, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    assert seen & {8, 16, 32}, seen
+
+
+@pytest.mark.parametrize("bpc", [1, 3, 8])
+@pytest.mark.parametrize("kernel", ["pipe", "pipe_stage"])
+def test_pipe_grid_sizes_bitwise(kernel, bpc):
+    """Kernels 9/10 with few persistent blocks (long tile lists per block, up to the 64-tile
+    chunk) and many, on R-MAT (hub blocks at the front of the grid) against the C oracle."""
+    g = fu.Graph.rmat(15, 16, seed=7)
+    v = fu.uniform_values(g.n, seed=7)
+    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=32)
+    eng.set_option("pipe_bpc", bpc)
+    eng.run(20)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)

@@ -41,6 +41,25 @@ VARIANTS = {
     "diag5_no_hub_chain": ("recon", {"diag": 5}),
     "recon_hub256": ("recon", {"hub_threshold": 256}),
     "recon_hub2048": ("recon", {"hub_threshold": 2048}),
+    "stage": ("stage", {}),
+    "stage_nopack": ("stage", {"pack": 0}),
+    "diag1_stage": ("stage", {"diag": 1}),
+    "diag2_stage": ("stage", {"diag": 2}),
+    "diag1_stage_nopack": ("stage", {"pack": 0, "diag": 1}),
+    "diag2_stage_nopack": ("stage", {"pack": 0, "diag": 2}),
+    "diag3_stage": ("stage", {"diag": 3}),
+    "pipe": ("pipe", {}),
+    "pipe_nopack": ("pipe", {"pack": 0}),
+    "pipe_stage": ("pipe_stage", {}),
+    "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
+    "pipe_b2": ("pipe", {"pipe_bpc": 2}),
+    "pipe_b4": ("pipe", {"pipe_bpc": 4}),
+    "pipe_b8": ("pipe", {"pipe_bpc": 8}),
+    "pipe_stage_b4": ("pipe_stage", {"pipe_bpc": 4}),
+    "pipe_stage_b8": ("pipe_stage", {"pipe_bpc": 8}),
+    "diag3_stage_nopack": ("stage", {"pack": 0, "diag": 3}),
+    "diag1_512_nopack": ("recon", {"tile_edges": 512, "pack": 0, "diag": 1}),
+    "recon_512_nopack": ("recon", {"tile_edges": 512, "pack": 0}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
