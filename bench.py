@@ -58,6 +58,22 @@ def parse():
     return ap.parse_args()
 
 
+def round_kernels(kinfo):
+    """The launches one round of the selected kernel consists of (the roofline's unit)."""
+    k = kinfo["kernel"]
+    if k == "recon":
+        return "k_round_recon %dx%d%s" % (kinfo["tile"][0], kinfo["tile"][1], "+nt" if kinfo["nt"] else "")
+    if k == "stage":
+        return "k_stage + k_round_staged 512x64"
+    if k == "pipe_stage":
+        return "k_stage + k_round_pipe<staged> 512x64"
+    if k == "pipe":
+        return "k_round_pipe<recon> 512x64"
+    if k == "split2":
+        return "k_gather_part0 + k_round_split"
+    return k
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -198,7 +214,7 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
-                "kernel": kinfo["kernel"] + ("+nt" if kinfo["nt"] else "") + " %dx%d" % kinfo["tile"],
+                "kernel": round_kernels(kinfo),
                 "avg_launch_us": dom_s * 1e6,
                 "launch_window": "rounds %d-%d" % (tail[0]["rounds"][0], tail[-1]["rounds"][1]),
                 "whole_region_avg_round_us": avg_round_s * 1e6,

@@ -128,7 +128,7 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done);
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
  * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
  * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run). With kernel
- * "auto" (the default) a fu_run_collectall(_timed) with >= 25 rounds left after round 0
+ * "auto" (the default) a fu_run_collectall(_timed) with >= 45 rounds left after round 0
  * times the candidates on real rounds (they share state and are bitwise identical) and keeps
  * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */
 int fu_get_info(fu_handle *h, int64_t info[32]);  /* ABI 2: 32 entries */

@@ -65,6 +65,8 @@ __device__ inline void block_max_to(unsigned long long x, unsigned long long *ds
 // ------------------------------------------------------------------------------------
 // Round 0: the timeout fire on zero state (CA:33-34, CA:87-91 -> CA:105-128)
 // ------------------------------------------------------------------------------------
+// SPLIT: kernels >= 4 keep flows as split words (see st_f); kernels 1-3 as doubles
+template <bool SPLIT>
 __global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict__ rowptr,
                                                    const double *__restrict__ v,
                                                    double *__restrict__ f,
@@ -75,7 +77,16 @@ __global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict_
   double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
   a[i] = ai;
   double fv = (0.0 + ai) - 0.0;
-  for (int k = b; k < e; ++k) f[k] = fv;
+  for (int k = b; k < e; ++k) {
+    if constexpr (SPLIT) {
+      unsigned *w = reinterpret_cast<unsigned *>(f);
+      const long long j = ((long long)(k & ~31) << 1) | (k & 31);
+      w[j] = (unsigned)__double2hiint(fv);
+      w[j + 32] = (unsigned)__double2loint(fv);
+    } else {
+      f[k] = fv;
+    }
+  }
 }
 
 // ------------------------------------------------------------------------------------
@@ -301,6 +312,24 @@ struct PackCtl {
   int pad;
 };
 
+// Write-through store (global_store ... sc1): the line leaves the XCD's L2 at once instead
+// of staying dirty there. A kernel's end writes back every dirty L2 line before the next
+// launch may start, so round kernels that leave their output (flows, estimates, codes,
+// staged words) dirty pay that writeback serially at each boundary (MI355X_MICROARCH.md:
+// + bytes / 6 TB/s per boundary); streamed through, it overlaps the kernel's own work.
+// Byte and short sc1 stores go out as one fabric write each (MI355X_MICROARCH.md: 6-12x the
+// per-byte cost of wide ones), so 1- and 2-byte elements keep plain (write-back) stores.
+// Measured on ER-1M: write-through did not shorten the round kernels (kernel 4 lost 4.5 us,
+// kernel 8 gained nothing), so it is off unless built with -DFU_WT=1.
+#ifndef FU_WT
+#define FU_WT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void st_wt(T *p, T v) {
+  if constexpr (FU_WT && sizeof(T) >= 4) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *p = v;
+}
+
 __device__ inline unsigned long long dkey(double x) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(x);
   return (b >> 63) ? ~b : (b | (1ull << 63));
@@ -319,9 +348,9 @@ __device__ inline void put_code(const PackCtl &pc, void *tab, int i, double a) {
   const unsigned long long off = dkey(a) - pc.base;
   const unsigned esc = pc.width == 32 ? 0xFFFFFFFFu : (1u << pc.width) - 1u;
   const unsigned cd = off < (unsigned long long)esc ? (unsigned)off : esc;
-  if (pc.width == 8) reinterpret_cast<unsigned char *>(tab)[i] = (unsigned char)cd;
-  else if (pc.width == 16) reinterpret_cast<unsigned short *>(tab)[i] = (unsigned short)cd;
-  else reinterpret_cast<unsigned *>(tab)[i] = cd;
+  if (pc.width == 8) st_wt(reinterpret_cast<unsigned char *>(tab) + i, (unsigned char)cd);
+  else if (pc.width == 16) st_wt(reinterpret_cast<unsigned short *>(tab) + i, (unsigned short)cd);
+  else st_wt(reinterpret_cast<unsigned *>(tab) + i, cd);
 }
 template <int W>
 __device__ inline double decode_or(unsigned cd, unsigned long long base, const double *a_prev, int j) {
@@ -400,6 +429,35 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
 }
 
 // ------------------------------------------------------------------------------------
+// Flow storage of kernels >= 4 (state shared by kernels 4-10): split words. The flow of
+// edge e is stored as its double's high and low 32-bit words in separate 128-byte lines:
+// block e / 32 holds 32 high words, then 32 low words. Each round rewrites every low word,
+// but a high word (sign, exponent, top 20 mantissa bits) only when it changes. Once the
+// estimates have converged the flows move by a few ulps per round and their high words
+// stay put, so a round writes 4 instead of 8 bytes per edge (the store of an identical
+// word is skipped; the value in memory is always the exact f_r).
+// ------------------------------------------------------------------------------------
+__device__ __forceinline__ long long fhi_idx(int e) { return ((long long)(e & ~31) << 1) | (e & 31); }
+__device__ __forceinline__ double ld_f(const double *F, int e) {
+  const unsigned *w = reinterpret_cast<const unsigned *>(F);
+  const long long i = fhi_idx(e);
+  return __hiloint2double((int)w[i], (int)w[i + 32]);
+}
+// store f_r over f_old (the value the slot held)
+__device__ __forceinline__ void st_f(double *F, int e, double v, double f_old) {
+  unsigned *w = reinterpret_cast<unsigned *>(F);
+  const long long i = fhi_idx(e);
+  st_wt(w + i + 32, (unsigned)__double2loint(v));
+  if (__double2hiint(v) != __double2hiint(f_old)) st_wt(w + i, (unsigned)__double2hiint(v));
+}
+__device__ __forceinline__ void st_f_full(double *F, int e, double v) {
+  unsigned *w = reinterpret_cast<unsigned *>(F);
+  const long long i = fhi_idx(e);
+  st_wt(w + i + 32, (unsigned)__double2loint(v));
+  st_wt(w + i, (unsigned)__double2hiint(v));
+}
+
+// ------------------------------------------------------------------------------------
 // Variant 4: flow reconstruction ("recon"). Node j computed, in round r-1,
 //     f_{r-1}[j->i] = ((-f_{r-2}[i->j]) + a_{r-1}[j]) - a_{r-2}[i]        (CA:99, CA:117)
 // from three operands that node i also holds: its own previous flow f_{r-2}[i->j] (its
@@ -414,6 +472,34 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
 __device__ inline double recon_fr(double f_own_old, double a_nb, double a_own_old2) {
   const double f_rev = ((-f_own_old) + a_nb) - a_own_old2;  // j's f_{r-1}[j->i], bitwise
   return -f_rev;                                            // CA:99 flows[j] = -msg.flow
+}
+
+// Exact left-to-right chains S += xs[q], T += es[q] over q = 0 .. cn-1 (one wave, lane-
+// uniform). The LDS reads of the next 8 elements are issued before the 16 dependent adds of
+// the current 8, so the chain runs at the fp64 add latency instead of add + LDS latency.
+__device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
+  constexpr int B = 8;
+  int q = 0;
+  if (cn >= B) {
+    double a[B], b[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) { a[k] = xs[k]; b[k] = es[k]; }
+    for (q = B; q + B <= cn; q += B) {
+      double a2[B], b2[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) { a2[k] = xs[q + k]; b2[k] = es[q + k]; }
+#pragma unroll
+      for (int k = 0; k < B; ++k) { S = S + a[k]; T = T + b[k]; }
+#pragma unroll
+      for (int k = 0; k < B; ++k) { a[k] = a2[k]; b[k] = b2[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < B; ++k) { S = S + a[k]; T = T + b[k]; }
+  }
+  for (; q < cn; ++q) {
+    S = S + xs[q];
+    T = T + es[q];
+  }
 }
 
 template <typename T>
@@ -486,7 +572,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           const int e = s_rb[r] + c0 + k;
           const double er = ld_est(pp, code_prev, a_prev, col[e]);
           const int slot = (r << lgC) + (k ^ sw(r));
-          s_x[slot] = recon_fr(F[e], er, s_own2[r]);
+          s_x[slot] = recon_fr(ld_f(F, e), er, s_own2[r]);
           s_er[slot] = er;
         }
       }
@@ -505,7 +591,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (t < R) {
       const int node = s_node[t];
       a_mine = ((v[node] - S) + T) / (double)(my_deg + 1);
-      a_new[node] = a_mine;
+      st_wt(a_new + node, a_mine);
       if (pc.width) put_code(pc, code_new, node, a_mine);
       if (CHECK) eb = err_bits(a_mine, target[node]);
     }
@@ -517,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         const int r = q >> lgC, k = q & (C - 1);
         if (k < s_deg[r]) {
           const int slot = (r << lgC) + (k ^ sw(r));
-          F[s_rb[r] + k] = (s_x[slot] + s_a[r]) - s_er[slot];
+          st_f_full(F, s_rb[r] + k, (s_x[slot] + s_a[r]) - s_er[slot]);
         }
       }
     } else {  // long rows: re-read the flow, re-gather the estimate (L2-warm)
@@ -526,7 +612,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         const double own2 = a_prev2[s_node[r]], a = s_a[r];
         for (int k = t; k < d; k += kBlock) {
           const double er = ld_est(pp, code_prev, a_prev, col[rb + k]);
-          F[rb + k] = (recon_fr(F[rb + k], er, own2) + a) - er;
+          const double fo = ld_f(F, rb + k);
+          st_f(F, rb + k, (recon_fr(fo, er, own2) + a) - er, fo);
         }
       }
     }
@@ -537,30 +624,37 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 
   if (tl.y < 0) {
     // ---------------- heavy node ----------------
+    // chunks of CH = TE / 2 in the two halves of s_x / s_er: wave 0 runs the exact
+    // left-to-right chain of chunk c (lane-uniform) while waves 1-3 stage chunk c + 1
     const int i = tl.x;
     const int b = rowptr[i], e = rowptr[i + 1];
     const double own2 = a_prev2[i];
     double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += TE) {
-      const int cn = min(TE, e - c0);
-      for (int q = t; q < cn; q += kBlock) {
+    constexpr int CH = TE / 2;
+    const int nch = (e - b + CH - 1) / CH;
+    auto stage = [&](int c, int tid, int nthr) {
+      const int c0 = b + c * CH, cn = min(CH, e - c0);
+      double *xs = s_x + (c & 1) * CH, *es = s_er + (c & 1) * CH;
+      for (int q = tid; q < cn; q += nthr) {
         const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
-        s_x[q] = recon_fr(F[c0 + q], er, own2);
-        s_er[q] = er;
+        xs[q] = recon_fr(ld_f(F, c0 + q), er, own2);
+        es[q] = er;
       }
-      __syncthreads();
-      if (t < 64 && DIAG != 5) {
-        for (int q = 0; q < cn; ++q) {  // exact left-to-right chain, lane-uniform
-          S = S + s_x[q];
-          T = T + s_er[q];
-        }
+    };
+    if (nch > 0) stage(0, t, kBlock);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      if (t >= 64) {
+        if (c + 1 < nch) stage(c + 1, t - 64, kBlock - 64);
+      } else if (DIAG != 5) {
+        chain_sum(s_x + (c & 1) * CH, s_er + (c & 1) * CH, min(CH, e - (b + c * CH)), S, T);
       }
       __syncthreads();
     }
     if (t == 0) {
       const double a = ((v[i] - S) + T) / (double)(e - b + 1);
       s_a[0] = a;
-      a_new[i] = a;
+      st_wt(a_new + i, a);
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
@@ -568,7 +662,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const double a = s_a[0];
     for (int k = b + t; k < e; k += kBlock) {
       const double er = ld_est(pp, code_prev, a_prev, col[k]);
-      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+      const double fo = ld_f(F, k);
+      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -590,10 +685,10 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (q < ne) {
       if (NT) {
         c[k] = ld_stream(col + e0 + q);
-        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_stream(F + e0 + q);
+        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_f(F, e0 + q);
       } else {
         c[k] = col[e0 + q];
-        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : F[e0 + q];
+        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_f(F, e0 + q);
       }
     }
   }
@@ -646,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
-    a_new[nb + t] = a;
+    st_wt(a_new + nb + t, a);
     if (pc.width) put_code(pc, code_new, nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
@@ -658,11 +753,9 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (q < ne) {
       const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
       if (DIAG == 2 || DIAG == 12) {
-        if (fnew == 12345.678) F[e0 + q] = fnew;  // keep the value live, store ~never
-      } else if (NT) {
-        __builtin_nontemporal_store(fnew, F + e0 + q);
+        if (fnew == 12345.678) st_f_full(F, e0 + q, fnew);  // keep the value live, store ~never
       } else {
-        F[e0 + q] = fnew;
+        st_f(F, e0 + q, fnew, x[k]);
       }
     }
   }
@@ -726,7 +819,7 @@ __global__ __launch_bounds__(kBlock) void k_round_wave(
   for (int k = 0; k < kPer; ++k) {
     const int q = lane + k * 64;
     c[k] = q < ne ? col[e0 + q] : 0;
-    x[k] = q < ne ? F[e0 + q] : 0.0;
+    x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
   }
   const int rp = lane <= nn ? rowptr[nb + lane] : 0;
   const int rp_last = (TN == 64 && lane == 0 && nn == 64) ? rowptr[nb + 64] : 0;
@@ -780,7 +873,7 @@ __global__ __launch_bounds__(kBlock) void k_round_wave(
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[w][lane] = a;
-    a_new[nb + lane] = a;
+    st_wt(a_new + nb + lane, a);
     if (pc.width) put_code(pc, code_new, nb + lane, a);
     if (CHECK) eb = err_bits(a, target[nb + lane]);
   }
@@ -789,7 +882,7 @@ __global__ __launch_bounds__(kBlock) void k_round_wave(
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int q = lane + k * 64;
-    if (q < ne) F[e0 + q] = (s_x[w][q] + s_a[w][s_own[w][q]]) - g[k];
+    if (q < ne) st_f(F, e0 + q, (s_x[w][q] + s_a[w][s_own[w][q]]) - g[k], x[k]);
   }
   if (CHECK) wave_max_to(eb, err);
 }
@@ -815,111 +908,165 @@ constexpr int kStageThreads = 512;
 constexpr int kStageLds = 65536;  // bytes of table per slice
 constexpr int kStageTE = 512, kStageTN = 64;
 
-constexpr int kStageMaxItems = 513;  // per stage block: <= 512 group segments + sentinel
-constexpr int kStageU = 8;           // elements per thread per pass (all loads issued first)
-
-// LDS: the table slice is in s_tab (ds_read); else it is read from global memory (the
-// two are separate instantiations, so no load goes through the generic address space).
-template <typename T, bool LDS>
-__device__ inline void stage_pass(const int2 *s_item, int nit, int total, int j0,
-                                  const unsigned short *__restrict__ colS,
-                                  const unsigned char *s_tab, const T *__restrict__ gtab,
-                                  T *__restrict__ G) {
-  int kk[kStageU];
-  unsigned o[kStageU];
-#pragma unroll
-  for (int u = 0; u < kStageU; ++u) {  // flat index -> element: last item with pre <= j
-    const int j = j0 + u * kStageThreads;
-    int lo = 0, hi = nit - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (s_item[mid].y <= j) lo = mid; else hi = mid - 1;
-    }
-    kk[u] = j < total ? s_item[lo].x + (j - s_item[lo].y) : -1;
-  }
-#pragma unroll
-  for (int u = 0; u < kStageU; ++u) o[u] = kk[u] >= 0 ? colS[kk[u]] : 0u;
-  T val[kStageU];
-#pragma unroll
-  for (int u = 0; u < kStageU; ++u) {
-    if constexpr (LDS) val[u] = reinterpret_cast<const T *>(s_tab)[o[u]];
-    else val[u] = kk[u] >= 0 ? gtab[o[u]] : T(0);
-  }
-#pragma unroll
-  for (int u = 0; u < kStageU; ++u)
-    if (kk[u] >= 0) G[kk[u]] = val[u];
+// The slice layouts (element bytes 1, 2, 4, 8) passed by value to the stage and round
+// launches; the device picks the layout from the table's actual packing width, so the
+// choice never depends on the host having seen the (asynchronous) packing plan.
+struct StageArgs {
+  int P[4], Q[4];
+  const int *aoff[4];
+  const int2 *aitem[4];
+  const unsigned short *colS[4];
+  const unsigned *sidx[4];
+  int sel[4];  // layout used for tables of width 8, 16, 32, 0 (0..3)
+};
+__device__ __forceinline__ int width_index(int width) {
+  return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
 }
 
-template <int LB>  // bytes per element the layout was built for (1, 2, 4, 8)
-__global__ __launch_bounds__(kStageThreads) void k_stage(
-    int P, int n, const int *__restrict__ aoff, const int2 *__restrict__ aitem,
-    const unsigned short *__restrict__ colS, const double *__restrict__ a_prev,
-    const void *__restrict__ code_prev, const PackCtl *__restrict__ ctl, int rslot,
-    void *__restrict__ G) {
-  constexpr int SN = kStageLds / LB;
+constexpr int kStageItem = 1024;  // elements per stage item (one wave, 16 per lane)
+constexpr int kStageIU = kStageItem / 64;
+constexpr int kStageChunk = 256;  // item descriptors staged in LDS at a time
+
+// One stage item (<= 1024 consecutive elements of one segment, one wave): column-offset
+// loads (unconditional, clamped to the item) into o[].
+template <typename T>
+__device__ __forceinline__ void stage_item_load(unsigned (&o)[kStageIU], int2 itm, int lane,
+                                                const unsigned short *__restrict__ colS) {
+  const int last = itm.x + max(itm.y, 1) - 1;
+#pragma unroll
+  for (int u = 0; u < kStageIU; ++u) o[u] = colS[min(itm.x + lane + 64 * u, last)];
+}
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_item_store(const unsigned (&o)[kStageIU], int2 itm, int lane,
+                                                 const unsigned char *s_tab, const T *__restrict__ tab,
+                                                 int nb, T *__restrict__ G) {
+  T val[kStageIU];
+#pragma unroll
+  for (int u = 0; u < kStageIU; ++u) {
+    if constexpr (LDS) val[u] = reinterpret_cast<const T *>(s_tab)[o[u]];
+    else val[u] = tab[nb + (int)o[u]];
+  }
+#pragma unroll
+  for (int u = 0; u < kStageIU; ++u)
+    if (lane + 64 * u < itm.y) st_wt(G + itm.x + lane + 64 * u, val[u]);
+}
+
+// One stage block: slice s of the table (element type T) -> LDS (LDS = false: read from
+// global memory, the table being wider than the layout), then its items, wave w taking
+// items ib + w, ib + w + 8, ... Every load of an item is issued before any of its uses, and
+// the next item's loads are issued before the current item is looked up and stored
+// (two register sets, unrolled by two so no in-flight register is copied).
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_body(unsigned char *s_tab, int2 *s_items, int nb, int cnt,
+                                           const int2 *__restrict__ items, int ib, int ie,
+                                           const unsigned short *__restrict__ colS,
+                                           const T *__restrict__ tab, T *__restrict__ G) {
+  constexpr int kW = kStageLds / 16 / kStageThreads;
+  constexpr int NW = kStageThreads / 64;
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint4 buf[kW];
+  const int bytes = LDS ? cnt * (int)sizeof(T) : 0;
+  const int w16 = bytes >> 4;
+  const uint4 *s16 = reinterpret_cast<const uint4 *>(tab + nb);
+  if constexpr (LDS) {
+#pragma unroll
+    for (int u = 0; u < kW; ++u) {
+      const int k = t + u * kStageThreads;
+      buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  }
+  const int2 z = make_int2(0, 0);
+  bool filled = !LDS;
+  // the block's item descriptors go through LDS in chunks of kStageChunk (one chunk on
+  // ER-1M), so a wave never waits on a descriptor load behind its own column loads
+  for (int cb = ib; cb < ie || !filled; cb += kStageChunk) {
+    const int ce = min(ie, cb + kStageChunk);
+    if (cb > ib) __syncthreads();  // previous chunk consumed
+    for (int i = t; i < ce - cb; i += kStageThreads) s_items[i] = items[cb + i];
+    __syncthreads();
+    int it = w;
+    const int nit = ce - cb;
+    int2 i0 = it < nit ? s_items[it] : z;
+    unsigned o0[kStageIU], o1[kStageIU];
+    stage_item_load<T>(o0, i0, lane, colS);
+    if (!filled) {  // slice stores after the first item's loads are in flight
+#pragma unroll
+      for (int u = 0; u < kW; ++u) {
+        const int k = t + u * kStageThreads;
+        if (k < w16) reinterpret_cast<uint4 *>(s_tab)[k] = buf[u];
+      }
+      const int tb = w16 << 4;
+      if (t < bytes - tb) s_tab[tb + t] = reinterpret_cast<const unsigned char *>(tab + nb)[tb + t];
+      __syncthreads();
+      filled = true;
+    }
+    while (it < nit) {
+      const int2 i1 = it + NW < nit ? s_items[it + NW] : z;
+      stage_item_load<T>(o1, i1, lane, colS);
+      stage_item_store<T, LDS>(o0, i0, lane, s_tab, tab, nb, G);
+      it += NW;
+      if (it >= nit) break;
+      i0 = it + NW < nit ? s_items[it + NW] : z;
+      stage_item_load<T>(o0, i0, lane, colS);
+      stage_item_store<T, LDS>(o1, i1, lane, s_tab, tab, nb, G);
+      it += NW;
+    }
+  }
+}
+
+__global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
+                                                        const double *__restrict__ a_prev,
+                                                        const void *__restrict__ code_prev,
+                                                        const PackCtl *__restrict__ ctl, int rslot,
+                                                        void *__restrict__ G) {
   __shared__ __align__(16) unsigned char s_tab[kStageLds];
-  __shared__ int2 s_item[kStageMaxItems];
+  __shared__ int2 s_items[kStageChunk];
   const PackCtl pp = ctl[rslot ^ 1];
   const int wb = pp.width ? pp.width / 8 : 8;  // bytes per element of the table gathered
+  const int li = sa.sel[width_index(pp.width)];
+  const int P = sa.P[li];
+  if ((int)blockIdx.x >= P * sa.Q[li]) return;
+  const int LB = 1 << li;  // bytes per element the layout was built for
+  const int SN = kStageLds >> li;
   const int s = blockIdx.x % P;
   const int nb = s * SN;
   const int cnt = min(SN, n - nb);
-  const unsigned char *src = pp.width ? reinterpret_cast<const unsigned char *>(code_prev)
-                                      : reinterpret_cast<const unsigned char *>(a_prev);
-  const bool lds = wb <= LB;
-  // this block's segments: {first element, flat prefix}, then a sentinel {-, total}
-  const int ib = aoff[blockIdx.x], nit = aoff[blockIdx.x + 1] - ib;
-  for (int i = threadIdx.x; i < nit; i += kStageThreads) s_item[i] = aitem[ib + i];
-  if (lds) {  // slice -> LDS: every 16-byte load issued before the stores, byte tail
-    const int bytes = cnt * wb;
-    const uint4 *s16 = reinterpret_cast<const uint4 *>(src + (size_t)nb * wb);
-    uint4 *d16 = reinterpret_cast<uint4 *>(s_tab);
-    constexpr int kW = kStageLds / 16 / kStageThreads;
-    const int w16 = bytes >> 4;
-    uint4 buf[kW];
-#pragma unroll
-    for (int u = 0; u < kW; ++u) {
-      const int k = threadIdx.x + u * kStageThreads;
-      buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
-    }
-#pragma unroll
-    for (int u = 0; u < kW; ++u) {
-      const int k = threadIdx.x + u * kStageThreads;
-      if (k < w16) d16[k] = buf[u];
-    }
-    const int tb = w16 << 4;
-    if ((int)threadIdx.x < bytes - tb) s_tab[tb + threadIdx.x] = src[(size_t)nb * wb + tb + threadIdx.x];
-  }
-  __syncthreads();
-  const int items = nit - 1, total = s_item[nit - 1].y;
-  for (int j0 = threadIdx.x; j0 < total; j0 += kStageU * kStageThreads) {
-#define FU_PASS(T)                                                                                   \
-  do {                                                                                               \
-    if (lds) stage_pass<T, true>(s_item, items, total, j0, colS, s_tab, nullptr, reinterpret_cast<T *>(G)); \
-    else stage_pass<T, false>(s_item, items, total, j0, colS, s_tab,                                \
-                              reinterpret_cast<const T *>(src) + nb, reinterpret_cast<T *>(G));      \
+  const void *src = pp.width ? code_prev : static_cast<const void *>(a_prev);
+  const unsigned short *colS = sa.colS[li];
+  const int2 *aitem = sa.aitem[li];
+  // this block's items {first element, count <= kStageItem}
+  const int ib = sa.aoff[li][blockIdx.x], ie = sa.aoff[li][blockIdx.x + 1];
+#define FU_BODY(T)                                                                                  \
+  do {                                                                                              \
+    if ((int)sizeof(T) <= LB)                                                                       \
+      stage_body<T, true>(s_tab, s_items, nb, cnt, aitem, ib, ie, colS, reinterpret_cast<const T *>(src), \
+                          reinterpret_cast<T *>(G));                                                \
+    else                                                                                            \
+      stage_body<T, false>(s_tab, s_items, nb, cnt, aitem, ib, ie, colS, reinterpret_cast<const T *>(src), \
+                           reinterpret_cast<T *>(G));                                               \
   } while (0)
-    if (wb == 1) FU_PASS(unsigned char);
-    else if (wb == 2) FU_PASS(unsigned short);
-    else if (wb == 4) FU_PASS(unsigned);
-    else FU_PASS(unsigned long long);
-#undef FU_PASS
-  }
+  if (wb == 1) FU_BODY(unsigned char);
+  else if (wb == 2) FU_BODY(unsigned short);
+  else if (wb == 4) FU_BODY(unsigned);
+  else FU_BODY(unsigned long long);
+#undef FU_BODY
 }
 
 // DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
-// 2 = no stage launch and G read as in 1 (prices the round without staging).
+// 2 = no stage launch and G read as in 1 (prices the round without staging), 3 = 2 without
+// the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
 template <bool CHECK, int TE, int TN, int DIAG = 0>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
     const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
     const int *__restrict__ rowptr, const int *__restrict__ col,
-    const unsigned *__restrict__ sidx, const void *__restrict__ G, const double *__restrict__ v,
+    const StageArgs sa, const void *__restrict__ G, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
     unsigned long long *__restrict__ err, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot) {
   static_assert(TE % kBlock == 0 && TN <= kBlock, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];
+  const unsigned *__restrict__ sidx = sa.sidx[sa.sel[width_index(pp.width)]];
   const PackCtl pc = ctl[2];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
   __shared__ double s_x[TE];
@@ -944,14 +1091,15 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   for (int k = 0; k < kPer; ++k) {
     const int q = t + k * kBlock;
     si[k] = q < ne ? sidx[e0 + q] : 0u;
-    x[k] = q < ne ? F[e0 + q] : 0.0;
+    x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
   }
   const int rp = t <= nn ? rowptr[nb + t] : 0;
   const double vv = t < nn ? v[nb + t] : 0.0;
   const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
   int gi[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) gi[k] = t + k * kBlock < ne ? (DIAG ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
+  for (int k = 0; k < kPer; ++k)
+    gi[k] = t + k * kBlock < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
   // every G load of the tile first, then decode (escapes gather the double via col)
   if (pp.width == 0) {
 #pragma unroll
@@ -999,7 +1147,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
-    a_new[nb + t] = a;
+    st_wt(a_new + nb + t, a);
     if (pc.width) put_code(pc, code_new, nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
@@ -1008,7 +1156,9 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const int q = t + k * kBlock;
-    if (q < ne) F[e0 + q] = (s_x[q] + s_a[s_own[q]]) - s_er[q];
+    if (q < ne) {
+      st_f(F, e0 + q, (s_x[q] + s_a[s_own[q]]) - s_er[q], x[k]);
+    }
   }
   if (CHECK) block_max_to(eb, err);
 }
@@ -1059,7 +1209,7 @@ __device__ inline void pipe_load(PipeStream &s, int it, int m, const int4 *s_tl,
   for (int k = 0; k < kPipeKP; ++k) {
     const int e = min(s.e0 + t + k * kBlock, elast);
     s.c[k] = cidx[e];
-    s.x[k] = F[e];
+    s.x[k] = ld_f(F, e);
   }
   const int nn = tl.y - tl.x;
   s.rp = rowptr[s.nb + min(t, nn)];
@@ -1159,7 +1309,7 @@ __device__ inline void pipe_step(
     }
     const double a = ((sa.vv - S) + T) / (double)(qe - qb + 1);
     L.a[bf][t] = a;
-    a_new[sa.nb + t] = a;
+    st_wt(a_new + sa.nb + t, a);
     if (pc.width) put_code(pc, code_new, sa.nb + t, a);
     if (CHECK) {
       const unsigned long long b2 = err_bits(a, target[sa.nb + t]);
@@ -1171,7 +1321,7 @@ __device__ inline void pipe_step(
   for (int k = 0; k < KP; ++k) {  // phase C (CA:117-118)
     const int q = t + k * kBlock;
     if (q < sa.ne) {
-      F[sa.e0 + q] = (L.x[bf][q] + L.a[bf][L.own[bf][q]]) - L.er[bf][q];
+      st_f(F, sa.e0 + q, (L.x[bf][q] + L.a[bf][L.own[bf][q]]) - L.er[bf][q], sa.x[k]);
     }
   }
 }
@@ -1209,7 +1359,7 @@ template <bool CHECK, int MODE>
 __global__ __launch_bounds__(kBlock) void k_round_pipe(
     const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
     const int4 *__restrict__ heavy, int nheavy, const int *__restrict__ rowptr,
-    const int *__restrict__ col, const unsigned *__restrict__ sidx, const void *__restrict__ G,
+    const int *__restrict__ col, const StageArgs sa, const void *__restrict__ G,
     const double *__restrict__ v, double *__restrict__ F, const double *__restrict__ a_prev,
     const double *__restrict__ a_prev2, double *__restrict__ a_new,
     const double *__restrict__ target, unsigned long long *__restrict__ err,
@@ -1225,30 +1375,34 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
 
   if ((int)blockIdx.x < nheavy) {
     // ---------------- heavy row: kernel 4's exact chunked chain ----------------
+    // chunks of TE in the two LDS buffers: wave 0 chains chunk c while waves 1-3 stage c + 1
     const int4 tl = heavy[blockIdx.x];
     const int i = tl.x, b = tl.z, e = tl.w;
     const double own2 = a_prev2[i];
     double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += TE) {
-      const int cn = min(TE, e - c0);
-      for (int q = t; q < cn; q += kBlock) {
+    const int nch = (e - b + TE - 1) / TE;
+    auto stage = [&](int c, int tid, int nthr) {
+      const int c0 = b + c * TE, cn = min(TE, e - c0);
+      for (int q = tid; q < cn; q += nthr) {
         const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
-        L.x[0][q] = recon_fr(F[c0 + q], er, own2);
-        L.er[0][q] = er;
+        L.x[c & 1][q] = recon_fr(ld_f(F, c0 + q), er, own2);
+        L.er[c & 1][q] = er;
       }
-      __syncthreads();
-      if (t < 64) {
-        for (int q = 0; q < cn; ++q) {
-          S = S + L.x[0][q];
-          T = T + L.er[0][q];
-        }
+    };
+    if (nch > 0) stage(0, t, kBlock);
+    __syncthreads();
+    for (int c = 0; c < nch; ++c) {
+      if (t >= 64) {
+        if (c + 1 < nch) stage(c + 1, t - 64, kBlock - 64);
+      } else {
+        chain_sum(L.x[c & 1], L.er[c & 1], min(TE, e - (b + c * TE)), S, T);
       }
       __syncthreads();
     }
     if (t == 0) {
       const double a = ((v[i] - S) + T) / (double)(e - b + 1);
       L.a[0][0] = a;
-      a_new[i] = a;
+      st_wt(a_new + i, a);
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
@@ -1256,7 +1410,8 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
     const double a = L.a[0][0];
     for (int k = b + t; k < e; k += kBlock) {
       const double er = ld_est(pp, code_prev, a_prev, col[k]);
-      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+      const double fo = ld_f(F, k);
+      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -1277,7 +1432,7 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
     L.gb[0] = 0;
   }
   __syncthreads();
-  const unsigned *cidx = MODE ? sidx : reinterpret_cast<const unsigned *>(col);
+  const unsigned *cidx = MODE ? sa.sidx[sa.sel[width_index(pp.width)]] : reinterpret_cast<const unsigned *>(col);
   const void *tab = MODE ? G : code_prev;
 #define FU_TILES(W_)                                                                                  \
   pipe_tiles<CHECK, MODE, W_>(L, m, rowptr, col, cidx, tab, v, F, a_prev, a_prev2, a_new, target,     \
@@ -1290,6 +1445,15 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
   if (CHECK) block_max_to(eb, err);
 }
 
+__global__ void k_fill_split(long long cnt, double val, double *__restrict__ p) {
+  long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (q < cnt) st_f_full(p, (int)q, val);
+}
+// split-word flows -> doubles (fu_get_flows of kernels >= 4)
+__global__ void k_unsplit(long long cnt, const double *__restrict__ src, double *__restrict__ dst) {
+  long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (q < cnt) dst[q] = ld_f(src, (int)q);
+}
 __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) p[q] = val;
@@ -1392,22 +1556,17 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
       for (int q = t; q < cn; q += kBlock) {
         const int gi = split_index(c0 - b + q, split_i, p0, p1);
         const double er = (GATHER1 && c0 - b + q >= split_i) ? a_prev[col_pm[gi]] : G[gi];
-        s_x[q] = recon_fr(F[c0 + q], er, own2);
+        s_x[q] = recon_fr(ld_f(F, c0 + q), er, own2);
         s_g[q] = er;
       }
       __syncthreads();
-      if (t < 64) {
-        for (int q = 0; q < cn; ++q) {
-          S = S + s_x[q];
-          T = T + s_g[q];
-        }
-      }
+      if (t < 64) chain_sum(s_x, s_g, cn, S, T);
       __syncthreads();
     }
     if (t == 0) {
       const double a = ((v[i] - S) + T) / (double)(e - b + 1);
       s_a[0] = a;
-      a_new[i] = a;
+      st_wt(a_new + i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
     __syncthreads();
@@ -1415,7 +1574,8 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     for (int k = b + t; k < e; k += kBlock) {
       const int gi = split_index(k - b, split_i, p0, p1);
       const double er = (GATHER1 && k - b >= split_i) ? a_prev[col_pm[gi]] : G[gi];
-      F[k] = (recon_fr(F[k], er, own2) + a) - er;
+      const double fo = ld_f(F, k);
+      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -1434,7 +1594,7 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     x[k] = 0.0;
     g[k] = 0.0;
     if (q < ne) {
-      x[k] = F[e0 + q];
+      x[k] = ld_f(F, e0 + q);
       if (GATHER1) g[k] = q < n0 ? G[g0b + q] : a_prev[col_pm[g1b + (q - n0)]];
       else g[k] = q < n0 ? G[g0b + q] : G[g1b + (q - n0)];
     }
@@ -1478,7 +1638,7 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
-    a_new[nb + t] = a;
+    st_wt(a_new + nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
   __syncthreads();
@@ -1492,7 +1652,7 @@ __global__ __launch_bounds__(kBlock) void k_round_split(
       const int p0 = s_rp0[o] - g0b;
       const int p1 = n0 + ((s_rp[o] - s_rp0[o]) - (e0 - g0b));
       const double er = s_g[split_index(q - qb, split_t, p0, p1)];
-      F[e0 + q] = (s_x[q] + s_a[o]) - er;
+      st_f(F, e0 + q, (s_x[q] + s_a[o]) - er, x[k]);
     }
   }
   if (CHECK) block_max_to(eb, err);
@@ -1773,7 +1933,7 @@ struct fu_handle {
   struct StageLayout {
     int P = 0, Q = 0;              // slices, blocks per slice
     int *aoff = nullptr;           // per stage block: first entry in aitem
-    int2 *aitem = nullptr;         // per stage block: {segment start, flat prefix}..., {0, total}
+    int2 *aitem = nullptr;         // stage items {first element, count}, grouped by block
     unsigned short *colS = nullptr;  // per staged element: column offset within its slice
     unsigned *sidx = nullptr;      // per tile edge (slice order): G index in group << 16 | position
   };
@@ -2097,26 +2257,25 @@ int ensure_stage(fu_handle *h) {
           sidx[e0 + m] = ((uint32_t)kpos[e0 + ord[m] - ge0] << 16) | (uint32_t)ord[m];
       }
     }
-    // stage blocks (s, q), blockIdx = s + P * q (slice s on XCD s % 8 when 8 | P): q takes
-    // groups [ng q / Q, ng (q+1) / Q), at most kStageMaxItems - 1 of them
-    int64_t Q = std::max<int64_t>(1, std::min<int64_t>(ng, 512 / P));
-    Q = std::max<int64_t>(Q, (ng + kStageMaxItems - 2) / (kStageMaxItems - 1));
+    // stage blocks (s, q), blockIdx = s + P * q (slice s on XCD s % 8 when 8 | P); slice
+    // s's segments are cut into items of <= kStageItem elements (one wave each), and its Q
+    // blocks take equal shares of the item list
+    const int64_t Q = std::max<int64_t>(1, 512 / P);
     std::vector<int32_t> aoff(P * Q + 1, 0);
     std::vector<int2> aitem;
-    for (int64_t q = 0; q < Q; ++q)
-      for (int64_t s = 0; s < P; ++s) {
-        const int64_t b = s + P * q;
-        const int64_t g0 = ng * q / Q, g1 = ng * (q + 1) / Q;
-        aoff[b] = (int32_t)aitem.size();
-        int32_t pre = 0;
-        for (int64_t g = g0; g < g1; ++g) {
-          const int32_t kb = segs[g * (P + 1) + s], ke = segs[g * (P + 1) + s + 1];
-          if (ke > kb) aitem.push_back(make_int2(kb, pre));
-          pre += ke - kb;
-        }
-        aitem.push_back(make_int2(0, pre));
+    std::vector<std::vector<int2>> per_s(P);
+    for (int64_t s = 0; s < P; ++s)
+      for (int g = 0; g < ng; ++g) {
+        const int32_t kb = segs[(size_t)g * (P + 1) + s], ke = segs[(size_t)g * (P + 1) + s + 1];
+        for (int32_t k = kb; k < ke; k += kStageItem) per_s[s].push_back(make_int2(k, std::min(kStageItem, ke - k)));
       }
-    aoff[P * Q] = (int32_t)aitem.size();  // q outer, s inner: b = s + P q in order
+    for (int64_t q = 0; q < Q; ++q)
+      for (int64_t s = 0; s < P; ++s) {  // q outer, s inner: b = s + P q in order
+        const int64_t b = s + P * q, ni = (int64_t)per_s[s].size();
+        aoff[b] = (int32_t)aitem.size();
+        for (int64_t i = ni * q / Q; i < ni * (q + 1) / Q; ++i) aitem.push_back(per_s[s][i]);
+      }
+    aoff[P * Q] = (int32_t)aitem.size();
     L.P = (int)P;
     L.Q = (int)Q;
     if (int rc = up(&L.aoff, aoff.data(), aoff.size())) return rc;
@@ -2132,16 +2291,33 @@ int ensure_stage(fu_handle *h) {
   return FU_OK;
 }
 
-// Layout for the packing width the host last saw: the narrowest built layout that holds
-// the table's elements in LDS, else the widest built one (the stage launch then gathers).
-inline int stage_layout(fu_handle *h) {
-  if (h->st_force >= 0 && h->st[h->st_force].P) return h->st_force;
-  const int want = h->seen_width == 8 ? 0 : h->seen_width == 16 ? 1 : h->seen_width == 32 ? 2 : 3;
-  for (int li = want; li < 4; ++li)
-    if (h->st[li].P) return li;
-  for (int li = want; li >= 0; --li)
-    if (h->st[li].P) return li;
-  return -1;
+// Layout per table width (device-side choice): the narrowest built layout whose elements
+// hold the width's (the table sits in LDS), else the widest built one (the stage launch
+// then reads the table from global memory); a forced layout (tests) for every width.
+StageArgs stage_args(fu_handle *h, unsigned *grid) {
+  StageArgs sa{};
+  unsigned g = 1;
+  for (int li = 0; li < 4; ++li) {
+    const auto &L = h->st[li];
+    sa.P[li] = L.P ? L.P : 1;
+    sa.Q[li] = L.P ? L.Q : 0;
+    sa.aoff[li] = L.aoff;
+    sa.aitem[li] = L.aitem;
+    sa.colS[li] = L.colS;
+    sa.sidx[li] = L.sidx;
+    if (L.P) g = std::max<unsigned>(g, (unsigned)(L.P * L.Q));
+  }
+  for (int want = 0; want < 4; ++want) {
+    int pick = -1;
+    if (h->st_force >= 0 && h->st[h->st_force].P) pick = h->st_force;
+    for (int li = want; li < 4 && pick < 0; ++li)
+      if (h->st[li].P) pick = li;
+    for (int li = want; li >= 0 && pick < 0; --li)
+      if (h->st[li].P) pick = li;
+    sa.sel[want] = pick < 0 ? 0 : pick;
+  }
+  if (grid) *grid = g;
+  return sa;
 }
 
 int ensure_a2(fu_handle *h) {
@@ -2170,10 +2346,10 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   if (h->kernel >= 4) {
     const int64_t r = h->rounds;
     if (r == 0) {
-      hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
+      hipLaunchKernelGGL(k_round0<true>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
                          h->rowptr, h->v, h->f[0], h->a[0]);
-      if (h->E)  // f_{-1} = -0.0 so that round 1 reproduces (0.0 + a) - 0.0
-        hipLaunchKernelGGL(k_fill, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
+      if (h->E)  // f_{-1} = -0.0 (split words) so that round 1 reproduces (0.0 + a) - 0.0
+        hipLaunchKernelGGL(k_fill_split, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
                            -0.0, h->f[1]);
       HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
       HIP_TRY(hipMemsetAsync(h->pctl, 0, sizeof(PackCtl) * 3, h->stream));      // no codes yet
@@ -2220,23 +2396,18 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *an = h->a[r % 3];
       const void *cp = h->code[(r - 1) & 1];
       const bool staged = h->kernel == 10;
-      const int li = staged ? stage_layout(h) : 0;
-      const fu_handle::StageLayout &L = h->st[li < 0 ? 0 : li];
-      if (staged && h->st_ngroups) {
-        const dim3 grid((unsigned)(L.P * L.Q));
-#define FU_STAGE(LB)                                                                              \
-  hipLaunchKernelGGL(k_stage<LB>, grid, dim3(kStageThreads), 0, h->stream, L.P, h->n, L.aoff, L.aitem, \
-                     L.colS, ap, cp, h->pctl, (int)(r & 1), h->stG)
-        if (li == 0) FU_STAGE(1); else if (li == 1) FU_STAGE(2); else if (li == 2) FU_STAGE(4); else FU_STAGE(8);
-#undef FU_STAGE
-      }
+      unsigned sgrid = 1;
+      const StageArgs sa = staged ? stage_args(h, &sgrid) : StageArgs{};
+      if (staged && h->st_ngroups)
+        hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
+                           (int)(r & 1), h->stG);
       long long nbl = std::max<long long>((h->st_ntiles + kPipeChunk - 1) / kPipeChunk, (long long)h->pipe_bpc * h->n_cu);
       nbl = std::min<long long>(nbl, ((long long)h->st_ntiles + 7) / 8 * 8);
       nbl = std::max<long long>(8, (nbl + 7) / 8 * 8);
       const dim3 grid((unsigned)(nbl + h->st_nheavy));
 #define FU_PIPE(C, M)                                                                                  \
   hipLaunchKernelGGL((k_round_pipe<C, M>), grid, dim3(kBlock), 0, h->stream, h->st_tiles, h->st_gbase,       \
-                     h->st_ntiles, h->st_heavy, h->st_nheavy, h->rowptr, h->col, L.sidx, h->stG, h->v, F, ap, \
+                     h->st_ntiles, h->st_heavy, h->st_nheavy, h->rowptr, h->col, sa, h->stG, h->v, F, ap,     \
                      ap2, an, h->target, err_slot, cp, h->code[r & 1], h->pctl, (int)(r & 1),           \
                      (int)std::max<int64_t>(0, h->E - 1))
       if (check) {
@@ -2249,17 +2420,12 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
-      const int li = stage_layout(h);
-      const fu_handle::StageLayout &L = h->st[li];
+      unsigned sgrid = 1;
+      const StageArgs sa = stage_args(h, &sgrid);
       const void *cp = h->code[(r - 1) & 1];
-      if (h->st_ngroups && h->diag < 2) {
-        const dim3 grid((unsigned)(L.P * L.Q));
-#define FU_STAGE(LB)                                                                              \
-  hipLaunchKernelGGL(k_stage<LB>, grid, dim3(kStageThreads), 0, h->stream, L.P, h->n, L.aoff, L.aitem, \
-                     L.colS, ap, cp, h->pctl, (int)(r & 1), h->stG)
-        if (li == 0) FU_STAGE(1); else if (li == 1) FU_STAGE(2); else if (li == 2) FU_STAGE(4); else FU_STAGE(8);
-#undef FU_STAGE
-      }
+      if (h->st_ngroups && h->diag < 2)
+        hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
+                           (int)(r & 1), h->stG);
       if (h->st_nheavy) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
@@ -2270,23 +2436,27 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
                              h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1));
       }
-      if (h->st_ntiles && h->diag) {
+      if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
+        hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
+                           h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
+                           h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
+      } else if (h->st_ntiles && h->diag) {
         if (h->diag == 3)
           hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 3>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
                              h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
         else
           hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 1>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
                              h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
       } else if (h->st_ntiles) {
         if (check)
           hipLaunchKernelGGL((k_round_staged<true, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
                              h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
         else
           hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, L.sidx, h->stG,
+                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
                              h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
       }
     } else if (h->kernel == 7) {
@@ -2351,7 +2521,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       hipLaunchKernelGGL(k_round0_push, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
                          h->rowptr, h->rev, h->v, h->inbox[dst], h->a[dst]);
     } else {
-      hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
+      hipLaunchKernelGGL(k_round0<false>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
                          h->rowptr, h->v, h->f[dst], h->a[dst]);
     }
     if (check) {
@@ -2389,8 +2559,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   HIP_TRY(hipGetLastError());
   h->cur = dst;
   h->rounds++;
-  // refresh the packing plan from a_r (kernel 4 encodes with it from the next round on)
-  if (h->kernel >= 4 && h->pack && !h->dist && h->n_psample > 0 && h->rounds % h->pack_every == 0) {
+  // refresh the packing plan from a_r (kernel 4 encodes with it from the next round on);
+  // once the host has seen the narrowest width (8), every 8th time only: the plan and its
+  // width copy stall the stream for ~20 us
+  const int every = h->seen_width == 8 ? 8 * h->pack_every : h->pack_every;
+  if (h->kernel >= 4 && h->pack && !h->dist && h->n_psample > 0 && h->rounds % every == 0) {
     hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample, h->pctl);
     HIP_TRY(hipGetLastError());
     if (!h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
@@ -2478,7 +2651,8 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
   *h->h_pw = 0;
   if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (!no_rev && (rc = dmalloc(&h->rev, e))) ||
-      (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) ||
+      (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], (fe + 31) / 32 * 32)) ||
+      (rc = dmalloc(&h->f[1], (fe + 31) / 32 * 32)) ||
       (rc = dmalloc(&h->a[0], na)) || (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->target, n)) ||
       (rc = dmalloc(&h->err, 1)))
     return cleanup(rc);
@@ -2689,7 +2863,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
     cands.push_back({8, 0, 0});
     cands.push_back({10, 0, 0});
   }
-  constexpr int kTimed = 4;
+  constexpr int kTimed = 8;
   const int32_t need = (1 + kTimed) * (int32_t)cands.size();
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
@@ -2843,6 +3017,13 @@ int fu_get_flows(fu_handle *h, double *f_out) {
     }
     hipLaunchKernelGGL(k_push_flows, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
                        h->rev, h->inbox[h->cur], h->ftmp);
+    HIP_TRY(hipGetLastError());
+    src = h->ftmp;
+  } else if (h->kernel >= 4) {  // split words (st_f) -> doubles
+    if (!h->ftmp) {
+      if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
+    }
+    hipLaunchKernelGGL(k_unsplit, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E, src, h->ftmp);
     HIP_TRY(hipGetLastError());
     src = h->ftmp;
   }

@@ -49,6 +49,8 @@ VARIANTS = {
     "diag2_stage_nopack": ("stage", {"pack": 0, "diag": 2}),
     "diag3_stage": ("stage", {"diag": 3}),
     "pipe": ("pipe", {}),
+    "diag4_stage": ("stage", {"diag": 4}),
+    "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
     "pipe_nopack": ("pipe", {"pack": 0}),
     "pipe_stage": ("pipe_stage", {}),
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
