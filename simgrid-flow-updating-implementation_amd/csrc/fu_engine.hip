@@ -917,38 +917,67 @@ struct StageArgs {
   const int2 *aitem[4];
   const unsigned short *colS[4];
   const unsigned *sidx[4];
+  const int *gbase[4];
   int sel[4];  // layout used for tables of width 8, 16, 32, 0 (0..3)
 };
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
 }
 
-constexpr int kStageItem = 1024;  // elements per stage item (one wave, 16 per lane)
-constexpr int kStageIU = kStageItem / 64;
+constexpr int kStagePad = 8;      // segment padding: 8 consecutive elements per lane access
+constexpr int kStageItem = 1024;  // elements per stage item (one wave: 2 x 8 per lane)
+constexpr int kStageIU = kStageItem / (64 * kStagePad);
 constexpr int kStageChunk = 256;  // item descriptors staged in LDS at a time
 
-// One stage item (<= 1024 consecutive elements of one segment, one wave): column-offset
-// loads (unconditional, clamped to the item) into o[].
+// One stage item (<= 1024 consecutive elements of one padded segment, one wave): lane l
+// loads the column offsets of elements x + 8 (l + 64 u) .. + 7 with one 16-byte load each.
 template <typename T>
-__device__ __forceinline__ void stage_item_load(unsigned (&o)[kStageIU], int2 itm, int lane,
+__device__ __forceinline__ void stage_item_load(uint4 (&o)[kStageIU], int2 itm, int lane,
                                                 const unsigned short *__restrict__ colS) {
-  const int last = itm.x + max(itm.y, 1) - 1;
-#pragma unroll
-  for (int u = 0; u < kStageIU; ++u) o[u] = colS[min(itm.x + lane + 64 * u, last)];
-}
-template <typename T, bool LDS>
-__device__ __forceinline__ void stage_item_store(const unsigned (&o)[kStageIU], int2 itm, int lane,
-                                                 const unsigned char *s_tab, const T *__restrict__ tab,
-                                                 int nb, T *__restrict__ G) {
-  T val[kStageIU];
 #pragma unroll
   for (int u = 0; u < kStageIU; ++u) {
-    if constexpr (LDS) val[u] = reinterpret_cast<const T *>(s_tab)[o[u]];
-    else val[u] = tab[nb + (int)o[u]];
+    const int k = itm.x + kStagePad * (lane + 64 * u);
+    o[u] = *reinterpret_cast<const uint4 *>(colS + (k < itm.x + itm.y ? k : itm.x));
   }
+}
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_item_store(const uint4 (&o)[kStageIU], int2 itm, int lane,
+                                                 const unsigned char *s_tab, const T *__restrict__ tab,
+                                                 int nb, T *__restrict__ G) {
 #pragma unroll
-  for (int u = 0; u < kStageIU; ++u)
-    if (lane + 64 * u < itm.y) st_wt(G + itm.x + lane + 64 * u, val[u]);
+  for (int u = 0; u < kStageIU; ++u) {
+    const int k = itm.x + kStagePad * (lane + 64 * u);
+    const unsigned w4[4] = {o[u].x, o[u].y, o[u].z, o[u].w};
+    T val[kStagePad];
+#pragma unroll
+    for (int j = 0; j < kStagePad; ++j) {
+      const unsigned off = (w4[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
+      if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
+      else val[j] = tab[nb + (int)off];
+    }
+    if (k < itm.x + itm.y) {  // 8 consecutive elements, 16-byte aligned stores
+      if constexpr (sizeof(T) == 1) {
+        uint2 v;
+        v.x = val[0] | (val[1] << 8) | (val[2] << 16) | ((unsigned)val[3] << 24);
+        v.y = val[4] | (val[5] << 8) | (val[6] << 16) | ((unsigned)val[7] << 24);
+        *reinterpret_cast<uint2 *>(G + k) = v;
+      } else if constexpr (sizeof(T) == 2) {
+        uint4 v;
+        v.x = val[0] | ((unsigned)val[1] << 16);
+        v.y = val[2] | ((unsigned)val[3] << 16);
+        v.z = val[4] | ((unsigned)val[5] << 16);
+        v.w = val[6] | ((unsigned)val[7] << 16);
+        *reinterpret_cast<uint4 *>(G + k) = v;
+      } else {
+#pragma unroll
+        for (int j = 0; j < kStagePad; j += 16 / (int)sizeof(T)) {
+          uint4 v;
+          __builtin_memcpy(&v, &val[j], 16);
+          *reinterpret_cast<uint4 *>(G + k + j) = v;
+        }
+      }
+    }
+  }
 }
 
 // One stage block: slice s of the table (element type T) -> LDS (LDS = false: read from
@@ -987,7 +1016,7 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int2 *s_items, 
     int it = w;
     const int nit = ce - cb;
     int2 i0 = it < nit ? s_items[it] : z;
-    unsigned o0[kStageIU], o1[kStageIU];
+    uint4 o0[kStageIU], o1[kStageIU];
     stage_item_load<T>(o0, i0, lane, colS);
     if (!filled) {  // slice stores after the first item's loads are in flight
 #pragma unroll
@@ -1066,7 +1095,8 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     int rslot) {
   static_assert(TE % kBlock == 0 && TN <= kBlock, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];
-  const unsigned *__restrict__ sidx = sa.sidx[sa.sel[width_index(pp.width)]];
+  const int lsel = sa.sel[width_index(pp.width)];
+  const unsigned *__restrict__ sidx = sa.sidx[lsel];
   const PackCtl pc = ctl[2];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
   __shared__ double s_x[TE];
@@ -1081,7 +1111,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   const int xcd = blockIdx.x & 7, per = ntl >> 3, rem = ntl & 7;
   const int tile = DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3);
   const int4 tl = tiles[tile];
-  const int gb = tgbase[tile];
+  const int gb = sa.gbase[lsel][tile];
   const int nb = tl.x, nn = tl.y - tl.x;
   const int e0 = tl.z, ne = tl.w - tl.z;
   constexpr int kPer = TE / kBlock;
@@ -1425,7 +1455,7 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
   const int m = j < hi - lo ? (hi - lo - j + nbx - 1) / nbx : 0;
   if (t < m) {
     L.tl[t] = tiles[lo + j + t * nbx];
-    if (MODE) L.gb[t] = tgbase[lo + j + t * nbx];
+    if (MODE) L.gb[t] = sa.gbase[sa.sel[width_index(pp.width)]][lo + j + t * nbx];
   }
   if (t == 0 && m == 0) {  // keep the clamped prefetch of an empty list in bounds
     L.tl[0] = make_int4(0, 0, 0, 0);
@@ -1887,6 +1917,7 @@ struct fu_handle {
   bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
   bool tuned = false;
   float tune_ms[12] = {};  // per candidate (autotune_kernel order)
+  int tune_out[12] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
   int tuned_width = 0;    // packing width the last pass ran under
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
@@ -1936,6 +1967,7 @@ struct fu_handle {
     int2 *aitem = nullptr;         // stage items {first element, count}, grouped by block
     unsigned short *colS = nullptr;  // per staged element: column offset within its slice
     unsigned *sidx = nullptr;      // per tile edge (slice order): G index in group << 16 | position
+    int *gbase = nullptr;          // per light tile: its group's first staged element
   };
   StageLayout st[4];            // element bytes 1, 2, 4, 8
   bool st_ready = false;
@@ -2151,7 +2183,7 @@ int ensure_split(fu_handle *h) {
 
 // Kernel 8 preparation: light tiles, edge groups and the four slice layouts.
 constexpr int kStageMaxP = 512;      // slices per layout (more: layout not built)
-constexpr int kStageGroupEdges = 65536;  // G index within a group is u16
+constexpr int kStageGroupEdges = 60000;  // G index within a group is u16 (room for padding)
 
 // Light tiles (kStageTE x kStageTN), their edge groups and the heavy rows (kernels 8-10).
 int ensure_light(fu_handle *h) {
@@ -2220,33 +2252,51 @@ int ensure_stage(fu_handle *h) {
     if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
     return FU_OK;
   };
-  if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)h->E)) return rc;
-  HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long)));
+  // Staged index space per layout: group g's region holds its (slice, tile, position)
+  // ordered elements, each (group, slice) segment padded to a multiple of kStagePad so the
+  // stage launch moves 8 consecutive elements per lane with 16-byte column loads; a pad
+  // element's column offset is 0 and its staged word is never read.
+  int64_t gmax = 1;
   for (int li = 0; li < 4; ++li) {
     const int64_t SN = kStageLds >> li;
     const int64_t P = (n + SN - 1) / SN;
     auto &L = h->st[li];
     if (P > kStageMaxP) continue;
     std::vector<int32_t> segs((size_t)ng * (P + 1));
-    std::vector<uint16_t> colS(h->E > 0 ? h->E : 1);
-    std::vector<uint32_t> sidx(h->E > 0 ? h->E : 1);
+    std::vector<int32_t> gpos(ng + 1, 0);
     std::vector<int32_t> cur(P + 1);
+    for (int g = 0; g < ng; ++g) {  // padded segment sizes -> group regions
+      const int32_t ge0 = light[gstart[g]].z, ge1 = light[gstart[g + 1] - 1].w;
+      std::fill(cur.begin(), cur.end(), 0);
+      for (int32_t e = ge0; e < ge1; ++e) cur[h->h_col[e] / SN + 1]++;
+      int32_t acc = 0;
+      for (int64_t s = 0; s < P; ++s) {
+        segs[(size_t)g * (P + 1) + s] = acc;
+        acc += (cur[s + 1] + kStagePad - 1) / kStagePad * kStagePad;
+      }
+      segs[(size_t)g * (P + 1) + P] = acc;
+      if (acc > 65536) return fail(FU_ERR_GRAPH, "kernel 8: staged group region exceeds 2^16 elements");
+      gpos[g + 1] = gpos[g] + acc;
+    }
+    const int64_t total = gpos[ng];
+    gmax = std::max<int64_t>(gmax, total);
+    std::vector<uint16_t> colS(std::max<int64_t>(total, kStagePad), 0);  // >= one 16-B load
+    std::vector<uint32_t> sidx(h->E > 0 ? h->E : 1);
+    std::vector<int32_t> gbase(light.size());
     std::vector<int32_t> kpos;
     for (int g = 0; g < ng; ++g) {
       const int t0 = gstart[g], t1 = gstart[g + 1];
       const int32_t ge0 = light[t0].z, ge1 = light[t1 - 1].w;
-      std::fill(cur.begin(), cur.end(), 0);
-      for (int32_t e = ge0; e < ge1; ++e) cur[h->h_col[e] / SN + 1]++;
-      for (int64_t s = 0; s < P; ++s) cur[s + 1] += cur[s];
-      for (int64_t s = 0; s <= P; ++s) segs[(size_t)g * (P + 1) + s] = ge0 + cur[s];
+      for (int64_t s = 0; s <= P; ++s) cur[s] = segs[(size_t)g * (P + 1) + s];
       kpos.assign(ge1 - ge0, 0);
       for (int32_t e = ge0; e < ge1; ++e) {  // stable: (slice, tile, position) order
         const int32_t c = h->h_col[e];
         const int32_t k = cur[c / SN]++;
-        colS[ge0 + k] = (uint16_t)(c % SN);
+        colS[gpos[g] + k] = (uint16_t)(c % SN);
         kpos[e - ge0] = k;
       }
       for (int t = t0; t < t1; ++t) {  // tile elements in slice order (stable in position)
+        gbase[t] = gpos[g];
         const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
         std::vector<int32_t> ord(ne);
         for (int32_t m = 0; m < ne; ++m) ord[m] = m;
@@ -2256,10 +2306,11 @@ int ensure_stage(fu_handle *h) {
         for (int32_t m = 0; m < ne; ++m)
           sidx[e0 + m] = ((uint32_t)kpos[e0 + ord[m] - ge0] << 16) | (uint32_t)ord[m];
       }
+      for (int64_t s = 0; s <= P; ++s) segs[(size_t)g * (P + 1) + s] += gpos[g];  // absolute
     }
     // stage blocks (s, q), blockIdx = s + P * q (slice s on XCD s % 8 when 8 | P); slice
-    // s's segments are cut into items of <= kStageItem elements (one wave each), and its Q
-    // blocks take equal shares of the item list
+    // s's padded segments are cut into items of <= kStageItem elements (one wave each), and
+    // its Q blocks take equal shares of the item list
     const int64_t Q = std::max<int64_t>(1, 512 / P);
     std::vector<int32_t> aoff(P * Q + 1, 0);
     std::vector<int2> aitem;
@@ -2280,10 +2331,12 @@ int ensure_stage(fu_handle *h) {
     L.Q = (int)Q;
     if (int rc = up(&L.aoff, aoff.data(), aoff.size())) return rc;
     if (int rc = up(&L.aitem, aitem.data(), aitem.size())) return rc;
-    if (int rc = up(&L.colS, colS.data(), (size_t)h->E)) return rc;
-    if (int rc = up(&L.sidx, sidx.data(), (size_t)h->E)) return rc;
-    if (h->E == 0) HIP_TRY(hipMemset(L.sidx, 0, sizeof(unsigned)));  // kernel 10 reads sidx[0]
+    if (int rc = up(&L.colS, colS.data(), colS.size())) return rc;
+    if (int rc = up(&L.sidx, sidx.data(), sidx.size())) return rc;
+    if (int rc = up(&L.gbase, gbase.data(), gbase.size())) return rc;
   }
+  if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)gmax)) return rc;
+  HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long) * (size_t)gmax));
   bool any = false;
   for (int li = 0; li < 4; ++li) any |= h->st[li].P > 0;
   if (!any) return fail(FU_ERR_GRAPH, "kernel 8 (staged slices): graph has too many nodes for a slice layout");
@@ -2305,6 +2358,7 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
     sa.aitem[li] = L.aitem;
     sa.colS[li] = L.colS;
     sa.sidx[li] = L.sidx;
+    sa.gbase[li] = L.gbase;
     if (L.P) g = std::max<unsigned>(g, (unsigned)(L.P * L.Q));
   }
   for (int want = 0; want < 4; ++want) {
@@ -2869,6 +2923,9 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   float best = 1e30f;
   int bi = -1;
   for (size_t c = 0; c < cands.size(); ++c) {
+    // a candidate more than 1.3x slower than the winner in two passes sits out the later
+    // ones (its last ns per round stays reported)
+    if (h->tune_out[c] >= 2) continue;
     h->tune_ms[c] = 0.f;
     if (cands[c].kernel == 9) {
       if (ensure_light(h) != FU_OK) {
@@ -2905,6 +2962,9 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
       bi = (int)c;
     }
   }
+  if (bi < 0) return fail(FU_ERR_STATE, "autotune: no candidate ran");
+  for (size_t c = 0; c < cands.size(); ++c)
+    if (h->tune_ms[c] > 1.3f * h->tune_ms[bi]) h->tune_out[c]++;
   h->kernel = cands[bi].kernel;
   h->nt = cands[bi].nt;
   if (h->kernel == 7) h->wgeo = cands[bi].geo;
@@ -3083,7 +3143,7 @@ int fu_destroy(fu_handle *h) {
                   h->stG, h->st[0].aoff, h->st[0].aitem, h->st[0].colS, h->st[0].sidx, h->st[1].aoff,
                   h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
                   h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
-                  h->st[3].sidx};
+                  h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
