@@ -180,8 +180,9 @@ def main():
         if os.path.exists(pmc_path):
             with open(pmc_path) as f:
                 pmc = json.load(f)
-            if pmc.get("n") == g.n and pmc.get("E") == g.E and pmc.get("kernel") == args.kernel:
-                traffic = pmc.get("bytes_per_launch")
+            if pmc.get("n") == g.n and pmc.get("E") == g.E and pmc.get("kernel") == args.kernel and \
+                    pmc.get("kernel_selected") == kinfo["kernel"]:
+                traffic = pmc.get("bytes_per_launch")  # per round, all of the round's launches
         out = {
             "metric": "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error",
             "value": value,
