@@ -50,6 +50,7 @@ def parse():
                          "rgg-dist (ONE random geometric graph of --n nodes per GPU, partitioned "
                          "into slabs across the ranks, RCCL halo exchange every round)")
     ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--tile-edges", type=int, default=0, help="kernel 4 tile (2048/1024/512); 0 = default")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -116,7 +117,10 @@ def main():
         wl = f"rr:n={args.n},d=8 collect-all generation-synchronous rounds"
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
+    print(f"[bench] graph {wl}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
+    if args.tile_edges:
+        eng.set_option("tile_edges", args.tile_edges)
     eng.run(args.warmup)  # with kernel "auto" the first warmup rounds also pick the kernel
     eng.reset()           # the timed region is rounds 0 .. steps-1 from the zero state
     eng.synchronize()

@@ -77,16 +77,26 @@ __global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict_
   double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
   a[i] = ai;
   double fv = (0.0 + ai) - 0.0;
-  for (int k = b; k < e; ++k) {
-    if constexpr (SPLIT) {
-      unsigned *w = reinterpret_cast<unsigned *>(f);
-      const long long j = ((long long)(k & ~31) << 1) | (k & 31);
-      w[j] = (unsigned)__double2hiint(fv);
-      w[j + 32] = (unsigned)__double2loint(fv);
-    } else {
-      f[k] = fv;
-    }
+  if constexpr (!SPLIT)
+    for (int k = b; k < e; ++k) f[k] = fv;  // kernels 1-3 (split flows: k_round0_flows)
+}
+
+// Round 0's flows of kernels >= 4, one thread per edge (a hub's row is not one thread's
+// loop): f[k] = (0.0 + a_0[row of k]) - 0.0 (CA:117 on zero state), split words.
+__global__ __launch_bounds__(kBlock) void k_round0_flows(int n, long long E, const int *__restrict__ rowptr,
+                                                         const double *__restrict__ a, double *__restrict__ f) {
+  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (k >= E) return;
+  int lo = 0, hi = n - 1;  // row i with rowptr[i] <= k < rowptr[i + 1] (non-empty rows only)
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rowptr[mid] <= k) lo = mid; else hi = mid - 1;
   }
+  const double fv = (0.0 + a[lo]) - 0.0;
+  unsigned *w = reinterpret_cast<unsigned *>(f);
+  const long long j = ((k & ~31LL) << 1) | (k & 31);
+  w[j] = (unsigned)__double2hiint(fv);
+  w[j + 32] = (unsigned)__double2loint(fv);
 }
 
 // ------------------------------------------------------------------------------------
@@ -474,6 +484,14 @@ __device__ inline double recon_fr(double f_own_old, double a_nb, double a_own_ol
   return -f_rev;                                            // CA:99 flows[j] = -msg.flow
 }
 
+__device__ inline void wave_sync() {
+  // LDS traffic of one wave is processed in order; this only stops the compiler from moving
+  // LDS accesses across the hand-off between lanes
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // Exact left-to-right chains S += xs[q], T += es[q] over q = 0 .. cn-1 (one wave, lane-
 // uniform). The LDS reads of the next 8 elements are issued before the 16 dependent adds of
 // the current 8, so the chain runs at the fp64 add latency instead of add + LDS latency.
@@ -521,7 +539,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     double *__restrict__ a_new, const double *__restrict__ target,
     unsigned long long *__restrict__ err, const int *__restrict__ perm,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
-    int rslot) {
+    int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -621,6 +639,57 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     return;
   }
   }  // if constexpr (default geometry)
+
+  if (tl.y == -3) {
+    // ---------------- mega hub (degree > mega_hub, default 8192) ----------------
+    // k_hub_stage has already put (fr, er) of every edge of the row into hubxy (many
+    // blocks, coalesced), so the exact left-to-right chain is all that is left: wave 0
+    // streams the pairs through two LDS halves (the loads of chunk c + 1 in flight while
+    // chunk c is summed), with no block barrier and no gather on the chain's path.
+    const int i = tl.x, b = tl.z, e = tl.w;
+    const double2 *xy = hubxy + hub_off[blockIdx.x];
+    const int d = e - b;
+    double S = 0.0, T = 0.0;
+    constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
+    if (t < 64) {
+      double2 nx[PL];
+#pragma unroll
+      for (int u = 0; u < PL; ++u) nx[u] = t + 64 * u < d ? xy[t + 64 * u] : make_double2(0.0, 0.0);
+      for (int c0 = 0; c0 < d; c0 += CH) {
+        double *xs = s_x + ((c0 / CH) & 1) * CH, *es = s_er + ((c0 / CH) & 1) * CH;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          xs[t + 64 * u] = nx[u].x;
+          es[t + 64 * u] = nx[u].y;
+        }
+        const int c1 = c0 + CH;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int k = c1 + t + 64 * u;
+          nx[u] = k < d ? xy[k] : make_double2(0.0, 0.0);
+        }
+        wave_sync();
+        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+        wave_sync();
+      }
+    }
+    if (t == 0) {
+      const double a = ((v[i] - S) + T) / (double)(d + 1);
+      s_a[0] = a;
+      st_wt(a_new + i, a);
+      if (pc.width) put_code(pc, code_new, i, a);
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+    __syncthreads();
+    const double a = s_a[0];
+    for (int k = t; k < d; k += kBlock) {
+      const double2 p2 = xy[k];
+      const double fo = ld_f(F, b + k);
+      st_f(F, b + k, (p2.x + a) - p2.y, fo);
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
 
   if (tl.y < 0) {
     // ---------------- heavy node ----------------
@@ -771,13 +840,6 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 // them. Heavy rows (degree > min(hub_threshold, TE)) run through kernel 4's heavy path in
 // a separate launch before this one.
 // ------------------------------------------------------------------------------------
-__device__ inline void wave_sync() {
-  // LDS traffic of one wave is processed in order; this only stops the compiler from moving
-  // LDS accesses across the hand-off between lanes
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
 
 __device__ inline void wave_max_to(unsigned long long x, unsigned long long *dst) {
   for (int off = 32; off > 0; off >>= 1) {
@@ -1475,6 +1537,30 @@ __global__ __launch_bounds__(kBlock) void k_round_pipe(
   if (CHECK) block_max_to(eb, err);
 }
 
+// Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
+// reconstruction of kernel 4), so k_round_recon's hub block only runs the chain.
+__global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__restrict__ hubs,
+                                                      long long total, const int *__restrict__ col,
+                                                      const double *__restrict__ F,
+                                                      const double *__restrict__ a_prev,
+                                                      const double *__restrict__ a_prev2,
+                                                      const void *__restrict__ code_prev,
+                                                      const PackCtl *__restrict__ ctl, int rslot,
+                                                      double2 *__restrict__ hubxy) {
+  const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= total) return;
+  int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (hubs[mid].w <= q) lo = mid; else hi = mid - 1;
+  }
+  const int4 hb = hubs[lo];
+  const int k = hb.y + (int)(q - hb.w);
+  const PackCtl pp = ctl[rslot ^ 1];
+  const double er = ld_est(pp, code_prev, a_prev, col[k]);
+  hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
+}
+
 __global__ void k_fill_split(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) st_f_full(p, (int)q, val);
@@ -1948,6 +2034,13 @@ struct fu_handle {
   int nwheavy[2] = {0, 0};
   int wgeo = 1;
   int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
+  // kernel 4 mega hubs (degree > mega_hub): first tiles of every geometry ({i, -3, b, e})
+  int mega_hub = 8192;  // degree above which a row is a mega hub (option "mega_hub")
+  int n_hub = 0;
+  int64_t hub_total = 0;
+  int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
+  int *hub_off = nullptr;    // per mega tile: offset in hubxy
+  double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   int bins = 0;         // kernel 4 (geometry 0): degree bins for rows above hub_threshold
   // kernel 4 packed estimate table (see PackCtl): code[r & 1] = codes of a_r
   unsigned char *code[2] = {nullptr, nullptr};
@@ -1993,13 +2086,19 @@ extern "C" void fu__dist_free(fu_handle *h);
 
 namespace {
 
+
 int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
-                     std::vector<int4> *host_out = nullptr) {
-  std::vector<int4> heavy, light;
+                     std::vector<int4> *host_out = nullptr, bool mega = false) {
+  std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
   while (i < n) {
     int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
+    if (mega && d > h->mega_hub) {
+      hubs.push_back(make_int4(i, -3, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
+      ++i;
+      continue;
+    }
     if (d > h->hub_threshold || d > te) {
       heavy.push_back(make_int4(i, -1, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
       ++i;
@@ -2015,8 +2114,9 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
     }
     light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
-  // heavy tiles first so their long sequential chains start early
-  std::vector<int4> all(heavy);
+  // mega hubs, then heavy tiles first so their long sequential chains start early
+  std::vector<int4> all(hubs);
+  all.insert(all.end(), heavy.begin(), heavy.end());
   all.insert(all.end(), light.begin(), light.end());
   if (host_out) *host_out = all;
   if (*dst) hipFree(*dst);
@@ -2114,6 +2214,35 @@ int build_wave_tiles(fu_handle *h, int wg) {
   return FU_OK;
 }
 
+// Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
+int build_hubs(fu_handle *h) {
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy})
+    if (p) hipFree(p);
+  h->hub_rows = nullptr;
+  h->hub_off = nullptr;
+  h->hubxy = nullptr;
+  std::vector<int4> rows;
+  std::vector<int32_t> off;
+  int64_t tot = 0;
+  for (int32_t i = 0; i < h->n; ++i) {
+    const int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
+    if (d > h->mega_hub) {
+      rows.push_back(make_int4(i, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1], (int)tot));
+      off.push_back((int32_t)tot);
+      tot += d;
+    }
+  }
+  h->n_hub = (int)rows.size();
+  h->hub_total = tot;
+  if (rows.empty()) return FU_OK;
+  if (int rc = dmalloc(&h->hub_rows, rows.size())) return rc;
+  if (int rc = dmalloc(&h->hub_off, off.size())) return rc;
+  if (int rc = dmalloc(&h->hubxy, (size_t)tot)) return rc;
+  HIP_TRY(hipMemcpy(h->hub_rows, rows.data(), sizeof(int4) * rows.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->hub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
+  return FU_OK;
+}
+
 int build_tiles(fu_handle *h) {
   if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
   for (int wg = 0; wg < 2; ++wg)
@@ -2123,9 +2252,10 @@ int build_tiles(fu_handle *h) {
       if (int rc = build_tiles_binned(h)) return rc;
       continue;
     }
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g])) return rc;
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], nullptr, true))
+      return rc;
   }
-  return FU_OK;
+  return build_hubs(h);
 }
 
 // Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
@@ -2402,6 +2532,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (r == 0) {
       hipLaunchKernelGGL(k_round0<true>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
                          h->rowptr, h->v, h->f[0], h->a[0]);
+      if (h->E)
+        hipLaunchKernelGGL(k_round0_flows, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, h->n,
+                           (long long)h->E, h->rowptr, h->a[0], h->f[0]);
       if (h->E)  // f_{-1} = -0.0 (split words) so that round 1 reproduces (0.0 + a) - 0.0
         hipLaunchKernelGGL(k_fill_split, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
                            -0.0, h->f[1]);
@@ -2484,11 +2617,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1));
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1));
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
       }
       if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
         hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
@@ -2522,11 +2655,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1));
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1));
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
       }
       if (h->nwtiles[wg]) {
         const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
@@ -2545,10 +2678,14 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
+      if (h->n_hub && !(h->geo == 0 && h->bins))
+        hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream, h->n_hub,
+                           h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1],
+                           h->pctl, (int)(r & 1), h->hubxy);
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
   hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_geo[h->geo]), dim3(kBlock), 0, \
                      h->stream, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1))
+                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
     if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
@@ -2857,6 +2994,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
     return FU_OK;
   }
+  if (!std::strcmp(key, "mega_hub")) {  // kernel 4: staged-chain rows (tests lower it)
+    if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: mega_hub must be >= 1");
+    h->mega_hub = (int)std::min<int64_t>(value, INT32_MAX);
+    return build_tiles(h);
+  }
   if (!std::strcmp(key, "hub_threshold")) {
     if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: hub_threshold must be >= 1");
     h->hub_threshold = (int)std::min<int64_t>(value, kTileEdges);
@@ -3143,7 +3285,8 @@ int fu_destroy(fu_handle *h) {
                   h->stG, h->st[0].aoff, h->st[0].aitem, h->st[0].colS, h->st[0].sidx, h->st[1].aoff,
                   h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
                   h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
-                  h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase};
+                  h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase,
+                  h->hub_rows, h->hub_off, h->hubxy};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

@@ -418,3 +418,39 @@ def test_pipe_grid_sizes_bitwise(kernel, bpc):
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+@pytest.mark.parametrize("tile", [2048, 1024, 512])
+@pytest.mark.parametrize("mega", [64, 300, 8192])
+def test_mega_hub_staged_chain_bitwise(tile, mega):
+    """Kernel 4's mega-hub path (k_hub_stage + a chain-only block) on R-MAT rows above the
+    threshold, every tile geometry, unpacked and packed rounds, against the C oracle."""
+    g = fu.Graph.rmat(14, 16, seed=12)
+    v = fu.uniform_values(g.n, seed=12)
+    eng = fu.CollectAll(g, v, kernel="recon")
+    eng.set_option("tile_edges", tile)
+    eng.set_option("mega_hub", mega)
+    eng.set_option("pack_every", 4)
+    eng.run(60)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 60, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
+def test_star_hub_above_default_mega_threshold():
+    """A 20000-leaf star (one row far above the default 8192 threshold) joined to an ER graph."""
+    n_er, leaves = 30_000, 20_000
+    er = fu.Graph.erdos_renyi(n_er, 120_000, seed=13)
+    src = np.repeat(np.arange(er.n), np.diff(er.rowptr))
+    keep = src < er.col
+    hub = n_er + leaves
+    s = np.concatenate([src[keep], np.full(leaves, hub), [0]])
+    d = np.concatenate([er.col[keep], n_er + np.arange(leaves), [hub]])
+    g = fu.Graph.from_edges(hub + 1, s, d)
+    assert g.max_deg > 8192
+    v = fu.uniform_values(g.n, seed=13)
+    eng = fu.CollectAll(g, v, kernel="recon")
+    eng.run(40)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 40, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
