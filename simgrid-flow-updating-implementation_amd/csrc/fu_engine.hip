@@ -496,7 +496,7 @@ __device__ inline void wave_sync() {
 // uniform). The LDS reads of the next 8 elements are issued before the 16 dependent adds of
 // the current 8, so the chain runs at the fp64 add latency instead of add + LDS latency.
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
-  constexpr int B = 8;
+  constexpr int B = 4;
   int q = 0;
   if (cn >= B) {
     double a[B], b[B];
@@ -539,7 +539,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     double *__restrict__ a_new, const double *__restrict__ target,
     unsigned long long *__restrict__ err, const int *__restrict__ perm,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
-    int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off) {
+    int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
+    const int *__restrict__ hrows) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -639,6 +640,70 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     return;
   }
   }  // if constexpr (default geometry)
+
+  if (tl.y == -4) {
+    // ---------------- heavy rows, one per wave ----------------
+    // Rows hrows[tl.x .. tl.x + tl.z) (degree > hub_threshold, <= mega_hub, sorted by
+    // degree so a block's waves finish together): wave w owns one row and its quarter of
+    // s_x / s_er, stages the row chunk by chunk (each lane TE / 256 elements), runs the
+    // exact left-to-right chain (lane-uniform) and rewrites the row's flows. No block
+    // barrier: 4 rows per block progress independently.
+    constexpr int CH = TE / 4, PL = CH / 64;
+    const int w = t >> 6, lane = t & 63;
+    if (w < tl.z) {
+      const int i = hrows[tl.x + w];
+      const int b = rowptr[i], e = rowptr[i + 1], d = e - b;
+      const double own2 = a_prev2[i];
+      double *xs = s_x + w * CH, *es = s_er + w * CH;
+      double S = 0.0, T = 0.0;
+      for (int c0 = 0; c0 < d; c0 += CH) {
+        int cc[PL];
+        double fo[PL];
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int k = c0 + lane + 64 * u;
+          cc[u] = k < d ? col[b + k] : 0;
+          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+        }
+        double er[PL];
+#pragma unroll
+        for (int u = 0; u < PL; ++u) er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+        wave_sync();  // the previous chunk's chain is done with the buffer
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          xs[lane + 64 * u] = recon_fr(fo[u], er[u], own2);
+          es[lane + 64 * u] = er[u];
+        }
+        wave_sync();
+        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+      }
+      const double a = ((v[i] - S) + T) / (double)(d + 1);
+      if (lane == 0) {
+        st_wt(a_new + i, a);
+        if (pc.width) put_code(pc, code_new, i, a);
+        if (CHECK) eb = err_bits(a, target[i]);
+      }
+      for (int k0 = 0; k0 < d; k0 += 4 * 64) {  // flows (CA:117-118), 4 loads in flight per lane
+        int cc[4];
+        double fo[4], er[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + lane + 64 * u;
+          cc[u] = k < d ? col[b + k] : 0;
+          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) er[u] = k0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int k = k0 + lane + 64 * u;
+          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
+        }
+      }
+    }
+    if (CHECK) block_max_to(eb, err);
+    return;
+  }
 
   if (tl.y == -3) {
     // ---------------- mega hub (degree > mega_hub, default 8192) ----------------
@@ -2036,6 +2101,9 @@ struct fu_handle {
   int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
   // kernel 4 mega hubs (degree > mega_hub): first tiles of every geometry ({i, -3, b, e})
   int mega_hub = 8192;  // degree above which a row is a mega hub (option "mega_hub")
+  int wave_heavy = 1;   // kernel 4: heavy rows one per wave (option "wave_heavy")
+  std::vector<int32_t> h_hrows;
+  int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first
   int n_hub = 0;
   int64_t hub_total = 0;
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
@@ -2114,9 +2182,23 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
     }
     light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
-  // mega hubs, then heavy tiles first so their long sequential chains start early
+  // mega hubs, then heavy tiles first so their long sequential chains start early; heavy
+  // rows of up to mega_hub go four to a block (one per wave) when wave_heavy is on, longest
+  // first (the row list hrows is shared by every geometry)
   std::vector<int4> all(hubs);
-  all.insert(all.end(), heavy.begin(), heavy.end());
+  if (mega && h->wave_heavy && !heavy.empty()) {
+    std::vector<int32_t> rows;
+    for (const int4 &hv : heavy) rows.push_back(hv.x);
+    std::stable_sort(rows.begin(), rows.end(), [&](int32_t x, int32_t y) {
+      return h->h_rowptr[x + 1] - h->h_rowptr[x] > h->h_rowptr[y + 1] - h->h_rowptr[y];
+    });
+    const size_t base = h->h_hrows.size();  // each geometry appends its own list
+    h->h_hrows.insert(h->h_hrows.end(), rows.begin(), rows.end());
+    for (size_t q = 0; q < rows.size(); q += 4)
+      all.push_back(make_int4((int)(base + q), -4, (int)std::min<size_t>(4, rows.size() - q), 0));
+  } else {
+    all.insert(all.end(), heavy.begin(), heavy.end());
+  }
   all.insert(all.end(), light.begin(), light.end());
   if (host_out) *host_out = all;
   if (*dst) hipFree(*dst);
@@ -2244,6 +2326,7 @@ int build_hubs(fu_handle *h) {
 }
 
 int build_tiles(fu_handle *h) {
+  h->h_hrows.clear();
   if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
   for (int wg = 0; wg < 2; ++wg)
     if (int rc = build_wave_tiles(h, wg)) return rc;
@@ -2255,6 +2338,11 @@ int build_tiles(fu_handle *h) {
     if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], nullptr, true))
       return rc;
   }
+  if (h->hrows) hipFree(h->hrows);
+  h->hrows = nullptr;
+  if (int rc = dmalloc(&h->hrows, std::max<size_t>(1, h->h_hrows.size()))) return rc;
+  if (!h->h_hrows.empty())
+    HIP_TRY(hipMemcpy(h->hrows, h->h_hrows.data(), sizeof(int32_t) * h->h_hrows.size(), hipMemcpyHostToDevice));
   return build_hubs(h);
 }
 
@@ -2617,11 +2705,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
       }
       if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
         hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
@@ -2655,11 +2743,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
       }
       if (h->nwtiles[wg]) {
         const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
@@ -2685,7 +2773,8 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
   hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_geo[h->geo]), dim3(kBlock), 0, \
                      h->stream, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off)
+                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
+                     h->hrows)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
     if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
@@ -2994,6 +3083,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
     return FU_OK;
   }
+  if (!std::strcmp(key, "wave_heavy")) {  // kernel 4: heavy rows one per wave (1) or per block (0)
+    h->wave_heavy = value != 0;
+    return build_tiles(h);
+  }
   if (!std::strcmp(key, "mega_hub")) {  // kernel 4: staged-chain rows (tests lower it)
     if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: mega_hub must be >= 1");
     h->mega_hub = (int)std::min<int64_t>(value, INT32_MAX);
@@ -3286,7 +3379,7 @@ int fu_destroy(fu_handle *h) {
                   h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
                   h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
                   h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase,
-                  h->hub_rows, h->hub_off, h->hubxy};
+                  h->hub_rows, h->hub_off, h->hubxy, h->hrows};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

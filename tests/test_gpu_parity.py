@@ -454,3 +454,21 @@ def test_star_hub_above_default_mega_threshold():
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 40, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+@pytest.mark.parametrize("wave_heavy", [0, 1])
+@pytest.mark.parametrize("tile", [2048, 1024, 512])
+def test_heavy_rows_wave_and_block_paths_bitwise(tile, wave_heavy):
+    """Kernel 4's heavy rows (degree > hub_threshold) one per wave (default) or one per block,
+    with mega hubs above 300 in the staged path, every geometry, packed rounds included."""
+    g = fu.Graph.rmat(14, 16, seed=14)
+    v = fu.uniform_values(g.n, seed=14)
+    eng = fu.CollectAll(g, v, kernel="recon", hub_threshold=16)
+    eng.set_option("tile_edges", tile)
+    eng.set_option("wave_heavy", wave_heavy)
+    eng.set_option("mega_hub", 300)
+    eng.set_option("pack_every", 4)
+    eng.run(80)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 80, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)

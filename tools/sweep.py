@@ -49,6 +49,8 @@ VARIANTS = {
     "diag2_stage_nopack": ("stage", {"pack": 0, "diag": 2}),
     "diag3_stage": ("stage", {"diag": 3}),
     "pipe": ("pipe", {}),
+    "recon_512_blockheavy": ("recon", {"tile_edges": 512, "wave_heavy": 0}),
+    "recon_blockheavy": ("recon", {"wave_heavy": 0}),
     "diag4_stage": ("stage", {"diag": 4}),
     "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
     "pipe_nopack": ("pipe", {"pack": 0}),
