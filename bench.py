@@ -50,6 +50,10 @@ def parse():
                          "rgg-dist (ONE random geometric graph of --n nodes per GPU, partitioned "
                          "into slabs across the ranks, RCCL halo exchange every round)")
     ap.add_argument("--kernel", default="auto")
+    ap.add_argument("--layout", default="auto", choices=["auto", "given", "degree"],
+                    help="device node numbering: degree = relabelled by degree (hot estimates "
+                         "share cache lines; outputs keep the caller's numbering); auto = "
+                         "degree for rmat, given otherwise")
     ap.add_argument("--tile-edges", type=int, default=0, help="kernel 4 tile (2048/1024/512); 0 = default")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
@@ -118,7 +122,8 @@ def main():
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
     print(f"[bench] graph {wl}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
-    eng = fu.CollectAll(g, v, device=local, kernel=args.kernel)
+    layout = args.layout if args.layout != "auto" else ("degree" if args.workload == "rmat" else "given")
+    eng = fu.CollectAll(g, v, device=local, kernel=args.kernel, layout=layout)
     if args.tile_edges:
         eng.set_option("tile_edges", args.tile_edges)
     eng.run(args.warmup)  # with kernel "auto" the first warmup rounds also pick the kernel
@@ -199,11 +204,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f64",
-            "data": "synthetic (seeded ER graph, U[0,100) values)",
+            "data": f"synthetic (seeded {args.workload} graph, U[0,100) values)",
             "config": {
                 "workload": wl,
                 "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
-                "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel,
+                "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel, "layout": layout,
                 "kernel_selected": kinfo["kernel"] + ("+nt" if kinfo["nt"] else ""),
                 "tile_selected": kinfo["tile"],
                 "autotune_passes": kinfo["tune_passes"],

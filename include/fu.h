@@ -74,6 +74,12 @@ int fu_graph_info(const fu_graph *g, int32_t *n, int64_t *e, int32_t *max_deg,
 /* Copy out; any output may be NULL. rev[e] = index of the reverse edge (symmetric only). */
 int fu_graph_export(const fu_graph *g, int64_t *rowptr, int32_t *col, int32_t *rev);
 int fu_graph_free(fu_graph *g);
+/* Node relabelling for gather locality: node i of g becomes node new_of_old[i] of *out.
+ * Rows move as blocks and keep their neighbour order (the summation order of
+ * avg_and_send, CA:106 / CA:110), so a round on *out computes, per node, the same bits.
+ * order 0: new_of_old is given (must be a permutation); order 1: degree descending, ties
+ * by id (the nodes most gathered first), written to new_of_old. rev follows the rows. */
+int fu_graph_relabel(const fu_graph *g, int32_t order, int32_t *new_of_old, fu_graph **out);
 /* value[i] = lo + (hi - lo) * U_i, U_i = (splitmix64(seed + (i+1)*0x9E3779B97F4A7C15) >> 11) * 2^-53 */
 int fu_values_uniform(int64_t n, uint64_t seed, double lo, double hi, double *out);
 
@@ -92,6 +98,11 @@ int fu_create(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
               const int32_t *rev, const double *value, int32_t device, fu_handle **out);
 int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
                          fu_handle **out);
+/* layout 0 = as fu_create_from_graph; 1 = the device graph is relabelled by degree
+ * (fu_graph_relabel order 1) so the most-gathered estimates share cache lines. value,
+ * targets, estimates and flows stay in the caller's numbering: the handle maps them. */
+int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t device,
+                            int32_t layout, fu_handle **out);
 /* Options: "kernel" (0 = auto = 4, 1 = thread-per-node, 2 = LDS tile (pull), 3 = push/inbox,
  *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch,
  *          6 = 4 with the low half of each row staged by a gather launch

@@ -496,7 +496,7 @@ __device__ inline void wave_sync() {
 // uniform). The LDS reads of the next 8 elements are issued before the 16 dependent adds of
 // the current 8, so the chain runs at the fp64 add latency instead of add + LDS latency.
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
-  constexpr int B = 4;
+  constexpr int B = 8;
   int q = 0;
   if (cn >= B) {
     double a[B], b[B];
@@ -2044,6 +2044,10 @@ int dmalloc(T **p, size_t count) {
 // ======================================================================================
 struct fu_handle {
   int device = 0;
+  // layout 1 (fu_create_from_graph_ex): device node p = caller node old_of_new[p]; the
+  // caller's row pointer maps flows back (rows moved as blocks)
+  std::vector<int32_t> h_new_of_old;
+  std::vector<int64_t> h_orig_rowptr;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
@@ -2995,6 +2999,26 @@ int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
   return fu__create_common(g->n, E, g->rowptr.data(), g->col.data(), g->rev.data(), value, device, 0, 0, out);
 }
 
+int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t device,
+                            int32_t layout, fu_handle **out) {
+  FU_TRY_BEGIN
+  if (!g || !value || !out || layout < 0 || layout > 1) return fail(FU_ERR_ARG, "fu_create_from_graph_ex: bad arguments");
+  if (layout == 0) return fu_create_from_graph(g, value, device, out);
+  const int32_t n = g->n;
+  std::vector<int32_t> nofo(n);
+  fu_graph *rg = nullptr;
+  if (int rc = fu_graph_relabel(g, 1, nofo.data(), &rg)) return rc;
+  std::vector<double> v2(n);
+  for (int32_t i = 0; i < n; ++i) v2[nofo[i]] = value[i];
+  const int rc = fu_create_from_graph(rg, v2.data(), device, out);
+  fu_graph_free(rg);
+  if (rc) return rc;
+  (*out)->h_new_of_old.swap(nofo);
+  (*out)->h_orig_rowptr = g->rowptr;
+  return FU_OK;
+  FU_TRY_END
+}
+
 int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
@@ -3115,6 +3139,12 @@ int fu_reset(fu_handle *h) {
 int fu_set_targets(fu_handle *h, const double *target) {
   if (!h || !target) return fail(FU_ERR_ARG, "fu_set_targets: NULL argument");
   if (int rc = set_device(h)) return rc;
+  std::vector<double> t2;
+  if (!h->h_new_of_old.empty()) {  // caller numbering -> device numbering
+    t2.resize(h->n);
+    for (int32_t i = 0; i < h->n; ++i) t2[h->h_new_of_old[i]] = target[i];
+    target = t2.data();
+  }
   HIP_TRY(hipMemcpyAsync(h->target, target, sizeof(double) * h->n, hipMemcpyHostToDevice, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->has_target = true;
@@ -3296,6 +3326,13 @@ int fu_max_err(fu_handle *h, double *out) {
 int fu_get_estimates(fu_handle *h, double *a_out) {
   if (!h || !a_out) return fail(FU_ERR_ARG, "fu_get_estimates: NULL argument");
   if (int rc = set_device(h)) return rc;
+  if (!h->h_new_of_old.empty()) {  // device numbering -> caller numbering
+    std::vector<double> a2(h->n);
+    HIP_TRY(hipMemcpyAsync(a2.data(), cur_a(h), sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    for (int32_t i = 0; i < h->n; ++i) a_out[i] = a2[h->h_new_of_old[i]];
+    return FU_OK;
+  }
   HIP_TRY(hipMemcpyAsync(a_out, cur_a(h), sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FU_OK;
@@ -3321,6 +3358,17 @@ int fu_get_flows(fu_handle *h, double *f_out) {
     hipLaunchKernelGGL(k_unsplit, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E, src, h->ftmp);
     HIP_TRY(hipGetLastError());
     src = h->ftmp;
+  }
+  if (!h->h_new_of_old.empty()) {  // rows back to the caller's order (blocks, same order inside)
+    std::vector<double> f2(h->E);
+    HIP_TRY(hipMemcpyAsync(f2.data(), src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    const auto &orp = h->h_orig_rowptr;
+    for (int32_t i = 0; i < h->n; ++i) {
+      const int64_t nb = h->h_rowptr[h->h_new_of_old[i]];
+      std::memcpy(f_out + orp[i], f2.data() + nb, sizeof(double) * (orp[i + 1] - orp[i]));
+    }
+    return FU_OK;
   }
   HIP_TRY(hipMemcpyAsync(f_out, src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));

@@ -413,6 +413,60 @@ int fu_graph_free(fu_graph *g) {
   return FU_OK;
 }
 
+int fu_graph_relabel(const fu_graph *g, int32_t order, int32_t *new_of_old, fu_graph **out) {
+  FU_TRY_BEGIN
+  if (!g || !new_of_old || !out || order < 0 || order > 1) return fail(FU_ERR_ARG, "fu_graph_relabel: bad arguments");
+  const int32_t n = g->n;
+  const int64_t E = g->rowptr[n];
+  const bool sym = (int64_t)g->rev.size() == E;
+  std::vector<int32_t> old_of_new(n);
+  if (order == 1) {  // degree descending, ties by old id: the gather-hot nodes first
+    std::iota(old_of_new.begin(), old_of_new.end(), 0);
+    std::stable_sort(old_of_new.begin(), old_of_new.end(), [&](int32_t x, int32_t y) {
+      return g->rowptr[x + 1] - g->rowptr[x] > g->rowptr[y + 1] - g->rowptr[y];
+    });
+    for (int32_t p = 0; p < n; ++p) new_of_old[old_of_new[p]] = p;
+  } else {
+    std::vector<char> seen(n, 0);
+    for (int32_t i = 0; i < n; ++i) {
+      const int32_t p = new_of_old[i];
+      if (p < 0 || p >= n || seen[p]) return fail(FU_ERR_ARG, "fu_graph_relabel: new_of_old is not a permutation");
+      seen[p] = 1;
+      old_of_new[p] = i;
+    }
+  }
+  auto *h = new fu_graph();
+  h->n = n;
+  h->max_deg = g->max_deg;
+  h->rowptr.assign(n + 1, 0);
+  for (int32_t p = 0; p < n; ++p) {
+    const int32_t i = old_of_new[p];
+    h->rowptr[p + 1] = h->rowptr[p] + (g->rowptr[i + 1] - g->rowptr[i]);
+  }
+  h->col.resize(E);
+  // rows move as blocks and keep their neighbour order (the summation order, CA:106/110)
+#pragma omp parallel for schedule(dynamic, 4096)
+  for (int32_t p = 0; p < n; ++p) {
+    const int32_t i = old_of_new[p];
+    const int64_t b = g->rowptr[i], d = g->rowptr[i + 1] - b, nb = h->rowptr[p];
+    for (int64_t k = 0; k < d; ++k) h->col[nb + k] = new_of_old[g->col[b + k]];
+  }
+  if (sym) {  // new position of old edge k: rows moved as blocks, so rev maps through it
+    std::vector<int32_t> pos(E);
+#pragma omp parallel for schedule(dynamic, 4096)
+    for (int32_t i = 0; i < n; ++i) {
+      const int64_t b = g->rowptr[i], d = g->rowptr[i + 1] - b, nb = h->rowptr[new_of_old[i]];
+      for (int64_t k = 0; k < d; ++k) pos[b + k] = (int32_t)(nb + k);
+    }
+    h->rev.resize(E);
+#pragma omp parallel for schedule(static)
+    for (int64_t k = 0; k < E; ++k) h->rev[pos[k]] = pos[g->rev[k]];
+  }
+  *out = h;
+  return FU_OK;
+  FU_TRY_END
+}
+
 int fu_values_uniform(int64_t n, uint64_t seed, double lo, double hi, double *out) {
   if (n < 0 || (n > 0 && !out)) return fail(FU_ERR_ARG, "fu_values_uniform: bad arguments");
   const double w = hi - lo;

@@ -54,9 +54,11 @@ _SIGS = {
     "fu_graph_info": ([vp, P(i32), P(i64), P(i32), P(i32)], ctypes.c_int),
     "fu_graph_export": ([vp, vp, vp, vp], ctypes.c_int),
     "fu_graph_free": ([vp], ctypes.c_int),
+    "fu_graph_relabel": ([vp, i32, vp, P(vp)], ctypes.c_int),
     "fu_values_uniform": ([i64, u64, f64, f64, vp], ctypes.c_int),
     "fu_create": ([i32, i64, vp, vp, vp, vp, i32, P(vp)], ctypes.c_int),
     "fu_create_from_graph": ([vp, vp, i32, P(vp)], ctypes.c_int),
+    "fu_create_from_graph_ex": ([vp, vp, i32, i32, P(vp)], ctypes.c_int),
     "fu_set_option": ([vp, cp, i64], ctypes.c_int),
     "fu_reset": ([vp], ctypes.c_int),
     "fu_set_targets": ([vp, vp], ctypes.c_int),

@@ -18,6 +18,7 @@ from .graph import Graph
 
 KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6, "wave": 7, "stage": 8, "pipe": 9,
            "pipe_stage": 10}
+LAYOUTS = {"given": 0, "degree": 1}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
@@ -31,16 +32,21 @@ class CollectAll:
 
     def __init__(self, graph: Graph | None = None, values=None, *, rowptr=None, col=None,
                  rev=None, device: int = 0, kernel: str | int = "auto",
-                 hub_threshold: int | None = None):
+                 hub_threshold: int | None = None, layout: str = "given"):
+        """layout "degree" relabels the device graph by degree (fu_create_from_graph_ex):
+        the most-gathered estimates share cache lines; inputs and outputs keep the caller's
+        numbering, bits per node unchanged."""
         self.values = np.ascontiguousarray(values, dtype=np.float64)
         out = L.vp()
         if graph is not None:
             if len(self.values) != graph.n:
                 raise ValueError("len(values) != graph.n")
-            L.call("fu_create_from_graph", graph._h, L.ptr(self.values), int(device),
-                   ctypes.byref(out))
+            L.call("fu_create_from_graph_ex", graph._h, L.ptr(self.values), int(device),
+                   LAYOUTS[layout], ctypes.byref(out))
             self.n, self.E = graph.n, graph.E
         else:
+            if layout != "given":
+                raise ValueError("layout needs a Graph")
             rp = np.ascontiguousarray(rowptr, dtype=np.int64)
             c = np.ascontiguousarray(col, dtype=np.int32)
             r = None if rev is None else np.ascontiguousarray(rev, dtype=np.int32)

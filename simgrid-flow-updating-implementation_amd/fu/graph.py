@@ -96,6 +96,22 @@ class Graph:
                                         seed=seed)
         raise ValueError(f"unknown graph spec {spec!r}")
 
+    def relabel(self, order="degree", new_of_old=None):
+        """(relabelled Graph, new_of_old): node i becomes new_of_old[i]; rows keep their
+        neighbour order (fu_graph_relabel). order "degree" (descending, ties by id) or
+        "given" with new_of_old a permutation."""
+        if order == "degree":
+            perm, mode = np.empty(self.n, dtype=np.int32), 1
+        elif order == "given":
+            perm, mode = np.ascontiguousarray(new_of_old, dtype=np.int32).copy(), 0
+            if perm.shape != (self.n,):
+                raise ValueError("new_of_old must have n entries")
+        else:
+            raise ValueError(f"unknown order {order!r}")
+        out = L.vp()
+        L.call("fu_graph_relabel", self._h, mode, L.ptr(perm), ctypes.byref(out))
+        return Graph(out), perm
+
     # ---------------- arrays ----------------
     def arrays(self):
         if self._arrays is None:

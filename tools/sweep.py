@@ -64,6 +64,12 @@ VARIANTS = {
     "diag3_stage_nopack": ("stage", {"pack": 0, "diag": 3}),
     "diag1_512_nopack": ("recon", {"tile_edges": 512, "pack": 0, "diag": 1}),
     "recon_512_nopack": ("recon", {"tile_edges": 512, "pack": 0}),
+    "recon_deg": ("recon", {"layout": "degree"}),
+    "recon_512_deg": ("recon", {"tile_edges": 512, "layout": "degree"}),
+    "stage_deg": ("stage", {"layout": "degree"}),
+    "auto_deg": ("auto", {"layout": "degree"}),
+    "auto": ("auto", {}),
+    "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -78,9 +84,9 @@ for spec in specs:
     engs = {}
     for nm in names:
         kern, o = VARIANTS[nm]
-        e = fu.CollectAll(g, v, kernel=kern)
+        e = fu.CollectAll(g, v, kernel=kern, layout=o.get("layout", "given"))
         for k, val in o.items():
-            if k != "diag":
+            if k not in ("diag", "layout"):
                 e.set_option(k, val)
         e.run(warm)
         if "diag" in o:
