@@ -114,6 +114,10 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "pack" (kernel 4: gather lossless 8/16/32-bit codes of the estimates once they have
  *          converged into a narrow cluster; default 1), "pack_every" (rounds between
  *          encoding plans; default 16), "bins" (degree bins for kernel 4's heavy rows),
+ * "mega_hub" (kernel 4: degree above which a row's (fr, er) pairs are staged by many blocks;
+ *          default 8192), "hub_scan" (mega hubs: 1 = parallel exact left-to-right sums,
+ *          speculated per binade and verified; 0 = one wave's sequential chain, default),
+ * "wave_heavy" (kernel 4: rows above hub_threshold one per wave (1, default) or per block),
  * "pipe_bpc" (kernels 9/10: persistent blocks per CU; default 6), "stage_layout" (kernels
  *          8/10, tests: -1 = by packing width, 0..3 = slice layout of 1/2/4/8-byte elements). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
@@ -138,7 +142,9 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done);
 /* info[0] = kernel in use, [1] = nt, [2] = autotune (0 off, 1 pending, 2 done),
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
  * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
- * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run). With kernel
+ * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run), [20] = mega hubs, [21] = their
+ * pieces, [22] = pieces the exact-sum serial pass redid element by element (cumulative;
+ * synchronises). With kernel
  * "auto" (the default) a fu_run_collectall(_timed) with >= 45 rounds left after round 0
  * times the candidates on real rounds (they share state and are bitwise identical) and keeps
  * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */

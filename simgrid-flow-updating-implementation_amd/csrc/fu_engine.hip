@@ -520,6 +520,175 @@ __device__ __forceinline__ void chain_sum(const double *xs, const double *es, in
   }
 }
 
+// ------------------------------------------------------------------------------------
+// Mega hubs: the exact left-to-right sums of avg_and_send (CA:106, CA:110) in parallel.
+// Python's sum is the chain s_{k+1} = fl(s_k + x_k) from s_0 = 0: inherently sequential,
+// and one wave running it for a 406K-edge R-MAT hub needs ~3 ms per round. The chain is
+// decomposed instead (host prototype and adversarial checks: tools/exact_scan_proto.c):
+//   * an approximate prefix p_k (any summation order) gives a speculative key of s_{k+1}:
+//     its ulp exponent ue (u = 2^ue) and sign;
+//   * a step whose key differs from the previous step's is a BOUNDARY: it is done later as
+//     one exact fp64 add in a short serial pass;
+//   * every other step keeps s a multiple of u, so s_{k+1} = u (m_k + t_k) with
+//     t_k = round(x_k / u), ties to the even m_k + t_k: t_k depends on m_k only through its
+//     parity. A step is a 2-state transducer (t0, t1, q0, q1); compositions stay in that form,
+//     plus the min / max of the partial increments, so a RUN of such steps is one RunSum;
+//   * the serial pass walks pieces of 2048 elements: head run, then per boundary its exact
+//     add and the run after it, VERIFYING each run in O(1): every result must satisfy
+//     2^52 < |m| < 2^53 (the exact sum was inside the binade, so fl rounded at u). A piece
+//     that fails (speculation wrong, > kMaxBnd boundaries, zeros / subnormals) is redone
+//     element by element. The result is the chain's bits in every case.
+// ------------------------------------------------------------------------------------
+constexpr int kPieceT = 8;                // elements per thread
+constexpr int kPiece = kBlock * kPieceT;  // elements per piece (one block)
+constexpr int kMaxBnd = 32;               // boundaries listed per piece and chain
+constexpr int kKeySpecial = -1000000;     // zero, subnormal, inf, nan
+constexpr long long kRunLim = 1LL << 56;  // |t|, |mn|, |mx| bound of a verifiable run
+
+struct RunSum {
+  long long t0, t1, mn, mx;  // increment for start parity 0 / 1; min / max partial increment
+  int len, q;                // steps; q bit0 / bit1 = end parity for start parity 0 / 1, bit2 = bad
+};
+struct BndSum {
+  double x;  // the boundary element
+  int key, pad;
+  RunSum run;  // the run after it (up to the next boundary or the piece end)
+};
+struct PieceSum {
+  int first_key, nb, pad0, pad1;  // key the head run assumes; boundaries (> kMaxBnd: dense)
+  RunSum head;
+  BndSum b[kMaxBnd];
+  long long pad_end;
+};
+static_assert(sizeof(PieceSum) % 16 == 0, "PieceSum is copied in 16-byte words");
+constexpr int kPieceWords = (int)(sizeof(PieceSum) / 16);
+
+__device__ __forceinline__ int ulp_key(double x) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
+  const int E = (int)((b >> 52) & 0x7ff);
+  return (E == 0 || E == 0x7ff) ? kKeySpecial : ((E - 1075) * 2) | (int)(b >> 63);
+}
+__device__ __forceinline__ RunSum run_id() { return RunSum{0, 0, 0, 0, 0, 2}; }
+__device__ __forceinline__ RunSum run_cat(const RunSum &a, const RunSum &b) {  // a, then b
+  if (b.len == 0) return a;
+  if (a.len == 0) return b;
+  const int a0 = a.q & 1, a1 = (a.q >> 1) & 1, b0 = b.q & 1, b1 = (b.q >> 1) & 1;
+  RunSum r;
+  r.t0 = a.t0 + (a0 ? b.t1 : b.t0);
+  r.t1 = a.t1 + (a1 ? b.t1 : b.t0);
+  // b's partial increments start at a.t0 or a.t1: conservative bounds over both
+  r.mn = min(a.mn, min(a.t0, a.t1) + b.mn);
+  r.mx = max(a.mx, max(a.t0, a.t1) + b.mx);
+  r.len = a.len + b.len;
+  r.q = (a0 ? b1 : b0) | ((a1 ? b1 : b0) << 1) | ((a.q | b.q) & 4);
+  // |values| <= 2^56 in, <= 2^57 out: no overflow; a run that large can never verify
+  if (r.mn < -kRunLim || r.mx > kRunLim) r.q |= 4;
+  return r;
+}
+__device__ __forceinline__ RunSum run_step(double x, int ue) {
+  const double y = ldexp(x, -ue);  // exact (a power-of-two scaling)
+  RunSum r;
+  r.len = 1;
+  if (!(fabs(y) < 0x1p54)) {  // the result cannot stay in the binade
+    r.t0 = r.t1 = r.mn = r.mx = 0;
+    r.q = 2 | 4;
+    return r;
+  }
+  const double fl = floor(y), fr = y - fl;  // both exact
+  const long long f = (long long)fl;
+  long long t0, t1;
+  if (fr < 0.5) t0 = t1 = f;
+  else if (fr > 0.5) t0 = t1 = f + 1;
+  else {  // tie: the even m + t
+    t0 = (f & 1) ? f + 1 : f;
+    t1 = (f & 1) ? f : f + 1;
+  }
+  r.t0 = t0;
+  r.t1 = t1;
+  r.mn = min(t0, t1);
+  r.mx = max(t0, t1);
+  r.q = (int)(t0 & 1) | ((int)((t1 + 1) & 1) << 1);
+  return r;
+}
+// Applies a run to m (units 2^ue), verifying every result stays strictly inside the binade.
+__device__ __forceinline__ bool run_apply(const RunSum &r, long long &m) {
+  if (r.len == 0) return true;
+  if (r.q & 4) return false;
+  constexpr long long lo = 1LL << 52, hi = 1LL << 53;
+  if (m > 0) {
+    if (!(m + r.mn > lo && m + r.mx < hi)) return false;
+  } else {
+    if (!(m + r.mx < -lo && m + r.mn > -hi)) return false;
+  }
+  m += (m & 1) ? r.t1 : r.t0;
+  return true;
+}
+__device__ __forceinline__ long long key_m(double s, int key) {
+  return key == kKeySpecial ? 0 : (long long)ldexp(s, -(key >> 1));
+}
+
+// Serial pass of one chain over pieces [p0, p1) of a hub (one wave, lane-uniform). buf:
+// this wave's LDS buffer (a PieceSum, reused as 64 doubles by the element-wise fallback).
+// comp: 0 = fr (S), 1 = er (T); xy: the hub's (fr, er) pairs; d: its degree.
+__device__ double hub_serial_pass(const PieceSum *__restrict__ hsum, int p0, int p1, int comp,
+                                  const double2 *__restrict__ xy, int d, PieceSum *buf,
+                                  unsigned long long *__restrict__ redo) {
+  const int lane = threadIdx.x & 63;
+  double s = 0.0;
+  int key = kKeySpecial;
+  long long m = 0;
+  const int4 *src = reinterpret_cast<const int4 *>(hsum);
+  int4 *dst = reinterpret_cast<int4 *>(buf);
+  int4 w0 = make_int4(0, 0, 0, 0), w1 = w0;
+  auto fetch = [&](int p) {
+    const int4 *q = src + ((size_t)p * 2 + comp) * kPieceWords;
+    w0 = q[lane];
+    if (lane + 64 < kPieceWords) w1 = q[lane + 64];
+  };
+  if (p0 < p1) fetch(p0);
+  for (int p = p0; p < p1; ++p) {
+    wave_sync();
+    dst[lane] = w0;
+    if (lane + 64 < kPieceWords) dst[lane + 64] = w1;
+    wave_sync();
+    if (p + 1 < p1) fetch(p + 1);
+    const double s0 = s;
+    const int nb = buf->nb;
+    bool ok = nb <= kMaxBnd;
+    if (ok && buf->head.len) {
+      ok = key != kKeySpecial && key == buf->first_key && run_apply(buf->head, m);
+      if (ok) s = ldexp((double)m, key >> 1);
+    }
+    for (int j = 0; ok && j < nb; ++j) {
+      s = s + buf->b[j].x;  // the boundary step: one exact fp64 add
+      key = ulp_key(s);
+      m = key_m(s, key);
+      if (buf->b[j].run.len) {
+        ok = key != kKeySpecial && key == buf->b[j].key && run_apply(buf->b[j].run, m);
+        if (ok) s = ldexp((double)m, key >> 1);
+      }
+    }
+    if (!ok) {  // element by element from the piece start (64 at a time through LDS)
+      if (lane == 0) atomicAdd(redo, 1ull);
+      s = s0;
+      double *xs = reinterpret_cast<double *>(buf);
+      const int kb = (p - p0) * kPiece, ke = min(d, kb + kPiece);
+      for (int c0 = kb; c0 < ke; c0 += 64) {
+        const int k = c0 + lane;
+        const double2 v2 = k < ke ? xy[k] : make_double2(0.0, 0.0);
+        wave_sync();
+        xs[lane] = comp ? v2.y : v2.x;
+        wave_sync();
+        const int cn = min(64, ke - c0);
+        for (int q = 0; q < cn; ++q) s = s + xs[q];
+      }
+      key = ulp_key(s);
+      m = key_m(s, key);
+    }
+  }
+  return s;
+}
+
 template <typename T>
 __device__ inline T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);
@@ -540,7 +709,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     unsigned long long *__restrict__ err, const int *__restrict__ perm,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
-    const int *__restrict__ hrows) {
+    const int *__restrict__ hrows, const PieceSum *__restrict__ hsum, const int *__restrict__ hub_p0,
+    unsigned long long *__restrict__ hub_redo) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -716,7 +886,22 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int d = e - b;
     double S = 0.0, T = 0.0;
     constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
-    if (t < 64) {
+    if (hsum) {
+      // parallel exact sums: k_hub_sum summarised the pieces; wave 0 runs the serial pass
+      // of S, wave 1 that of T, each in its own LDS buffer
+      static_assert(2 * sizeof(PieceSum) <= sizeof(double) * TE, "LDS for the serial pass");
+      PieceSum *bufs = reinterpret_cast<PieceSum *>(s_x);
+      if (t < 128 && DIAG != 5) {
+        const double r = hub_serial_pass(hsum, hub_p0[blockIdx.x], hub_p0[blockIdx.x + 1], t >> 6, xy, d,
+                                         bufs + (t >> 6), hub_redo);
+        if ((t & 63) == 0) s_a[t >> 6] = r;
+      }
+      __syncthreads();
+      S = s_a[0];
+      T = s_a[1];
+      if (DIAG == 5) S = T = 0.0;
+      __syncthreads();
+    } else if (t < 64) {
       double2 nx[PL];
 #pragma unroll
       for (int u = 0; u < PL; ++u) nx[u] = t + 64 * u < d ? xy[t + 64 * u] : make_double2(0.0, 0.0);
@@ -1626,6 +1811,218 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
   hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
 }
 
+// Mega hubs, parallel exact sums: stage launch. One block per piece of kPiece elements of a
+// hub row ({hub, offset in hubxy, length, first edge}): (fr, er) of every edge into hubxy
+// (CA:98-99 + kernel 4's flow reconstruction, coalesced), and the piece's approximate sums
+// (any order: they only steer the speculation) into psum.
+__global__ __launch_bounds__(kBlock) void k_hub_stage_p(
+    const int4 *__restrict__ piece, const int4 *__restrict__ hubs, const int *__restrict__ col,
+    const double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
+    const void *__restrict__ code_prev, const PackCtl *__restrict__ ctl, int rslot,
+    double2 *__restrict__ hubxy, double2 *__restrict__ psum) {
+  __shared__ double2 s_w[kBlock / 64];
+  const int4 pc = piece[blockIdx.x];
+  const int t = threadIdx.x;
+  const double own2 = a_prev2[hubs[pc.x].x];
+  const PackCtl pp = ctl[rslot ^ 1];
+  int cc[kPieceT];
+  double fo[kPieceT], er[kPieceT];
+#pragma unroll
+  for (int i = 0; i < kPieceT; ++i) {
+    const int o = t + kBlock * i;
+    cc[i] = o < pc.z ? col[pc.w + o] : 0;
+    fo[i] = o < pc.z ? ld_f(F, pc.w + o) : 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < kPieceT; ++i) er[i] = t + kBlock * i < pc.z ? ld_est(pp, code_prev, a_prev, cc[i]) : 0.0;
+  double sx = 0.0, sy = 0.0;
+#pragma unroll
+  for (int i = 0; i < kPieceT; ++i) {
+    const int o = t + kBlock * i;
+    if (o < pc.z) {
+      const double fr = recon_fr(fo[i], er[i], own2);
+      hubxy[pc.y + o] = make_double2(fr, er[i]);
+      sx += fr;
+      sy += er[i];
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    sx += __shfl_down(sx, off);
+    sy += __shfl_down(sy, off);
+  }
+  if ((t & 63) == 0) s_w[t >> 6] = make_double2(sx, sy);
+  __syncthreads();
+  if (t == 0) {
+    double2 r = s_w[0];
+    for (int w = 1; w < kBlock / 64; ++w) {
+      r.x += s_w[w].x;
+      r.y += s_w[w].y;
+    }
+    psum[blockIdx.x] = r;
+  }
+}
+
+// (hasb, run) element of the reverse segmented scan over threads: the composition from a
+// thread's start up to (and including the head of) the first thread with a boundary.
+struct SegRun {
+  RunSum r;
+  int f;
+};
+__device__ __forceinline__ SegRun seg_cat(const SegRun &x, const SegRun &y) {  // x earlier
+  if (x.f) return x;
+  return SegRun{run_cat(x.r, y.r), y.f};
+}
+__device__ __forceinline__ SegRun shfl_down_seg(const SegRun &a, int off) {
+  SegRun b;
+  b.r.t0 = __shfl_down(a.r.t0, off);
+  b.r.t1 = __shfl_down(a.r.t1, off);
+  b.r.mn = __shfl_down(a.r.mn, off);
+  b.r.mx = __shfl_down(a.r.mx, off);
+  b.r.len = __shfl_down(a.r.len, off);
+  b.r.q = __shfl_down(a.r.q, off);
+  b.f = __shfl_down(a.f, off);
+  return b;
+}
+
+// Mega hubs, parallel exact sums: summary launch. One block per piece; for each chain
+// (comp 0 = fr -> S, 1 = er -> T) it writes the piece's PieceSum (see the helpers above).
+__global__ __launch_bounds__(kBlock) void k_hub_sum(const int4 *__restrict__ piece,
+                                                    const int *__restrict__ hub_p0,
+                                                    const double2 *__restrict__ psum,
+                                                    const double2 *__restrict__ hubxy,
+                                                    PieceSum *__restrict__ hsum) {
+  __shared__ double2 s_pre;
+  __shared__ double s_wd[kBlock / 64];
+  __shared__ int s_wi[kBlock / 64];
+  __shared__ SegRun s_agg[kBlock / 64];
+  __shared__ int s_lastkey[kBlock];
+  const int4 pc = piece[blockIdx.x];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (t < 64) {  // approximate sum of the hub's earlier pieces
+    double ax = 0.0, ay = 0.0;
+    for (int q = hub_p0[pc.x] + t; q < (int)blockIdx.x; q += 64) {
+      const double2 v = psum[q];
+      ax += v.x;
+      ay += v.y;
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      ax += __shfl_down(ax, off);
+      ay += __shfl_down(ay, off);
+    }
+    if (t == 0) s_pre = make_double2(ax, ay);
+  }
+  const int nv = max(0, min(kPieceT, pc.z - t * kPieceT));
+  double2 v[kPieceT];
+#pragma unroll
+  for (int i = 0; i < kPieceT; ++i) v[i] = i < nv ? hubxy[pc.y + t * kPieceT + i] : make_double2(0.0, 0.0);
+  __syncthreads();
+  for (int comp = 0; comp < 2; ++comp) {
+    PieceSum *out = hsum + (size_t)blockIdx.x * 2 + comp;
+    const double pre = comp ? s_pre.y : s_pre.x;
+    double x[kPieceT];
+#pragma unroll
+    for (int i = 0; i < kPieceT; ++i) x[i] = comp ? v[i].y : v[i].x;
+    // approximate prefix: thread sums, block exclusive scan, then in-thread order
+    double ls = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPieceT; ++i)
+      if (i < nv) ls += x[i];
+    double inc = ls;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(inc, off);
+      if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_wd[w] = inc;
+    __syncthreads();
+    double p = pre + (inc - ls);
+    for (int u = 0; u < w; ++u) p += s_wd[u];
+    int key[kPieceT];
+#pragma unroll
+    for (int i = 0; i < kPieceT; ++i) {
+      p += x[i];
+      key[i] = ulp_key(p);
+    }
+    if (nv) s_lastkey[t] = key[nv - 1];
+    __syncthreads();
+    const int key_in = t ? s_lastkey[t - 1] : ulp_key(pre);
+    // first walk: boundaries, the head run (before the thread's first boundary)
+    SegRun g{run_id(), 0};
+    int nbl = 0;
+    {
+      int prev = key_in;
+#pragma unroll
+      for (int i = 0; i < kPieceT; ++i) {
+        if (i < nv) {
+          const bool bnd = key[i] == kKeySpecial || prev == kKeySpecial || key[i] != prev;
+          if (bnd) {
+            g.f = 1;
+            ++nbl;
+          } else if (!g.f) {
+            g.r = run_cat(g.r, run_step(x[i], key[i] >> 1));
+          }
+          prev = key[i];
+        }
+      }
+    }
+    // reverse segmented scan: g = this thread's start up to the first boundary at or after it
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const SegRun y = shfl_down_seg(g, off);
+      if (lane + off < 64) g = seg_cat(g, y);
+    }
+    // boundary counts: exclusive scan
+    int ninc = nbl;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(ninc, off);
+      if (lane >= off) ninc += y;
+    }
+    if (lane == 0) s_agg[w] = g;
+    if (lane == 63) s_wi[w] = ninc;
+    __syncthreads();
+    SegRun suf{run_id(), 0};  // later waves, combined
+    for (int u = kBlock / 64 - 1; u > w; --u) suf = seg_cat(s_agg[u], suf);
+    g = seg_cat(g, suf);
+    SegRun gnext = shfl_down_seg(g, 1);  // the next thread's g (exclusive)
+    if (lane == 63) gnext = suf;
+    int jb = ninc - nbl, nbt = 0;
+    for (int u = 0; u < kBlock / 64; ++u) {
+      if (u < w) jb += s_wi[u];
+      nbt += s_wi[u];
+    }
+    if (t == 0) {
+      out->first_key = ulp_key(pre);
+      out->nb = nbt;
+      out->head = g.r;  // the piece start up to its first boundary
+    }
+    if (nbl && nbt <= kMaxBnd) {  // second walk: each boundary and the run after it
+      int prev = key_in, j = jb - 1;
+      RunSum rr = run_id();
+#pragma unroll
+      for (int i = 0; i < kPieceT; ++i) {
+        if (i < nv) {
+          const bool bnd = key[i] == kKeySpecial || prev == kKeySpecial || key[i] != prev;
+          if (bnd) {
+            if (j >= jb) out->b[j].run = rr;
+            ++j;
+            out->b[j].x = x[i];
+            out->b[j].key = key[i];
+            rr = run_id();
+          } else if (j >= jb) {
+            rr = run_cat(rr, run_step(x[i], key[i] >> 1));
+          }
+          prev = key[i];
+        }
+      }
+      out->b[j].run = run_cat(rr, gnext.r);
+    }
+    __syncthreads();  // s_wd / s_wi / s_agg / s_lastkey are reused by the next chain
+  }
+}
+
 __global__ void k_fill_split(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) st_f_full(p, (int)q, val);
@@ -2110,6 +2507,16 @@ struct fu_handle {
   int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first
   int n_hub = 0;
   int64_t hub_total = 0;
+  // parallel exact hub sums (option "hub_scan", default off: on converged R-MAT rounds the
+  // flow sums wander across binades, ~10% of their steps are boundaries, and the serial
+  // pass loses to the one-wave chain): pieces of kPiece edges
+  int hub_scan = 0;
+  int n_piece = 0;
+  int4 *hub_piece = nullptr;  // {hub, offset in hubxy, length, first edge}
+  int *hub_p0 = nullptr;      // first piece of each hub (n_hub + 1)
+  double2 *psum = nullptr;    // approximate (fr, er) sums per piece
+  PieceSum *hsum = nullptr;   // run summaries per piece and chain
+  unsigned long long *hub_redo = nullptr;  // pieces the serial pass redid element by element
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
@@ -2302,11 +2709,21 @@ int build_wave_tiles(fu_handle *h, int wg) {
 
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
-  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy})
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_piece,
+                  (void *)h->hub_p0, (void *)h->psum, (void *)h->hsum})
     if (p) hipFree(p);
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
+  h->hub_piece = nullptr;
+  h->hub_p0 = nullptr;
+  h->psum = nullptr;
+  h->hsum = nullptr;
+  h->n_piece = 0;
+  if (!h->hub_redo) {
+    if (int rc = dmalloc(&h->hub_redo, 1)) return rc;
+    HIP_TRY(hipMemset(h->hub_redo, 0, sizeof(unsigned long long)));
+  }
   std::vector<int4> rows;
   std::vector<int32_t> off;
   int64_t tot = 0;
@@ -2326,6 +2743,22 @@ int build_hubs(fu_handle *h) {
   if (int rc = dmalloc(&h->hubxy, (size_t)tot)) return rc;
   HIP_TRY(hipMemcpy(h->hub_rows, rows.data(), sizeof(int4) * rows.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->hub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
+  std::vector<int4> pcs;
+  std::vector<int32_t> p0;
+  for (size_t q = 0; q < rows.size(); ++q) {
+    p0.push_back((int32_t)pcs.size());
+    const int d = rows[q].z - rows[q].y;
+    for (int k = 0; k < d; k += kPiece)
+      pcs.push_back(make_int4((int)q, rows[q].w + k, std::min(kPiece, d - k), rows[q].y + k));
+  }
+  p0.push_back((int32_t)pcs.size());
+  h->n_piece = (int)pcs.size();
+  if (int rc = dmalloc(&h->hub_piece, pcs.size())) return rc;
+  if (int rc = dmalloc(&h->hub_p0, p0.size())) return rc;
+  if (int rc = dmalloc(&h->psum, pcs.size())) return rc;
+  if (int rc = dmalloc(&h->hsum, 2 * pcs.size())) return rc;
+  HIP_TRY(hipMemcpy(h->hub_piece, pcs.data(), sizeof(int4) * pcs.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->hub_p0, p0.data(), sizeof(int32_t) * p0.size(), hipMemcpyHostToDevice));
   return FU_OK;
 }
 
@@ -2709,11 +3142,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
       }
       if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
         hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
@@ -2747,11 +3180,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
       }
       if (h->nwtiles[wg]) {
         const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
@@ -2770,15 +3203,23 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
-      if (h->n_hub && !(h->geo == 0 && h->bins))
-        hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1],
-                           h->pctl, (int)(r & 1), h->hubxy);
+      if (h->n_hub && !(h->geo == 0 && h->bins)) {
+        if (h->hub_scan) {  // pieces: (fr, er) + approximate sums, then the run summaries
+          hipLaunchKernelGGL(k_hub_stage_p, dim3(h->n_piece), dim3(kBlock), 0, h->stream, h->hub_piece, h->hub_rows,
+                             h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->hubxy, h->psum);
+          hipLaunchKernelGGL(k_hub_sum, dim3(h->n_piece), dim3(kBlock), 0, h->stream, h->hub_piece, h->hub_p0,
+                             h->psum, h->hubxy, h->hsum);
+        } else {
+          hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream, h->n_hub,
+                             h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1],
+                             h->pctl, (int)(r & 1), h->hubxy);
+        }
+      }
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
   hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_geo[h->geo]), dim3(kBlock), 0, \
                      h->stream, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
                      h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
-                     h->hrows)
+                     h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
     if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
@@ -3107,6 +3548,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
     return FU_OK;
   }
+  if (!std::strcmp(key, "hub_scan")) {  // mega hubs: parallel exact sums (1) or one chain (0)
+    h->hub_scan = value != 0;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "wave_heavy")) {  // kernel 4: heavy rows one per wave (1) or per block (0)
     h->wave_heavy = value != 0;
     return build_tiles(h);
@@ -3386,6 +3831,16 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   info[6] = h->n_tunes;
   info[7] = h->tuned_width;
   for (int k = 0; k < 12; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  info[20] = h->n_hub;
+  info[21] = h->n_piece;
+  info[22] = 0;
+  if (h->hub_redo) {
+    if (int rc = set_device(h)) return rc;
+    unsigned long long redo = 0;
+    HIP_TRY(hipMemcpyAsync(&redo, h->hub_redo, sizeof(redo), hipMemcpyDeviceToHost, h->stream));
+    HIP_TRY(hipStreamSynchronize(h->stream));
+    info[22] = (int64_t)redo;
+  }
   return FU_OK;
 }
 
@@ -3427,7 +3882,8 @@ int fu_destroy(fu_handle *h) {
                   h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
                   h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
                   h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase,
-                  h->hub_rows, h->hub_off, h->hubxy, h->hrows};
+                  h->hub_rows, h->hub_off, h->hubxy, h->hrows, h->hub_piece, h->hub_p0, h->psum,
+                  h->hsum, h->hub_redo};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);

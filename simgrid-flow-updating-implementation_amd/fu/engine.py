@@ -113,6 +113,7 @@ class CollectAll:
                 "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
                 "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
                 "tuned_pack_width": int(a[7]),
+                "mega_hubs": int(a[20]), "hub_pieces": int(a[21]), "hub_pieces_redone": int(a[22]),
                 "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
                                       enumerate(("recon", "recon_512", "split2", "stage",
                                                  "pipe_stage"))}}

@@ -134,6 +134,181 @@ static int par_sum(const double *x, int n, int nthr, double *out, int *nseg_out)
   return 1;
 }
 
+
+// ---------------------------------------------------------------------------------------
+// v2: the GPU decomposition. Pieces of XB = 2048 elements (one block, 8 per thread) are
+// summarised independently (given the approximate sum of everything before the piece):
+// the head run (elements before the piece's first boundary), then per boundary its element
+// and the run that follows it. A run summary carries the transducer plus the min / max of
+// its partial increments, so one serial pass over pieces and boundaries both applies and
+// verifies every run in O(1).
+#define XB 2048
+#define XT 8
+#define MAXB 64
+#define SPECIAL (-100000)
+typedef struct {
+  int64_t t[2];
+  uint8_t q[2];
+  int64_t mn, mx;  // min / max partial increment over the run's results (both parities)
+  int len;
+} Run;
+typedef struct {
+  double x;
+  int ue;
+  Run run;
+} Bnd;
+typedef struct {
+  int first_ue;  // ulp exponent the head run assumes
+  Run head;
+  int nb;        // boundaries (> MAXB: dense, the serial pass walks the elements)
+  Bnd b[MAXB];
+} Piece;
+
+// speculation key of a value: ulp exponent and sign (a run keeps both); SPECIAL for 0,
+// subnormals, inf, nan
+static int ulp_key(double x) {
+  uint64_t bits;
+  memcpy(&bits, &x, 8);
+  const int E = (int)((bits >> 52) & 0x7ff);
+  if (E == 0 || E == 0x7ff) return SPECIAL;
+  return ((E - 1075) << 1) | (int)(bits >> 63);
+}
+static int key_ue(int key) { return key >> 1; }
+static Run run_id(void) {
+  Run r = {{0, 0}, {0, 1}, INT64_MAX, INT64_MIN, 0};
+  return r;
+}
+static Run run_push(Run a, Tr st) {  // a then one step
+  Run r;
+  for (int p = 0; p < 2; ++p) {
+    r.t[p] = a.t[p] + st.t[a.q[p]];
+    r.q[p] = st.q[a.q[p]];
+  }
+  r.mn = a.mn;
+  r.mx = a.mx;
+  for (int p = 0; p < 2; ++p) {
+    if (r.t[p] < r.mn) r.mn = r.t[p];
+    if (r.t[p] > r.mx) r.mx = r.t[p];
+  }
+  r.len = a.len + 1;
+  return r;
+}
+// apply a run to M (units 2^ue, M != 0), verifying every result stays strictly inside the binade
+static int run_apply(const Run *r, int64_t *M) {
+  if (r->len == 0) return 1;
+  const int64_t lo = 1LL << 52, hi = 1LL << 53, m = *M;
+  if (m > 0) {
+    if (!(m + r->mn > lo && m + r->mx < hi)) return 0;
+  } else {
+    if (!(m + r->mx < -lo && m + r->mn > -hi)) return 0;
+  }
+  *M = m + r->t[m & 1];
+  return 1;
+}
+
+static void summarise(const double *x, int n, double pre, Piece *P) {
+  // approximate prefix as the block does it: thread sums, exclusive scan, then in-thread
+  double ts[XB / XT + 1];
+  ts[0] = pre;
+  for (int t = 0; t < XB / XT; ++t) {
+    double s = 0;
+    for (int i = 0; i < XT; ++i) {
+      const int k = t * XT + i;
+      if (k < n) s += x[k];
+    }
+    ts[t + 1] = ts[t] + s;
+  }
+  P->first_ue = ulp_key(pre);
+  P->head = run_id();
+  P->nb = 0;
+  int prev = P->first_ue, in_head = 1, bad = 0;
+  Run *cur = &P->head;
+  for (int t = 0; t < XB / XT; ++t) {
+    double p = ts[t];
+    for (int i = 0; i < XT; ++i) {
+      const int k = t * XT + i;
+      if (k >= n) break;
+      p += x[k];
+      const int ue = ulp_key(p);
+      if (ue == SPECIAL || ue != prev || prev == SPECIAL) {
+        in_head = 0;
+        if (P->nb < MAXB) {
+          P->b[P->nb].x = x[k];
+          P->b[P->nb].ue = ue;
+          P->b[P->nb].run = run_id();
+          cur = &P->b[P->nb].run;
+        } else {
+          cur = NULL;
+        }
+        P->nb++;
+      } else if (cur) {
+        Tr st = tr_step(x[k], key_ue(ue), &bad);
+        *cur = run_push(*cur, st);
+        if (bad) cur->mn = INT64_MIN;  // forces the verification to fail
+      }
+      prev = ue;
+    }
+  }
+  (void)in_head;
+}
+
+// serial pass over the pieces of a row; returns 0 when verification fails (fallback)
+static long why[8];
+static int serial_pass(const double *x, int n, const Piece *Ps, int np, double *out) {
+  double s = 0.0;
+  int uec = SPECIAL;  // actual ulp exponent of s
+  int64_t M = 0;
+  for (int q = 0; q < np; ++q) {
+    const Piece *P = &Ps[q];
+    const int pb = q * XB, pn = n - pb < XB ? n - pb : XB;
+    if (P->nb > MAXB) {  // dense piece: element by element
+      for (int k = 0; k < pn; ++k) s = s + x[pb + k];
+      uec = ulp_key(s);
+      if (uec != SPECIAL) M = (int64_t)ldexp(s, -key_ue(uec));
+      continue;
+    }
+    if (P->head.len) {
+      if (uec == SPECIAL || uec != P->first_ue) { why[0]++; return 0; }
+      if (!run_apply(&P->head, &M)) { why[1]++; return 0; }
+      s = ldexp((double)M, key_ue(uec));
+    }
+    for (int j = 0; j < P->nb; ++j) {
+      s = s + P->b[j].x;
+      uec = ulp_key(s);
+      if (P->b[j].run.len) {
+        if (uec == SPECIAL || uec != P->b[j].ue) { why[2 + (uec == SPECIAL)]++; return 0; }
+        M = (int64_t)ldexp(s, -key_ue(uec));
+        if (!run_apply(&P->b[j].run, &M)) {
+          if (why[4] < 3) printf("fail piece %d bnd %d/%d M %lld mn %lld mx %lld len %d t %lld %lld ue %d x %g\n", q, j, P->nb, (long long)M, (long long)P->b[j].run.mn, (long long)P->b[j].run.mx, P->b[j].run.len, (long long)P->b[j].run.t[0], (long long)P->b[j].run.t[1], uec, P->b[j].x);
+          why[4]++; return 0; }
+        s = ldexp((double)M, key_ue(uec));
+      } else if (uec != SPECIAL) {
+        M = (int64_t)ldexp(s, -key_ue(uec));
+      }
+    }
+  }
+  *out = s;
+  return 1;
+}
+
+static int par_sum2(const double *x, int n, double *out, int *nbnd) {
+  const int np = (n + XB - 1) / XB;
+  Piece *Ps = malloc(sizeof(Piece) * (np ? np : 1));
+  double pre = 0.0;
+  *nbnd = 0;
+  for (int q = 0; q < np; ++q) {  // piece sums are approximate: any order will do
+    const int pb = q * XB, pn = n - pb < XB ? n - pb : XB;
+    summarise(x + pb, pn, pre, &Ps[q]);
+    *nbnd += Ps[q].nb;
+    double ps = 0;
+    for (int k = 0; k < pn; ++k) ps += x[pb + k];
+    pre += ps;
+  }
+  const int ok = serial_pass(x, n, Ps, np, out);
+  free(Ps);
+  return ok;
+}
+
 static uint64_t rs = 88172645463325252ull;
 static double urand(void) {
   rs ^= rs << 13;
@@ -142,9 +317,40 @@ static double urand(void) {
   return (double)(rs >> 11) * 0x1p-53;
 }
 
-int main(void) {
+static int from_file(const char *path) {  // raw doubles: chain sequences to test
+  FILE *f = fopen(path, "rb");
+  if (!f) return 2;
+  fseek(f, 0, SEEK_END);
+  const long n = ftell(f) / 8;
+  fseek(f, 0, SEEK_SET);
+  double *x = malloc(8 * n);
+  if (fread(x, 8, n, f) != (size_t)n) return 2;
+  fclose(f);
+  double got, ref = seq_sum(x, (int)n);
+  int nb;
+  memset(why, 0, sizeof(why));
+  const int ok = par_sum2(x, (int)n, &got, &nb);
+  printf("n %ld boundaries %d ok %d same %d why %ld %ld %ld %ld %ld\n", n, nb, ok, ok && memcmp(&got, &ref, 8) == 0,
+         why[0], why[1], why[2], why[3], why[4]);
+  const int np = (int)((n + XB - 1) / XB);
+  int dense = 0;
+  double pre = 0.0;
+  for (int q = 0; q < np; ++q) {
+    Piece P;
+    const int pn = n - q * XB < XB ? (int)(n - q * XB) : XB;
+    summarise(x + q * XB, pn, pre, &P);
+    if (P.nb > MAXB) ++dense;
+    for (int k = 0; k < pn; ++k) pre += x[q * XB + k];
+  }
+  printf("pieces %d dense %d\n", np, dense);
+  free(x);
+  return 0;
+}
+
+int main(int argc, char **argv) {
+  if (argc > 1) return from_file(argv[1]);
   const int sizes[] = {1, 2, 3, 7, 64, 100, 1000, 4097, 65536, 400000};
-  long trials = 0, fallbacks = 0, wrong = 0, fb_mode[7] = {0};
+  long trials = 0, fallbacks = 0, wrong = 0, fb_mode[7] = {0}, fb2[7] = {0}, wrong2 = 0;
   for (int mode = 0; mode < 7; ++mode) {
     for (int si = 0; si < 10; ++si) {
       const int n = sizes[si];
@@ -168,6 +374,16 @@ int main(void) {
         double got;
         int nseg;
         ++trials;
+        {
+          double g2;
+          int nb2;
+          if (!par_sum2(x, n, &g2, &nb2)) {
+            ++fb2[mode];
+          } else if (memcmp(&g2, &ref, 8) != 0) {
+            ++wrong2;
+            if (wrong2 < 10) printf("WRONG2 mode %d n %d: %.17g vs %.17g\n", mode, n, g2, ref);
+          }
+        }
         if (!par_sum(x, n, 256, &got, &nseg)) {
           ++fallbacks;
           ++fb_mode[mode];
@@ -182,7 +398,8 @@ int main(void) {
       free(x);
     }
   }
-  for (int m = 0; m < 7; ++m) printf("mode %d fallbacks %ld\n", m, fb_mode[m]);
+  for (int m = 0; m < 7; ++m) printf("mode %d fallbacks %ld (v2 %ld)\n", m, fb_mode[m], fb2[m]);
+  printf("v2 wrong %ld why %ld %ld %ld %ld %ld\n", wrong2, why[0], why[1], why[2], why[3], why[4]);
   printf("trials %ld fallbacks %ld wrong %ld\n", trials, fallbacks, wrong);
-  return wrong != 0;
+  return wrong != 0 || wrong2 != 0;
 }

@@ -70,6 +70,11 @@ VARIANTS = {
     "auto_deg": ("auto", {"layout": "degree"}),
     "auto": ("auto", {}),
     "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
+    "recon_noscan": ("recon", {"hub_scan": 0}),
+    "recon_mega4096": ("recon", {"mega_hub": 4096}),
+    "recon_mega2048": ("recon", {"mega_hub": 2048}),
+    "recon_mega1024": ("recon", {"mega_hub": 1024}),
+    "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -102,7 +107,8 @@ for spec in specs:
         med = sorted(ts)[len(ts) // 2]
         out[k] = {"us_per_round_med": med, "us_min": min(ts),
                   "alg_GBs": alg / (med * 1e-6) / 1e9, "edge_updates_per_s": g.E / (med * 1e-6),
-                  "pack": engs[k].pack_widths()}
+                  "pack": engs[k].pack_widths(),
+                  "hub": [engs[k].info()[x] for x in ("mega_hubs", "hub_pieces", "hub_pieces_redone")]}
     print(json.dumps(out), flush=True)
     for e in engs.values():
         e.close()
