@@ -41,7 +41,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=1000, help="timed rounds")
-    ap.add_argument("--warmup", type=int, default=60, help="untimed rounds first (autotune)")
+    ap.add_argument("--warmup", type=int, default=400,
+                    help="untimed rounds first: the autotuner times the candidate kernels at every "
+                         "packing width the run reaches (0, 32, 16, 8 bits), then fu_reset")
     ap.add_argument("--n", type=int, default=1_000_000)
     ap.add_argument("--m", type=int, default=4_000_000)
     ap.add_argument("--workload", default="er", choices=["er", "rgg", "rmat", "rr", "rgg-dist"],
@@ -126,7 +128,11 @@ def main():
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel, layout=layout)
     if args.tile_edges:
         eng.set_option("tile_edges", args.tile_edges)
-    eng.run(args.warmup)  # with kernel "auto" the first warmup rounds also pick the kernel
+    # with kernel "auto" the warmup rounds also pick the kernel for each packing width; run in
+    # chunks so the host sees each plan's width (an asynchronous copy) while the rounds run
+    for w0 in range(0, args.warmup, 50):
+        eng.run(min(50, args.warmup - w0))
+        eng.synchronize()
     eng.reset()           # the timed region is rounds 0 .. steps-1 from the zero state
     eng.synchronize()
 
@@ -213,6 +219,7 @@ def main():
                 "tile_selected": kinfo["tile"],
                 "autotune_passes": kinfo["tune_passes"],
                 "autotune_us_per_round": kinfo["tune_us_per_round"],
+                "autotune_winner_by_width": kinfo["tune_winner_by_width"],
                 "phases": phases,
                 "parallelism": "independent graph per GPU" if world > 1 else "single GPU",
             },

@@ -144,7 +144,8 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done);
  * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
  * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run), [20] = mega hubs, [21] = their
  * pieces, [22] = pieces the exact-sum serial pass redid element by element (cumulative;
- * synchronises). With kernel
+ * synchronises), [23..26] = the autotune winner per packing width 0, 8, 16, 32 (kernel * 10 +
+ * kernel-4 geometry index, -1 = not tuned yet). With kernel
  * "auto" (the default) a fu_run_collectall(_timed) with >= 45 rounds left after round 0
  * times the candidates on real rounds (they share state and are bitwise identical) and keeps
  * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */

@@ -2472,6 +2472,7 @@ struct fu_handle {
   int tune_out[12] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
   int tuned_width = 0;    // packing width the last pass ran under
+  int tune_cache[4] = {-1, -1, -1, -1};  // winner per packing width (0, 8, 16, 32), kept across fu_reset
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
   hipEvent_t ev_pw = nullptr;
   bool pw_pending = false;
@@ -3303,6 +3304,29 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   return FU_OK;
 }
 
+struct TuneCand {
+  int kernel, nt, geo;
+};
+// kernel 7 (wave tiles) is not a candidate: slower than kernel 4 at 512x64 everywhere
+// measured; it stays selectable as an option
+// measured on ER-1M / R-MAT: 4+nt, 4 at 1024x256, 5 and 9 never win; they stay options
+static std::vector<TuneCand> tune_cands(const fu_handle *h) {
+  std::vector<TuneCand> cands = {{4, 0, 0}, {4, 0, 3}};
+  if (!h->dist) {
+    cands.push_back({6, 0, 0});
+    cands.push_back({8, 0, 0});
+    cands.push_back({10, 0, 0});
+  }
+  return cands;
+}
+static int width_class(int w) { return w == 8 ? 1 : w == 16 ? 2 : w == 32 ? 3 : 0; }
+static void use_cand(fu_handle *h, const TuneCand &c) {
+  h->kernel = c.kernel;
+  h->nt = c.nt;
+  if (h->kernel == 7) h->wgeo = c.geo;
+  else h->geo = c.geo;
+}
+
 int set_device(fu_handle *h) {
   HIP_TRY(hipSetDevice(h->device));
   return FU_OK;
@@ -3578,6 +3602,10 @@ int fu_reset(fu_handle *h) {
   h->pw_pending = false;  // the stream is idle: no plan copy in flight
   *h->h_pw = 0;           // round 0 clears the packing plan
   h->seen_width = 0;
+  if (h->autotune && h->tuned && h->tune_cache[0] >= 0) {  // unpacked again: its winner
+    use_cand(h, tune_cands(h)[h->tune_cache[0]]);
+    h->tuned_width = 0;
+  }
   return FU_OK;
 }
 
@@ -3614,19 +3642,10 @@ int fu__err_slots(fu_handle *h, int count) {
 // packed gather shifts the balance between the candidates), at most kMaxTunes times.
 constexpr int kMaxTunes = 4;
 
-static int autotune_kernel(fu_handle *h, int32_t *budget) {
-  struct Cand {
-    int kernel, nt, geo;
-  };
-  // kernel 7 (wave tiles) is not a candidate: slower than kernel 4 at 512x64 everywhere
-  // measured; it stays selectable as an option
-  // measured on ER-1M / R-MAT: 4+nt, 4 at 1024x256, 5 and 9 never win; they stay options
-  std::vector<Cand> cands = {{4, 0, 0}, {4, 0, 3}};
-  if (!h->dist) {
-    cands.push_back({6, 0, 0});
-    cands.push_back({8, 0, 0});
-    cands.push_back({10, 0, 0});
-  }
+// width: the packing width the pass runs under (kernel 6 writes unpacked tables, so it is
+// only a candidate while the table is unpacked)
+static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
+  const std::vector<TuneCand> cands = tune_cands(h);
   constexpr int kTimed = 8;
   const int32_t need = (1 + kTimed) * (int32_t)cands.size();
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
@@ -3637,6 +3656,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
     // ones (its last ns per round stays reported)
     if (h->tune_out[c] >= 2) continue;
     h->tune_ms[c] = 0.f;
+    if (cands[c].kernel == 6 && width != 0) continue;
     if (cands[c].kernel == 9) {
       if (ensure_light(h) != FU_OK) {
         set_error("");
@@ -3675,10 +3695,8 @@ static int autotune_kernel(fu_handle *h, int32_t *budget) {
   if (bi < 0) return fail(FU_ERR_STATE, "autotune: no candidate ran");
   for (size_t c = 0; c < cands.size(); ++c)
     if (h->tune_ms[c] > 1.3f * h->tune_ms[bi]) h->tune_out[c]++;
-  h->kernel = cands[bi].kernel;
-  h->nt = cands[bi].nt;
-  if (h->kernel == 7) h->wgeo = cands[bi].geo;
-  else h->geo = cands[bi].geo;
+  use_cand(h, cands[bi]);
+  h->tune_cache[width_class(width)] = bi;
   h->tuned = true;
   h->n_tunes++;
   return FU_OK;
@@ -3690,7 +3708,14 @@ static void poll_pack_width(fu_handle *h) {
   if (!h->pw_pending || hipEventQuery(h->ev_pw) != hipSuccess) return;
   h->pw_pending = false;
   h->seen_width = *h->h_pw;
-  if (h->autotune && h->tuned && *h->h_pw != h->tuned_width && h->n_tunes < kMaxTunes) h->tuned = false;
+  if (!h->autotune || !h->tuned || *h->h_pw == h->tuned_width) return;
+  const int cached = h->tune_cache[width_class(*h->h_pw)];
+  if (cached >= 0) {  // this width was tuned before (e.g. before fu_reset): reuse its winner
+    use_cand(h, tune_cands(h)[cached]);
+    h->tuned_width = *h->h_pw;
+  } else if (h->n_tunes < kMaxTunes) {
+    h->tuned = false;
+  }
 }
 
 // The round loop shared by fu_run_collectall and fu_run_collectall_timed.
@@ -3701,7 +3726,7 @@ static int run_rounds(fu_handle *h, int32_t rounds, int32_t err_every, int nerr)
     if (h->autotune && !h->tuned && h->kernel >= 4 && h->rounds >= 1 && nerr == 0) {
       int32_t budget = rounds - r;
       const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
-      if (int rc = autotune_kernel(h, &budget)) return rc;
+      if (int rc = autotune_kernel(h, &budget, w)) return rc;
       if (h->tuned) h->tuned_width = w;
       r = rounds - budget;
       if (r >= rounds) break;
@@ -3831,6 +3856,11 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   info[6] = h->n_tunes;
   info[7] = h->tuned_width;
   for (int k = 0; k < 12; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  {  // autotune winner per packing width 0, 8, 16, 32 (kernel * 10 + geometry; -1 = none)
+    const std::vector<TuneCand> cands = tune_cands(h);
+    for (int k = 0; k < 4; ++k)
+      info[23 + k] = h->tune_cache[k] < 0 ? -1 : cands[h->tune_cache[k]].kernel * 10 + cands[h->tune_cache[k]].geo;
+  }
   info[20] = h->n_hub;
   info[21] = h->n_piece;
   info[22] = 0;

@@ -22,6 +22,12 @@ LAYOUTS = {"given": 0, "degree": 1}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
+def _cand_name(code: int) -> str:
+    kernel, geo = divmod(code, 10)
+    names = {4: "recon", 6: "split2", 8: "stage", 10: "pipe_stage"}
+    return names.get(kernel, str(kernel)) + ("_512" if kernel == 4 and geo == 3 else "")
+
+
 class CollectAll:
     """Synchronous collect-all engine on one GPU.
 
@@ -114,6 +120,8 @@ class CollectAll:
                 "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
                 "tuned_pack_width": int(a[7]),
                 "mega_hubs": int(a[20]), "hub_pieces": int(a[21]), "hub_pieces_redone": int(a[22]),
+                "tune_winner_by_width": {w: _cand_name(int(a[23 + k])) for k, w in
+                                         enumerate((0, 8, 16, 32)) if a[23 + k] >= 0},
                 "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
                                       enumerate(("recon", "recon_512", "split2", "stage",
                                                  "pipe_stage"))}}

@@ -296,6 +296,31 @@ def test_autotune_switches_kernels_bitwise():
     assert np.array_equal(eng.flows(), f_ref)
 
 
+def test_autotune_width_cache_across_reset_bitwise():
+    """The autotuner re-times the candidates when the packing width changes, keeps each
+    width's winner, and after fu_reset reuses them (no new pass); the kernel switches at
+    every width change must leave the bits untouched."""
+    g = fu.Graph.erdos_renyi(200_000, 800_000, seed=12)
+    v = fu.uniform_values(g.n, seed=12)
+    eng = fu.CollectAll(g, v)
+    eng.set_option("pack_every", 4)
+    for _ in range(8):  # the host sees each plan's width once the stream has passed it
+        eng.run(50)
+        eng.synchronize()
+    passes = eng.info()["tune_passes"]
+    assert passes >= 3
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 400, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    eng.reset()
+    for _ in range(8):
+        eng.run(50)
+        eng.synchronize()
+    assert eng.info()["tune_passes"] == passes
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
 def _er_with_outlier_pairs(n, m, pairs, seed):
     """ER(n, m) plus `pairs` disjoint 2-node components whose values are far from the giant
     component's mean: their estimates never enter the packed window, so every gather of

@@ -1,6 +1,6 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_hub_scan.py tests/test_relabel.py -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_hub.log 2>&1
+timeout -k 10 300 python -u tools/sweep.py --variants=stage_nopack,stage,stage_pe64 --warm=20 --timed=20 --reps=3 > gpurun_out/sweep_c.log 2>&1
 echo rc=$?
-tail -14 gpurun_out/pytest_hub.log
+python3 tools/show_sweep.py gpurun_out/sweep_c.log

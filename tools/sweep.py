@@ -54,6 +54,7 @@ VARIANTS = {
     "diag4_stage": ("stage", {"diag": 4}),
     "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
     "pipe_nopack": ("pipe", {"pack": 0}),
+    "stage_pe64": ("stage", {"pack_every": 64}),
     "pipe_stage": ("pipe_stage", {}),
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
     "pipe_b2": ("pipe", {"pipe_bpc": 2}),
@@ -71,6 +72,9 @@ VARIANTS = {
     "auto": ("auto", {}),
     "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
     "recon_noscan": ("recon", {"hub_scan": 0}),
+    "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
+    "pipe_nopack": ("pipe", {"pack": 0}),
+    "stage_pe64": ("stage", {"pack_every": 64}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
     "recon_mega2048": ("recon", {"mega_hub": 2048}),
     "recon_mega1024": ("recon", {"mega_hub": 1024}),
@@ -82,6 +86,10 @@ opts = [a for a in sys.argv[1:] if a.startswith("--variants=")]
 names = opts[0].split("=", 1)[1].split(",") if opts else list(VARIANTS)
 warm = [int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--warm=")]
 warm = warm[0] if warm else 10  # rounds before timing (packing engages after ~100-300)
+timed = [int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--timed=")]
+timed = timed[0] if timed else 200  # rounds per timed repetition
+reps = [int(a.split("=", 1)[1]) for a in sys.argv[1:] if a.startswith("--reps=")]
+reps = reps[0] if reps else 5
 specs = args or ["er:n=1000000,m=4000000"]
 for spec in specs:
     g = fu.Graph.from_spec(spec, seed=1)
@@ -98,9 +106,9 @@ for spec in specs:
             e.set_option("diag", o["diag"])
         engs[nm] = e
     res = {k: [] for k in engs}
-    for rep in range(5):
+    for rep in range(reps):
         for k, e in engs.items():
-            res[k].append(e.run_timed(200) / 200 * 1e3)
+            res[k].append(e.run_timed(timed) / timed * 1e3)
     alg = 24 * g.E + 28 * g.n
     out = {"spec": spec, "n": g.n, "E": g.E, "max_deg": g.max_deg, "warm": warm}
     for k, ts in res.items():
