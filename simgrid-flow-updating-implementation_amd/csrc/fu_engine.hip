@@ -700,7 +700,7 @@ __device__ inline T ld_stream(const T *p) {
 //   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
 //   5 = hub chains skipped (prices the exact sequential hub sums);
 //   12 = 1 and 2 together (prices col + the per-node arrays alone).
-template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes>
+template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
 
-  if constexpr (TE == kTileEdges && TN == kTileNodes) {
+  if constexpr (PART != 1 && TE == kTileEdges && TN == kTileNodes) {
   if (tl.y == -2) {
     // ---------------- degree bin: R rows of similar degree, one chain per row ----------
     // Rows perm[tl.x .. tl.x + R) (sorted by degree, longest first). Each iteration stages
@@ -811,6 +811,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   }
   }  // if constexpr (default geometry)
 
+  if constexpr (PART != 1) {  // heavy tiles (PART 1: light tiles only, 64 VGPRs)
   if (tl.y == -4) {
     // ---------------- heavy rows, one per wave ----------------
     // Rows hrows[tl.x .. tl.x + tl.z) (degree > hub_threshold, <= mega_hub, sorted by
@@ -987,6 +988,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (CHECK) block_max_to(eb, err);
     return;
   }
+  }  // PART != 1
+  if constexpr (PART != 2) {  // light tiles
 
   // ---------------- light tile ----------------
   // Every global load of the tile is issued up front with no dependence on an earlier load
@@ -1079,6 +1082,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     }
   }
   if (CHECK) block_max_to(eb, err);
+  }  // PART != 2
 }
 
 // ------------------------------------------------------------------------------------
@@ -2492,6 +2496,10 @@ struct fu_handle {
   // nodes); all four are built up front so autotuning can switch geometry between rounds
   int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
   int ntiles_geo[4] = {0, 0, 0, 0};
+  int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles (hubs, heavy rows, bins)
+  int fork_heavy = 1;                 // option "fork_heavy": heavy tiles on stream2, concurrently
+  hipStream_t stream2 = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   int geo = 0;
   // kernel 7 (wave tiles): per wave geometry (0 = 256 edges x 32 nodes, 1 = 512 x 64) the
   // light wave tiles and the heavy rows (kernel 4 heavy-path tiles) of that geometry
@@ -2568,7 +2576,7 @@ namespace {
 
 
 int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
-                     std::vector<int4> *host_out = nullptr, bool mega = false) {
+                     std::vector<int4> *host_out = nullptr, bool mega = false, int *nheavy = nullptr) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -2611,6 +2619,7 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
   } else {
     all.insert(all.end(), heavy.begin(), heavy.end());
   }
+  if (nheavy) *nheavy = (int)all.size();
   all.insert(all.end(), light.begin(), light.end());
   if (host_out) *host_out = all;
   if (*dst) hipFree(*dst);
@@ -2658,6 +2667,7 @@ int build_tiles_binned(fu_handle *h) {
   h->tiles_geo[0] = nullptr;
   h->perm = nullptr;
   h->ntiles_geo[0] = (int)all.size();
+  h->nheavy_geo[0] = (int)(all.size() - light.size());
   if (int rc = dmalloc(&h->tiles_geo[0], all.size())) return rc;
   if (int rc = dmalloc(&h->perm, std::max<size_t>(1, heavy.size()))) return rc;
   HIP_TRY(hipMemcpy(h->tiles_geo[0], all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
@@ -2773,7 +2783,8 @@ int build_tiles(fu_handle *h) {
       if (int rc = build_tiles_binned(h)) return rc;
       continue;
     }
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], nullptr, true))
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], nullptr, true,
+                                  &h->nheavy_geo[g]))
       return rc;
   }
   if (h->hrows) hipFree(h->hrows);
@@ -3204,23 +3215,41 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       double *F = h->f[r & 1];
       const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
       double *an = h->a[r % 3];
+      // heavy tiles (hubs, heavy rows, bins) lead the tile list: they run as their own launch
+      // on the side stream, concurrently with the light tiles' launch (which then keeps
+      // kernel 4's light-path register budget: 64 VGPRs, 8 waves per SIMD)
+      const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
+      const bool fork = nh > 0 && h->fork_heavy;
+      hipStream_t hs = fork ? h->stream2 : h->stream;
+      if (fork) {
+        HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+      }
       if (h->n_hub && !(h->geo == 0 && h->bins)) {
         if (h->hub_scan) {  // pieces: (fr, er) + approximate sums, then the run summaries
-          hipLaunchKernelGGL(k_hub_stage_p, dim3(h->n_piece), dim3(kBlock), 0, h->stream, h->hub_piece, h->hub_rows,
+          hipLaunchKernelGGL(k_hub_stage_p, dim3(h->n_piece), dim3(kBlock), 0, hs, h->hub_piece, h->hub_rows,
                              h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->hubxy, h->psum);
-          hipLaunchKernelGGL(k_hub_sum, dim3(h->n_piece), dim3(kBlock), 0, h->stream, h->hub_piece, h->hub_p0,
+          hipLaunchKernelGGL(k_hub_sum, dim3(h->n_piece), dim3(kBlock), 0, hs, h->hub_piece, h->hub_p0,
                              h->psum, h->hubxy, h->hsum);
         } else {
-          hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream, h->n_hub,
+          hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub,
                              h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1],
                              h->pctl, (int)(r & 1), h->hubxy);
         }
       }
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
-  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN>), dim3(h->ntiles_geo[h->geo]), dim3(kBlock), 0, \
-                     h->stream, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
-                     h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo)
+  do {                                                                                      \
+    if (nh)                                                                                 \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 ? 5 : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, hs, \
+                         h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
+                         h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo);   \
+    if (nl)                                                                                 \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl), dim3(kBlock), 0, h->stream, \
+                         h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
+                         h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, \
+                         nullptr, nullptr, nullptr, nullptr);                                \
+  } while (0)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
     if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
@@ -3241,6 +3270,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       }
 #undef FU_RECON
 #undef FU_RECON_G
+      if (fork) {
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+      }
     }
   } else if (h->rounds == 0) {
     if (h->kernel == 3) {
@@ -3387,14 +3421,18 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   int rc = FU_OK;
   auto cleanup = [&](int code) { fu_destroy(h); return code; };
   if ((rc = set_device(h))) return cleanup(rc);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
   {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) h->n_cu = cus;
   }
   if (hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess ||
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
@@ -3570,6 +3608,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     if (value != 0 && value != 128 && value != 256) return fail(FU_ERR_ARG, "fu_set_option: tile_nodes must be 0, 128 or 256");
     h->tile_nodes = (int)value;
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "fork_heavy")) {  // kernel 4: heavy tiles on a side stream (1) or in order (0)
+    h->fork_heavy = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "hub_scan")) {  // mega hubs: parallel exact sums (1) or one chain (0)
@@ -3921,8 +3963,11 @@ int fu_destroy(fu_handle *h) {
   if (h->ev2) hipEventDestroy(h->ev2);
   if (h->ev3) hipEventDestroy(h->ev3);
   if (h->ev_pw) hipEventDestroy(h->ev_pw);
+  if (h->ev_fork) hipEventDestroy(h->ev_fork);
+  if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
+  if (h->stream2) hipStreamDestroy(h->stream2);
   delete h;
   return FU_OK;
 }

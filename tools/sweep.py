@@ -55,6 +55,7 @@ VARIANTS = {
     "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
     "pipe_nopack": ("pipe", {"pack": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
+    "recon_nofork": ("recon", {"fork_heavy": 0}),
     "pipe_stage": ("pipe_stage", {}),
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
     "pipe_b2": ("pipe", {"pipe_bpc": 2}),
@@ -75,6 +76,7 @@ VARIANTS = {
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
     "pipe_nopack": ("pipe", {"pack": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
+    "recon_nofork": ("recon", {"fork_heavy": 0}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
     "recon_mega2048": ("recon", {"mega_hub": 2048}),
     "recon_mega1024": ("recon", {"mega_hub": 1024}),
