@@ -492,32 +492,36 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Exact left-to-right chains S += xs[q], T += es[q] over q = 0 .. cn-1 (one wave, lane-
-// uniform). The LDS reads of the next 8 elements are issued before the 16 dependent adds of
-// the current 8, so the chain runs at the fp64 add latency instead of add + LDS latency.
+// Exact left-to-right chains S += xs[q], T += es[q] over q = 0 .. cn-1 (one whole wave;
+// S and T lane-uniform in and out). Even lanes run the S chain, odd lanes the T chain, so
+// one fp64 add per element advances both sums: a wave64 v_add_f64 occupies the SIMD for the
+// same cycles whatever the EXEC mask, and two separate chains cost two. The LDS reads of
+// the next 8 elements are issued before the dependent adds of the current 8.
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
   constexpr int B = 8;
+  const bool odd = threadIdx.x & 1;
+  const double *src = odd ? es : xs;
+  double acc = odd ? T : S;
   int q = 0;
   if (cn >= B) {
-    double a[B], b[B];
+    double a[B];
 #pragma unroll
-    for (int k = 0; k < B; ++k) { a[k] = xs[k]; b[k] = es[k]; }
+    for (int k = 0; k < B; ++k) a[k] = src[k];
     for (q = B; q + B <= cn; q += B) {
-      double a2[B], b2[B];
+      double a2[B];
 #pragma unroll
-      for (int k = 0; k < B; ++k) { a2[k] = xs[q + k]; b2[k] = es[q + k]; }
+      for (int k = 0; k < B; ++k) a2[k] = src[q + k];
 #pragma unroll
-      for (int k = 0; k < B; ++k) { S = S + a[k]; T = T + b[k]; }
+      for (int k = 0; k < B; ++k) acc = acc + a[k];
 #pragma unroll
-      for (int k = 0; k < B; ++k) { a[k] = a2[k]; b[k] = b2[k]; }
+      for (int k = 0; k < B; ++k) a[k] = a2[k];
     }
 #pragma unroll
-    for (int k = 0; k < B; ++k) { S = S + a[k]; T = T + b[k]; }
+    for (int k = 0; k < B; ++k) acc = acc + a[k];
   }
-  for (; q < cn; ++q) {
-    S = S + xs[q];
-    T = T + es[q];
-  }
+  for (; q < cn; ++q) acc = acc + src[q];
+  S = __shfl(acc, 0);
+  T = __shfl(acc, 1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -710,7 +714,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
     const int *__restrict__ hrows, const PieceSum *__restrict__ hsum, const int *__restrict__ hub_p0,
-    unsigned long long *__restrict__ hub_redo) {
+    unsigned long long *__restrict__ hub_redo, int hub_sep) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -827,16 +831,15 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const double own2 = a_prev2[i];
       double *xs = s_x + w * CH, *es = s_er + w * CH;
       double S = 0.0, T = 0.0;
+      double fo[PL], er[PL];  // the last chunk's operands (a one-chunk row writes its flows from them)
       for (int c0 = 0; c0 < d; c0 += CH) {
         int cc[PL];
-        double fo[PL];
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
           const int k = c0 + lane + 64 * u;
           cc[u] = k < d ? col[b + k] : 0;
           fo[u] = k < d ? ld_f(F, b + k) : 0.0;
         }
-        double er[PL];
 #pragma unroll
         for (int u = 0; u < PL; ++u) er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
         wave_sync();  // the previous chunk's chain is done with the buffer
@@ -854,6 +857,13 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         if (pc.width) put_code(pc, code_new, i, a);
         if (CHECK) eb = err_bits(a, target[i]);
       }
+      if (d <= CH) {  // flows (CA:117-118) from the registers that staged the row
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int k = lane + 64 * u;
+          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
+        }
+      } else
       for (int k0 = 0; k0 < d; k0 += 4 * 64) {  // flows (CA:117-118), 4 loads in flight per lane
         int cc[4];
         double fo[4], er[4];
@@ -931,12 +941,14 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
-    __syncthreads();
-    const double a = s_a[0];
-    for (int k = t; k < d; k += kBlock) {
-      const double2 p2 = xy[k];
-      const double fo = ld_f(F, b + k);
-      st_f(F, b + k, (p2.x + a) - p2.y, fo);
+    if (!hub_sep) {  // else k_hub_flows writes the row's flows with many blocks
+      __syncthreads();
+      const double a = s_a[0];
+      for (int k = t; k < d; k += kBlock) {
+        const double2 p2 = xy[k];
+        const double fo = ld_f(F, b + k);
+        st_f(F, b + k, (p2.x + a) - p2.y, fo);
+      }
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -2025,6 +2037,26 @@ __global__ __launch_bounds__(kBlock) void k_hub_sum(const int4 *__restrict__ pie
     }
     __syncthreads();  // s_wd / s_wi / s_agg / s_lastkey are reused by the next chain
   }
+}
+
+// Mega hubs: the flows of every hub edge (CA:117-118) once the hub blocks have written a_r,
+// with many blocks (the hub block's own loop would hold one CU for d / 256 iterations on
+// the round's critical path).
+__global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__restrict__ hubs, long long total,
+                                                      const double2 *__restrict__ hubxy,
+                                                      const double *__restrict__ a_new, double *__restrict__ F) {
+  const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
+  if (q >= total) return;
+  int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (hubs[mid].w <= q) lo = mid; else hi = mid - 1;
+  }
+  const int4 hb = hubs[lo];
+  const int k = hb.y + (int)(q - hb.w);
+  const double a = a_new[hb.x];
+  const double2 p2 = hubxy[q];
+  st_f(F, k, (p2.x + a) - p2.y, ld_f(F, k));
 }
 
 __global__ void k_fill_split(long long cnt, double val, double *__restrict__ p) {
@@ -3154,11 +3186,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
       }
       if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
         hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
@@ -3192,11 +3224,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
                              h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
+                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
       }
       if (h->nwtiles[wg]) {
         const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
@@ -3219,6 +3251,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       // on the side stream, concurrently with the light tiles' launch (which then keeps
       // kernel 4's light-path register budget: 64 VGPRs, 8 waves per SIMD)
       const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
+      const int hub_sep = h->n_hub && !(h->geo == 0 && h->bins) ? 1 : 0;  // k_hub_flows after
       const bool fork = nh > 0 && h->fork_heavy;
       hipStream_t hs = fork ? h->stream2 : h->stream;
       if (fork) {
@@ -3243,12 +3276,12 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 ? 5 : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, hs, \
                          h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
-                         h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo);   \
+                         h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo, hub_sep); \
     if (nl)                                                                                 \
       hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl), dim3(kBlock), 0, h->stream, \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, \
-                         nullptr, nullptr, nullptr, nullptr);                                \
+                         nullptr, nullptr, nullptr, nullptr, 0);                             \
   } while (0)
 #define FU_RECON(C, N, D)                                                                   \
   do {                                                                                      \
@@ -3270,6 +3303,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       }
 #undef FU_RECON
 #undef FU_RECON_G
+      if (hub_sep)
+        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
+                           (long long)h->hub_total, h->hubxy, an, F);
       if (fork) {
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
@@ -3421,9 +3457,14 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   int rc = FU_OK;
   auto cleanup = [&](int code) { fu_destroy(h); return code; };
   if ((rc = set_device(h))) return cleanup(rc);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess)
-    return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  {  // the side stream (kernel 4's heavy tiles: the long exact chains) gets the highest
+     // priority, so its blocks are dispatched ahead of the light tiles when CU slots free up
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+    if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, hi) != hipSuccess)
+      return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
+  }
   {
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0) h->n_cu = cus;

@@ -19,6 +19,7 @@ ap.add_argument("--nt", type=int, default=-1)
 ap.add_argument("--pack", type=int, default=1)
 ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1024/512); 0 = default")
 ap.add_argument("--diag", type=int, default=0)
+ap.add_argument("--opt", action="append", default=[], help="extra engine option key=value (repeatable)")
 a = ap.parse_args()
 g = fu.Graph.from_spec(a.spec, seed=1)
 v = fu.uniform_values(g.n, seed=0)
@@ -28,6 +29,9 @@ if a.nt >= 0:
 eng.set_option("pack", a.pack)
 if a.tile:
     eng.set_option("tile_edges", a.tile)
+for kv in a.opt:
+    k, _, val = kv.partition("=")
+    eng.set_option(k, int(val))
 eng.run(a.warm)
 eng.reset()
 eng.set_option("diag", a.diag)
