@@ -703,6 +703,7 @@ __device__ inline T ld_stream(const T *p) {
 //   2 = no flow load/store (prices the flow stream);
 //   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
 //   5 = hub chains skipped (prices the exact sequential hub sums);
+//   6 = the flow pass of multi-chunk heavy rows skips its estimate gathers;
 //   12 = 1 and 2 together (prices col + the per-node arrays alone).
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
@@ -874,7 +875,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           fo[u] = k < d ? ld_f(F, b + k) : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) er[u] = k0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+        for (int u = 0; u < 4; ++u)
+          er[u] = k0 + lane + 64 * u < d ? (DIAG == 6 ? 0.0 : ld_est(pp, code_prev, a_prev, cc[u])) : 0.0;
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int k = k0 + lane + 64 * u;
@@ -3273,7 +3275,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #define FU_RECON_G(C, N, D, TE, TN)                                                         \
   do {                                                                                      \
     if (nh)                                                                                 \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 ? 5 : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, hs, \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, hs, \
                          h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
                          h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo, hub_sep); \
@@ -3295,6 +3297,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       else if (h->diag == 3) FU_RECON(false, false, 3);
       else if (h->diag == 4) FU_RECON(false, false, 4);
       else if (h->diag == 5) FU_RECON(false, false, 5);
+      else if (h->diag == 6) FU_RECON(false, false, 6);
       else if (h->diag == 12) FU_RECON(false, false, 12);
       else if (check) {
         if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);

@@ -19,11 +19,12 @@ ap.add_argument("--nt", type=int, default=-1)
 ap.add_argument("--pack", type=int, default=1)
 ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1024/512); 0 = default")
 ap.add_argument("--diag", type=int, default=0)
+ap.add_argument("--layout", default="given")
 ap.add_argument("--opt", action="append", default=[], help="extra engine option key=value (repeatable)")
 a = ap.parse_args()
 g = fu.Graph.from_spec(a.spec, seed=1)
 v = fu.uniform_values(g.n, seed=0)
-eng = fu.CollectAll(g, v, kernel=a.kernel)
+eng = fu.CollectAll(g, v, kernel=a.kernel, layout=a.layout)
 if a.nt >= 0:
     eng.set_option("nt", a.nt)
 eng.set_option("pack", a.pack)

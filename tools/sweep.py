@@ -56,6 +56,10 @@ VARIANTS = {
     "pipe_nopack": ("pipe", {"pack": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
     "recon_nofork": ("recon", {"fork_heavy": 0}),
+    "recon_deg_mega1024": ("recon", {"mega_hub": 1024, "layout": "degree"}),
+    "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
+    "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
+    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
     "pipe_stage": ("pipe_stage", {}),
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
     "pipe_b2": ("pipe", {"pipe_bpc": 2}),
@@ -77,6 +81,10 @@ VARIANTS = {
     "pipe_nopack": ("pipe", {"pack": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
     "recon_nofork": ("recon", {"fork_heavy": 0}),
+    "recon_deg_mega1024": ("recon", {"mega_hub": 1024, "layout": "degree"}),
+    "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
+    "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
+    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
     "recon_mega2048": ("recon", {"mega_hub": 2048}),
     "recon_mega1024": ("recon", {"mega_hub": 1024}),
