@@ -71,11 +71,11 @@ def round_kernels(kinfo):
     if k == "recon":
         return "k_round_recon %dx%d%s" % (kinfo["tile"][0], kinfo["tile"][1], "+nt" if kinfo["nt"] else "")
     if k == "stage":
-        return "k_stage + k_round_staged 512x64"
+        return "k_stage + k_round_staged 1024x128"
     if k == "pipe_stage":
-        return "k_stage + k_round_pipe<staged> 512x64"
+        return "k_stage + k_round_pipe<staged> 1024x128"
     if k == "pipe":
-        return "k_round_pipe<recon> 512x64"
+        return "k_round_pipe<recon> 1024x128"
     if k == "split2":
         return "k_gather_part0 + k_round_split"
     return k

@@ -1236,7 +1236,7 @@ __global__ __launch_bounds__(kBlock) void k_round_wave(
 // ------------------------------------------------------------------------------------
 constexpr int kStageThreads = 512;
 constexpr int kStageLds = 65536;  // bytes of table per slice
-constexpr int kStageTE = 512, kStageTN = 64;
+constexpr int kStageTE = 1024, kStageTN = 128;
 
 // The slice layouts (element bytes 1, 2, 4, 8) passed by value to the stage and round
 // launches; the device picks the layout from the table's actual packing width, so the
@@ -1528,7 +1528,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // per block through load -> gather -> LDS -> row chains -> store, so a block's memory
 // latency is exposed once per tile and the chip runs short of bytes in flight (kernel 4
 // without its gather still only streams 5.4 TB/s). Here a block owns a list of light tiles
-// (512 edges / 64 nodes, on its XCD) and keeps two of them ahead of the one it computes:
+// (1024 edges / 128 nodes, on its XCD) and keeps two of them ahead of the one it computes:
 // while tile i is staged in LDS and summed, the estimate loads of tile i+1 and the stream
 // loads (edges, flows, node arrays) of tile i+2 are in flight. LDS is double-buffered by
 // tile parity, so two barriers per tile suffice. Rows above the tile limit (hubs) get
@@ -1536,7 +1536,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // MODE 0: per edge col -> a_{r-1}[col] (or its packed code); MODE 1: the staged runs of
 // kernel 8 (sidx -> G). Arithmetic identical to kernel 4 (CA:98-99, CA:105-128).
 // ------------------------------------------------------------------------------------
-constexpr int kPipeTE = 512, kPipeTN = 64, kPipeKP = kPipeTE / kBlock;
+constexpr int kPipeTE = 1024, kPipeTN = 128, kPipeKP = kPipeTE / kBlock;
 constexpr int kPipeChunk = 64;  // max tiles per block (host sizes the grid accordingly)
 
 struct PipeStream {
