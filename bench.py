@@ -130,8 +130,9 @@ def main():
         eng.set_option("tile_edges", args.tile_edges)
     # with kernel "auto" the warmup rounds also pick the kernel for each packing width; run in
     # chunks so the host sees each plan's width (an asynchronous copy) while the rounds run
-    for w0 in range(0, args.warmup, 50):
-        eng.run(min(50, args.warmup - w0))
+    # (a pass needs 9 rounds per candidate within one call)
+    for w0 in range(0, args.warmup, 64):
+        eng.run(min(64, args.warmup - w0))
         eng.synchronize()
     eng.reset()           # the timed region is rounds 0 .. steps-1 from the zero state
     eng.synchronize()
@@ -296,6 +297,7 @@ def run_dist(args, world, rank, local, dist, barrier, allmax):
     else:
         n_tot, halo = part.n_local, part.n_ghost_a
     alg = 24 * e_tot + 28 * n_tot
+    kinfo = eng.info()
     if rank == 0:
         avg_s = kern_ms / 1e3 / args.steps
         achieved = alg / avg_s / 1e9 / world  # per GPU, against one GPU's peak
@@ -307,6 +309,7 @@ def run_dist(args, world, rank, local, dist, barrier, allmax):
             "data": "synthetic (seeded RGG, U[0,100) values)",
             "config": {"workload": f"rgg-dist:n={n_total} ({args.n} per GPU), deg=8, slabs, "
                                    "RCCL estimates-only halo", "E_directed": e_tot,
+                       "kernel_selected": kinfo["kernel"], "tile_selected": kinfo["tile"],
                        "halo_estimates_per_round": halo, "parallelism": f"graph partition x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None,

@@ -141,8 +141,8 @@ int fu_get_flows(fu_handle *h, double *f_out);
 int fu_get_round(fu_handle *h, int64_t *rounds_done);
 /* info[0] = kernel in use, [1] = nt, [2] = autotune (0 off, 1 pending, 2 done),
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
- * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
- * its candidates (4, 4 at 512x64, 6, 8, 10; 0 = not run), [20] = mega hubs, [21] = their
+ * passes, [7] = packing width of the last pass, [8..13] = the last pass's ns per round for
+ * its candidates (4, 4 at 512x64, 6, 8, 10, 4 at 1024x128; 0 = not run), [20] = mega hubs, [21] = their
  * pieces, [22] = pieces the exact-sum serial pass redid element by element (cumulative;
  * synchronises), [23..26] = the autotune winner per packing width 0, 8, 16, 32 (kernel * 10 +
  * kernel-4 geometry index, -1 = not tuned yet). With kernel

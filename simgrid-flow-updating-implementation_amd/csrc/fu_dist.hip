@@ -192,7 +192,9 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, cons
     d->comm = nullptr;
     return bail(fail(FU_ERR_NCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)));
   }
-  if (int rc = fu_set_option(h, "kernel", 4)) return bail(rc);  // halo: boundary estimates only
+  // kernel 4, "auto": its tile geometries are timed on real rounds; the halo carries only the
+  // boundary estimates
+  if (int rc = fu_set_option(h, "kernel", 0)) return bail(rc);
   *out = h;
   return FU_OK;
   FU_TRY_END

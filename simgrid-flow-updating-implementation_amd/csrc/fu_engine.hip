@@ -3384,13 +3384,9 @@ struct TuneCand {
 // measured; it stays selectable as an option
 // measured on ER-1M / R-MAT: 4+nt, 4 at 1024x256, 5 and 9 never win; they stay options
 static std::vector<TuneCand> tune_cands(const fu_handle *h) {
-  std::vector<TuneCand> cands = {{4, 0, 0}, {4, 0, 3}};
-  if (!h->dist) {
-    cands.push_back({6, 0, 0});
-    cands.push_back({8, 0, 0});
-    cands.push_back({10, 0, 0});
-  }
-  return cands;
+  // fixed order (fu_get_info reports per index); kernels 6, 8, 10 are single-GPU only
+  (void)h;
+  return {{4, 0, 0}, {4, 0, 3}, {6, 0, 0}, {8, 0, 0}, {10, 0, 0}, {4, 0, 1}};
 }
 static int width_class(int w) { return w == 8 ? 1 : w == 16 ? 2 : w == 32 ? 3 : 0; }
 static void use_cand(fu_handle *h, const TuneCand &c) {
@@ -3733,7 +3729,11 @@ constexpr int kMaxTunes = 4;
 static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   const std::vector<TuneCand> cands = tune_cands(h);
   constexpr int kTimed = 8;
-  const int32_t need = (1 + kTimed) * (int32_t)cands.size();
+  auto active = [&](size_t c) {
+    return h->tune_out[c] < 2 && !(cands[c].kernel == 6 && width != 0) && !(h->dist && cands[c].kernel != 4);
+  };
+  int32_t need = 0;
+  for (size_t c = 0; c < cands.size(); ++c) need += active(c) ? 1 + kTimed : 0;
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
   int bi = -1;
@@ -3742,7 +3742,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     // ones (its last ns per round stays reported)
     if (h->tune_out[c] >= 2) continue;
     h->tune_ms[c] = 0.f;
-    if (cands[c].kernel == 6 && width != 0) continue;
+    if (!active(c)) continue;
     if (cands[c].kernel == 9) {
       if (ensure_light(h) != FU_OK) {
         set_error("");

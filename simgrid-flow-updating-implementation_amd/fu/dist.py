@@ -255,6 +255,11 @@ class DistCollectAll:
     def synchronize(self):
         L.call("fu_synchronize", self._h)
 
+    def info(self) -> dict:
+        from .engine import handle_info
+
+        return handle_info(self._h)
+
     def close(self):
         if getattr(self, "_h", None):
             L.lib.fu_destroy(self._h)

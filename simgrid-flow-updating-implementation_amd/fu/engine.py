@@ -22,10 +22,28 @@ LAYOUTS = {"given": 0, "degree": 1}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
+def handle_info(h) -> dict:
+    """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
+    a = np.zeros(32, dtype=np.int64)
+    L.call("fu_get_info", h, L.ptr(a))
+    names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave", 8: "stage", 9: "pipe",
+             10: "pipe_stage"}
+    return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
+            "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
+            "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
+            "tuned_pack_width": int(a[7]),
+            "mega_hubs": int(a[20]), "hub_pieces": int(a[21]), "hub_pieces_redone": int(a[22]),
+            "tune_winner_by_width": {w: _cand_name(int(a[23 + k])) for k, w in
+                                     enumerate((0, 8, 16, 32)) if a[23 + k] >= 0},
+            "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
+                                  enumerate(("recon", "recon_512", "split2", "stage",
+                                             "pipe_stage", "recon_1024"))}}
+
+
 def _cand_name(code: int) -> str:
     kernel, geo = divmod(code, 10)
     names = {4: "recon", 6: "split2", 8: "stage", 10: "pipe_stage"}
-    return names.get(kernel, str(kernel)) + ("_512" if kernel == 4 and geo == 3 else "")
+    return names.get(kernel, str(kernel)) + ({3: "_512", 1: "_1024"}.get(geo, "") if kernel == 4 else "")
 
 
 class CollectAll:
@@ -111,20 +129,7 @@ class CollectAll:
 
     def info(self) -> dict:
         """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
-        a = np.zeros(32, dtype=np.int64)
-        L.call("fu_get_info", self._h, L.ptr(a))
-        names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave", 8: "stage", 9: "pipe",
-                 10: "pipe_stage"}
-        return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
-                "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
-                "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
-                "tuned_pack_width": int(a[7]),
-                "mega_hubs": int(a[20]), "hub_pieces": int(a[21]), "hub_pieces_redone": int(a[22]),
-                "tune_winner_by_width": {w: _cand_name(int(a[23 + k])) for k, w in
-                                         enumerate((0, 8, 16, 32)) if a[23 + k] >= 0},
-                "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
-                                      enumerate(("recon", "recon_512", "split2", "stage",
-                                                 "pipe_stage"))}}
+        return handle_info(self._h)
 
     def pack_widths(self) -> tuple:
         """Packed estimate table widths (0 = doubles): the last even / odd round's code

@@ -287,11 +287,11 @@ def test_autotune_switches_kernels_bitwise():
     v = fu.uniform_values(g.n, seed=8)
     eng = fu.CollectAll(g, v)
     assert eng.info()["autotune"] == "pending"
-    eng.run(50)
+    eng.run(64)
     info = eng.info()
-    assert info["autotune"] == "done" and info["rounds"] == 50
+    assert info["autotune"] == "done" and info["rounds"] == 64
     assert all(t > 0 for t in info["tune_us_per_round"].values())
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 50, nthreads=8)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 64, nthreads=8)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
 
@@ -304,17 +304,17 @@ def test_autotune_width_cache_across_reset_bitwise():
     v = fu.uniform_values(g.n, seed=12)
     eng = fu.CollectAll(g, v)
     eng.set_option("pack_every", 4)
-    for _ in range(8):  # the host sees each plan's width once the stream has passed it
-        eng.run(50)
+    for _ in range(7):  # the host sees each plan's width once the stream has passed it
+        eng.run(64)
         eng.synchronize()
     passes = eng.info()["tune_passes"]
     assert passes >= 3
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 400, nthreads=16)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 448, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     eng.reset()
-    for _ in range(8):
-        eng.run(50)
+    for _ in range(7):
+        eng.run(64)
         eng.synchronize()
     assert eng.info()["tune_passes"] == passes
     assert np.array_equal(eng.estimates(), a_ref)

@@ -1,9 +1,12 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-rm -f gpurun_out/ab_stage.log
-for p in ab/s1024 ab/s1024x256 ab/s2048 ab/s1024 ab/s1024x256 ab/s2048; do
-  timeout -k 10 200 python -u tools/_ab_stage.py $p >> gpurun_out/ab_stage.log 2>&1 || exit 1
-done
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "dist or autotune or rcc" > gpurun_out/pytest.log 2>&1 && \
+timeout -k 10 400 python -u bench.py --workload rgg-dist --n 8388608 --steps 300 > gpurun_out/bench_rggdist.log 2>&1
 echo rc=$?
-cat gpurun_out/ab_stage.log
+tail -3 gpurun_out/pytest.log
+for f in bench_rggdist; do python3 -c "
+import json,sys
+l=[x for x in open('gpurun_out/$f.log') if x.startswith('{')][-1]; d=json.loads(l)
+print('$f', '%.4g' % d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline'].get('avg_launch_us'), d['config'].get('kernel_selected'), d['config'].get('tile_selected'), d['config'].get('E_directed'))
+"; done
