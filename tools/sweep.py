@@ -60,6 +60,9 @@ VARIANTS = {
     "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
     "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
     "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
+    "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
+    "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
+    "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "pipe_stage": ("pipe_stage", {}),
     "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
     "pipe_b2": ("pipe", {"pipe_bpc": 2}),
@@ -85,6 +88,9 @@ VARIANTS = {
     "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
     "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
     "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
+    "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
+    "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
+    "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
     "recon_mega2048": ("recon", {"mega_hub": 2048}),
     "recon_mega1024": ("recon", {"mega_hub": 1024}),
