@@ -95,6 +95,12 @@ def main():
 
     import fu
 
+    # one rank per GPU; on a box with fewer GPUs than ranks (a functional check of the N > 1
+    # path) ranks share devices round-robin
+    ndev = fu.device_count()
+    if ndev > 0:
+        local = local % ndev
+
     def barrier():
         if dist is not None:
             dist.barrier()
@@ -159,7 +165,11 @@ def main():
                "us_per_round": chunk_ms[k] * 1e3 / max(1, bounds[k + 1] - bounds[k]),
                "pack_width_after": chunk_pack[k]} for k in range(nchunk)]
 
-    edges_total = g.E * world
+    edges_total = g.E  # every rank has its own graph (seed 1 + rank): sum their edges
+    if dist is not None:
+        te = torch.tensor([float(g.E)], dtype=torch.float64)
+        dist.all_reduce(te)
+        edges_total = int(te.item())
     value = edges_total * args.steps / wall
     ms_per_step = wall * 1e3 / args.steps
     # roofline of the dominant round kernel (one launch per round): its average launch time
