@@ -57,6 +57,7 @@ def parse():
                          "share cache lines; outputs keep the caller's numbering); auto = "
                          "degree for rmat, given otherwise")
     ap.add_argument("--tile-edges", type=int, default=0, help="kernel 4 tile (2048/1024/512); 0 = default")
+    ap.add_argument("--pack-every", type=int, default=0, help="rounds between packing plans; 0 = engine default (16)")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
@@ -134,6 +135,8 @@ def main():
     eng = fu.CollectAll(g, v, device=local, kernel=args.kernel, layout=layout)
     if args.tile_edges:
         eng.set_option("tile_edges", args.tile_edges)
+    if args.pack_every:
+        eng.set_option("pack_every", args.pack_every)
     # with kernel "auto" the warmup rounds also pick the kernel for each packing width; run in
     # chunks so the host sees each plan's width (an asynchronous copy) while the rounds run
     # (a pass needs 9 rounds per candidate within one call)
