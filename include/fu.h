@@ -185,6 +185,14 @@ int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_co
 int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                       int32_t mode, int32_t ticks, const char *order, const char *faults,
                       fu_trace **out);
+/* Same, with route transfer times: route_s[src * n + dst] = seconds
+ * a message from src to dst takes (SimGrid's LV08 model: 13.01 * sum(latency) +
+ * size / (0.97 * min bandwidth), fu/platform.py; link sharing is not modelled). A message
+ * matched at tick t is consumed from tick t + floor(T) + 1 (t + 1 for T < 1 s, the only
+ * case on the reference platform, CA:76). route_s NULL = every route under one tick. */
+int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                          int32_t mode, int32_t ticks, const char *order, const char *faults,
+                          const double *route_s, fu_trace **out);
 int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed);
 /* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
  * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */

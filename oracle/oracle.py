@@ -199,9 +199,14 @@ class TickEmulator:
     mode: "ca" (collect-all) or "pw" (pairwise).
     """
 
-    def __init__(self, actors, mode: str, faults: str | None = None):
+    def __init__(self, actors, mode: str, faults: str | None = None, route_s=None):
         """faults: "drop=P,delay=D:Q,seed=S" (extension, not in the reference; same spec and
-        draw order as fu_trace.cpp: one U[0,1) draw per put, in put order)."""
+        draw order as fu_trace.cpp: one U[0,1) draw per put, in put order).
+        route_s: optional n x n transfer times in seconds (sender row): a message matched at
+        tick t is consumed from tick t + floor(T) + 1 (the reference platform has T < 1 s on
+        every route, CA:76; the rule for longer routes is the extension fu_trace_build_routes
+        implements, parity unpinned against SimGrid itself)."""
+        self.route_s = route_s
         if mode not in ("ca", "pw"):
             raise ValueError(mode)
         self.p_drop, self.p_delay, self.d_ticks, self.fstate = 0.0, 0.0, 0, 0
@@ -327,6 +332,13 @@ class TickEmulator:
         nd.flows[sender] = -flow  # PW:99
         self._pw_fire(i, sender)  # PW:100
 
+    def _extra(self, sender_name, i):
+        """Whole ticks beyond the first that a transfer sender -> i takes."""
+        if self.route_s is None:
+            return 0
+        T = float(self.route_s[self.idx[sender_name]][i])
+        return int(math.floor(T)) if T >= 1.0 else 0
+
     def _set_last_avg(self, i, avg):
         self.nodes[i].last_avg = avg
         self.gv_last_avg[self.names[i]] = avg  # CA:62 / PW:61
@@ -347,7 +359,7 @@ class TickEmulator:
                     else:
                         c = [False, None, -1]
                     self.comm[i] = c
-                if c[0] and c[2] < self.t:  # CA:76 (transfer time in (0, 1) s)
+                if c[0] and c[2] + self._extra(c[1][0], i) < self.t:  # CA:76
                     msg = c[1]
                     self.comm[i] = None
                     self.events.append((self.t, i, 0, self.idx[msg[0]]))

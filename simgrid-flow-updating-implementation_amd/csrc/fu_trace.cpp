@@ -31,6 +31,7 @@
 // one. Lost messages exercise the timeouts (CA:87-91, PW:86-91), i.e. Flow Updating's
 // self-healing. The fault model lives entirely in the schedule, so the GPU replay is the
 // same code.
+#include <cmath>
 #include <cstring>
 #include <unordered_map>
 
@@ -79,6 +80,17 @@ struct Builder {
   int32_t delay_ticks = 0;
   uint64_t fstate = 0;
   std::vector<std::vector<std::pair<int32_t, int32_t>>> delayed;  // due tick -> (dst, id)
+  // route transfer times (seconds, n x n, sender row), NULL = every route under one tick
+  const double *route = nullptr;
+
+  // whole ticks a transfer on src -> dst takes beyond the first: a message matched at tick t
+  // completes at t + T and is consumed from tick t + floor(T) + 1 (t + 1 when T < 1, CA:76)
+  int32_t extra(int32_t src, int32_t dst) const {
+    if (!route) return 0;
+    const double T = route[(int64_t)src * n + dst];
+    if (!(T >= 1.0)) return 0;  // < 1 s, negative or NaN
+    return T >= 1e9 ? 1000000000 : (int32_t)std::floor(T);
+  }
 
   Builder(int32_t n_, int32_t mode_, fu_trace &tr_) : n(n_), mode(mode_), tr(tr_) {}
 
@@ -190,7 +202,7 @@ struct Builder {
         cstate[i] = 1;
       }
     }
-    if (cstate[i] == 2 && ctick[i] < t) {  // CA:76-82
+    if (cstate[i] == 2 && ctick[i] + extra(msg_sender[cmsg[i]], i) < t) {  // CA:76-82
       int32_t id = cmsg[i];
       cstate[i] = 0;
       int32_t s = slot_for(i, msg_sender[id]);
@@ -283,6 +295,12 @@ int fu_trace_build(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_co
 int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                       int32_t mode, int32_t ticks, const char *order, const char *faults,
                       fu_trace **out) {
+  return fu_trace_build_routes(n, decl_rowptr, decl_col, mode, ticks, order, faults, nullptr, out);
+}
+
+int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
+                          int32_t mode, int32_t ticks, const char *order, const char *faults,
+                          const double *route_s, fu_trace **out) {
   FU_TRY_BEGIN
   if (!out || n <= 0 || !decl_rowptr || ticks < 0 || (mode != FU_MODE_COLLECTALL && mode != FU_MODE_PAIRWISE))
     return fail(FU_ERR_ARG, "fu_trace_build: bad arguments");
@@ -305,6 +323,7 @@ int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl
   B.p_delay = p_delay;
   B.delay_ticks = dticks;
   B.fstate = fseed;
+  B.route = route_s;
   B.nbrs.resize(n);
   for (int32_t i = 0; i < n; ++i) {
     for (int64_t k = decl_rowptr[i]; k < decl_rowptr[i + 1]; ++k) {

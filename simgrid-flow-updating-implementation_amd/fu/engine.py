@@ -170,7 +170,9 @@ class Trace:
     """
 
     def __init__(self, decl_rowptr, decl_col, mode: str, ticks: int, order: str = "fwd",
-                 faults: str | None = None):
+                 faults: str | None = None, route_s=None):
+        """route_s: optional n x n transfer times in seconds (sender row); a message matched at
+        tick t is consumed from tick t + floor(T) + 1 (fu_trace_build_routes)."""
         rp = np.ascontiguousarray(decl_rowptr, dtype=np.int64)
         c = np.ascontiguousarray(decl_col, dtype=np.int32)
         self.n = len(rp) - 1
@@ -179,9 +181,14 @@ class Trace:
         self.ticks = int(ticks)
         self.order = order
         out = L.vp()
-        L.call("fu_trace_build_ex", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
+        self._route = None
+        if route_s is not None:
+            self._route = np.ascontiguousarray(route_s, dtype=np.float64)
+            if self._route.shape != (self.n, self.n):
+                raise ValueError("route_s must be n x n")
+        L.call("fu_trace_build_routes", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
                self.ticks, order.encode(), faults.encode() if faults else None,
-               ctypes.byref(out))
+               None if self._route is None else L.ptr(self._route), ctypes.byref(out))
         self._h = out
         self.faults = faults
         dr, dl = L.i64(), L.i64()

@@ -140,3 +140,85 @@ def test_fault_spec_errors():
     for bad in ("drop=2", "delay=0:0.1", "junk=1", "drop=0.6,delay=1:0.6"):
         with pytest.raises(fu.FuError, match="faults"):
             fu.Trace(rp, col, "pairwise", 10, faults=bad)
+
+
+@pytest.mark.parametrize("mode", ["collectall", "pairwise"])
+@pytest.mark.parametrize("order", ["fwd", "rand:3"])
+def test_route_times_match_emulator(mode, order):
+    """Route transfer times of one tick or more (§8(f) row 3, fu_trace_build_routes): a message
+    matched at tick t is consumed from tick t + floor(T) + 1. The native trace and the oracle
+    emulator agree event for event and snapshot for snapshot; every route under one tick
+    gives the plain schedule of the reference platform (CA:76)."""
+    d = load_json("tick_small_platform_ca_fwd.json")
+    names, vals, rp, col = fixture_decl_csr(d)
+    n = len(names)
+    rng = np.random.default_rng(11)
+    route = rng.uniform(0.0, 3.7, (n, n))
+    np.fill_diagonal(route, 0.0)
+    em = oracle.TickEmulator(d["actors"], "ca" if mode == "collectall" else "pw", route_s=route)
+    snaps = {}
+
+    def cb(t, e):
+        if t % 50 == 0 or t == 2999:
+            snaps[t] = dict(e.last_avg_items())
+
+    em.run(3000, order, on_tick=cb)
+    tr = fu.Trace(rp, col, mode, 3000, order, route_s=route)
+    a = tr.arrays()
+    assert trace_events_as_log(a) == [list(x) for x in em.events]
+    ticks = sorted(snaps)
+    last, flow, est, s2 = coracle.replay(a["rowptr"], vals, a["tick_task_off"], a["tasks"], a["events"],
+                                         a["out_ids"], tr.n_msgs, ticks)
+    for t in ticks:
+        for i, v in snaps[t].items():
+            assert s2[t][i] == v
+    mean = sum(vals) / len(vals)
+    assert max(abs(x - mean) for x in snaps[2999].values()) / mean < 1e-9
+    # all routes under one tick: the same trace as without route times
+    fast = fu.Trace(rp, col, mode, 600, order, route_s=np.full((n, n), 0.9)).arrays()
+    plain = fu.Trace(rp, col, mode, 600, order).arrays()
+    for k in ("tick_task_off", "tasks", "events", "out_ids"):
+        assert np.array_equal(fast[k], plain[k])
+    with pytest.raises(ValueError):
+        fu.Trace(rp, col, mode, 10, order, route_s=np.zeros((n, n + 1)))
+
+
+@pytest.mark.gpu
+def test_engine_runs_a_slow_platform(tmp_path):
+    """A platform whose routes need more than one tick (LV08: 13.01 x 100 ms + 154 B / (0.97
+    x 1 kB/s) = 1.46 s) is simulated with route times instead of being rejected: the drop-in
+    Engine's replay equals the oracle emulator with the same route matrix, and converges."""
+    import io
+
+    from conftest import write_deployment_xml
+
+    d = load_json("tick_small_platform_ca_fwd.json")
+    hosts = [a[0] for a in d["actors"]]
+    lines = ["<?xml version='1.0'?>", '<platform version="4.1">', '  <zone id="z" routing="Full">']
+    for h in hosts:
+        lines.append(f'    <host id="{h}" speed="1Gf"/>')
+    lines.append('    <link id="slow" bandwidth="1kBps" latency="100ms"/>')
+    for i, s_ in enumerate(hosts):
+        for t in hosts[i + 1:]:
+            lines += [f'    <route src="{s_}" dst="{t}">', '      <link_ctn id="slow"/>', "    </route>"]
+    lines += ["  </zone>", "</platform>"]
+    plat = tmp_path / "slow_platform.xml"
+    plat.write_text("\n".join(lines) + "\n")
+    dep = tmp_path / "actors.xml"
+    write_deployment_xml(dep, d["actors"])
+    p = fu.platform.load_platform(str(plat))
+    T = p.route_time(hosts[0], hosts[1])
+    assert 1.0 < T < 2.0
+    n = len(hosts)
+    route = np.full((n, n), T)
+    np.fill_diagonal(route, 0.0)
+    for mode, m in (("collectall", "ca"), ("pairwise", "pw")):
+        e, res = fu.run_reference_main(mode, str(plat), str(dep), 1000.0, 10.0, order="fwd",
+                                       out=io.StringIO())
+        em = oracle.TickEmulator(d["actors"], m, route_s=route)
+        em.run(1001, "fwd")
+        want = dict(em.last_avg_items())
+        for i, v in want.items():
+            assert res["last_avg"][i] == v, (mode, i)
+        # two-tick deliveries slow the mixing: 1e-7 at t = 1000 (1e-13 on the reference platform)
+        assert np.max(np.abs(res["last_avg"] - 190 / 6)) / (190 / 6) < 1e-6
