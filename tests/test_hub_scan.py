@@ -85,3 +85,23 @@ def test_hub_scan_degree_layout():
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 60, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+@pytest.mark.parametrize("fork", [1, 0])
+@pytest.mark.parametrize("kind", ["all_heavy", "mixed"])
+def test_heavy_light_split_launches(fork, kind):
+    """Kernel 4 runs heavy tiles (hubs, heavy rows) as their own launch on a side stream and
+    light tiles as a light-only launch (fork_heavy 1), or both in order on one stream
+    (fork_heavy 0). Graphs with only heavy rows and with both must give the oracle's bits."""
+    if kind == "all_heavy":  # K_300: every row has degree 299 > hub_threshold
+        n = 300
+        iu = np.triu_indices(n, 1)
+        g = fu.Graph.from_edges(n, iu[0].astype(np.int32), iu[1].astype(np.int32))
+    else:
+        g = _star_er(5_000, 12_000, seed=5)
+    v = fu.uniform_values(g.n, seed=5)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 40, nthreads=16)
+    for tile in (2048, 1024, 512):
+        a, f, _ = _run(g, v, 40, fork_heavy=fork, tile_edges=tile, mega_hub=256)
+        assert np.array_equal(a, a_ref), (kind, fork, tile)
+        assert np.array_equal(f, f_ref), (kind, fork, tile)
