@@ -1,6 +1,9 @@
 set -o pipefail
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_hub_scan.py -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest.log 2>&1
+rm -f gpurun_out/ab_stage.log
+for p in abtest/cur abtest/nt abtest/cur abtest/nt; do
+  timeout -k 10 120 python -u tools/_ab_stage.py $p >> gpurun_out/ab_stage.log 2>&1 || exit 1
+done
 echo rc=$?
-tail -5 gpurun_out/pytest.log
+grep '^{' gpurun_out/ab_stage.log
