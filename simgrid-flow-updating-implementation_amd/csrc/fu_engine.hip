@@ -1248,8 +1248,11 @@ struct StageArgs {
   const unsigned short *colS[4];
   const unsigned *sidx[4];
   const int *gbase[4];
+  const unsigned short *sidx16[4];  // compact sidx (null: use sidx)
+  const int *dtab[4];
   int sel[4];  // layout used for tables of width 8, 16, 32, 0 (0..3)
 };
+constexpr int kStageRuns = 64;  // slice runs per tile the compact sidx can address
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
 }
@@ -1445,21 +1448,40 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   const int nb = tl.x, nn = tl.y - tl.x;
   const int e0 = tl.z, ne = tl.w - tl.z;
   constexpr int kPer = TE / kBlock;
-  unsigned si[kPer];
+  const unsigned short *__restrict__ s16 = sa.sidx16[lsel];
+  unsigned si[kPer];  // position in the tile (low 16 bits) | G index in the group (high 16)
   double x[kPer], g[kPer];
+  int gi[kPer];
+  if (s16) {  // compact: u16 position | run << 10; G index = gbase + m + D[run] (lane run holds D)
+    const int dl = sa.dtab[lsel][(size_t)tile * kStageRuns + (t & 63)];
+    unsigned short c16[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    si[k] = q < ne ? sidx[e0 + q] : 0u;
-    x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      c16[k] = q < ne ? s16[e0 + q] : (unsigned short)0;
+      x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      const int dd = __shfl(dl, (int)(c16[k] >> 10));
+      si[k] = c16[k] & 1023u;
+      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : gb + q + dd) : -1;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      si[k] = q < ne ? sidx[e0 + q] : 0u;
+      x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k)
+      gi[k] = t + k * kBlock < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
   }
   const int rp = t <= nn ? rowptr[nb + t] : 0;
   const double vv = t < nn ? v[nb + t] : 0.0;
   const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
-  int gi[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k)
-    gi[k] = t + k * kBlock < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
   // every G load of the tile first, then decode (escapes gather the double via col)
   if (pp.width == 0) {
 #pragma unroll
@@ -2582,6 +2604,10 @@ struct fu_handle {
     int2 *aitem = nullptr;         // stage items {first element, count}, grouped by block
     unsigned short *colS = nullptr;  // per staged element: column offset within its slice
     unsigned *sidx = nullptr;      // per tile edge (slice order): G index in group << 16 | position
+    // compact form (when every tile's edges fall into <= 64 slice runs): per edge u16 =
+    // position | run << 10, and per tile the run offsets D (G index = gbase + m + D[run])
+    unsigned short *sidx16 = nullptr;
+    int *dtab = nullptr;           // kStageRuns per light tile
     int *gbase = nullptr;          // per light tile: its group's first staged element
   };
   StageLayout st[4];            // element bytes 1, 2, 4, 8
@@ -2595,6 +2621,7 @@ struct fu_handle {
   void *stG = nullptr;          // staged estimates, 8 B per light edge
   int seen_width = 0;           // packing width the host last saw (layout choice)
   int st_force = -1;            // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
+  int st_compact = 1;           // option "stage_compact": kernel 8 reads the u16 sidx
   std::vector<int4> h_light;    // host copies (layout construction)
   std::vector<int32_t> h_gstart;
   int n_cu = 256;               // compute units (kernel 9 grid)
@@ -3028,6 +3055,44 @@ int ensure_stage(fu_handle *h) {
         for (int64_t i = ni * q / Q; i < ni * (q + 1) / Q; ++i) aitem.push_back(per_s[s][i]);
       }
     aoff[P * Q] = (int32_t)aitem.size();
+    // compact sidx: within a tile's slice-order list, the elements of one slice are
+    // consecutive in the group region, so G index - m is constant per run
+    std::vector<uint16_t> s16;
+    std::vector<int32_t> dt;
+    bool compact = kStageTE <= 1024;
+    if (compact) {
+      s16.assign(h->E > 0 ? h->E : 1, 0);
+      dt.assign(light.size() * kStageRuns, 0);
+      for (size_t t = 0; t < light.size() && compact; ++t) {
+        const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
+        int run = -1;
+        int32_t dprev = 0;
+        int64_t sprev = -1;
+        for (int32_t m = 0; m < ne; ++m) {
+          const uint32_t v = sidx[e0 + m];
+          const int32_t pos = (int32_t)(v & 0xFFFFu), kp = (int32_t)(v >> 16);
+          const int64_t sl = h->h_col[e0 + pos] / SN;
+          if (sl != sprev) {
+            if (++run >= kStageRuns) { compact = false; break; }
+            sprev = sl;
+            dprev = kp - m;
+            dt[t * kStageRuns + run] = dprev;
+          } else if (kp - m != dprev) {
+            compact = false;
+            break;
+          }
+          s16[e0 + m] = (uint16_t)(pos | (run << 10));
+        }
+      }
+    }
+    if (L.sidx16) hipFree(L.sidx16);
+    if (L.dtab) hipFree(L.dtab);
+    L.sidx16 = nullptr;
+    L.dtab = nullptr;
+    if (compact) {
+      if (int rc = up(&L.sidx16, s16.data(), s16.size())) return rc;
+      if (int rc = up(&L.dtab, dt.data(), dt.size())) return rc;
+    }
     L.P = (int)P;
     L.Q = (int)Q;
     if (int rc = up(&L.aoff, aoff.data(), aoff.size())) return rc;
@@ -3060,6 +3125,8 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
     sa.colS[li] = L.colS;
     sa.sidx[li] = L.sidx;
     sa.gbase[li] = L.gbase;
+    sa.sidx16[li] = h->st_compact ? L.sidx16 : nullptr;
+    sa.dtab[li] = L.dtab;
     if (L.P) g = std::max<unsigned>(g, (unsigned)(L.P * L.Q));
   }
   for (int want = 0; want < 4; ++want) {
@@ -3650,6 +3717,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
     return FU_OK;
   }
+  if (!std::strcmp(key, "stage_compact")) {  // kernel 8: u16 sidx with per-tile runs (1) or u32 (0)
+    h->st_compact = value != 0;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "fork_heavy")) {  // kernel 4: heavy tiles on a side stream (1) or in order (0)
     h->fork_heavy = value != 0;
     return FU_OK;
@@ -4013,7 +4084,8 @@ int fu_destroy(fu_handle *h) {
                   h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
                   h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase,
                   h->hub_rows, h->hub_off, h->hubxy, h->hrows, h->hub_piece, h->hub_p0, h->psum,
-                  h->hsum, h->hub_redo};
+                  h->hsum, h->hub_redo, h->st[0].sidx16, h->st[1].sidx16, h->st[2].sidx16,
+                  h->st[3].sidx16, h->st[0].dtab, h->st[1].dtab, h->st[2].dtab, h->st[3].dtab};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (h->ev0) hipEventDestroy(h->ev0);
