@@ -62,6 +62,8 @@ VARIANTS = {
     "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
     "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
     "stage_u32": ("stage", {"stage_compact": 0}),
+    "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
+    "pipe_stage_nopack_": ("pipe_stage", {"pack": 0}),
     "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
     "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "pipe_stage": ("pipe_stage", {}),
@@ -91,6 +93,8 @@ VARIANTS = {
     "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
     "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
     "stage_u32": ("stage", {"stage_compact": 0}),
+    "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
+    "pipe_stage_nopack_": ("pipe_stage", {"pack": 0}),
     "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
     "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
