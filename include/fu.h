@@ -118,7 +118,7 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *          default 8192), "hub_scan" (mega hubs: 1 = parallel exact left-to-right sums,
  *          speculated per binade and verified; 0 = one wave's sequential chain, default),
  * "wave_heavy" (kernel 4: rows above hub_threshold one per wave (1, default) or per block),
- * "pipe_bpc" (kernels 9/10: persistent blocks per CU; default 6), "stage_layout" (kernels
+ * "pipe_bpc" (kernels 9/10: persistent blocks per CU; default 4), "stage_layout" (kernels
  *          8/10, tests: -1 = by packing width, 0..3 = slice layout of 1/2/4/8-byte elements). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */

@@ -2625,7 +2625,7 @@ struct fu_handle {
   std::vector<int4> h_light;    // host copies (layout construction)
   std::vector<int32_t> h_gstart;
   int n_cu = 256;               // compute units (kernel 9 grid)
-  int pipe_bpc = 6;             // kernel 9/10: persistent blocks per CU
+  int pipe_bpc = 4;             // kernel 9/10: persistent blocks per CU (4 fit at 1024x128 tiles)
   // multi-GPU (fu_dist.hip)
   void *dist = nullptr;
 };

@@ -63,7 +63,8 @@ VARIANTS = {
     "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
     "stage_u32": ("stage", {"stage_compact": 0}),
     "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
-    "pipe_stage_nopack_": ("pipe_stage", {"pack": 0}),
+    "pipe_stage_b2": ("pipe_stage", {"pipe_bpc": 2}),
+    "pipe_stage_b3": ("pipe_stage", {"pipe_bpc": 3}),
     "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
     "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "pipe_stage": ("pipe_stage", {}),
@@ -94,7 +95,8 @@ VARIANTS = {
     "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
     "stage_u32": ("stage", {"stage_compact": 0}),
     "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
-    "pipe_stage_nopack_": ("pipe_stage", {"pack": 0}),
+    "pipe_stage_b2": ("pipe_stage", {"pipe_bpc": 2}),
+    "pipe_stage_b3": ("pipe_stage", {"pipe_bpc": 3}),
     "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
     "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
     "recon_mega4096": ("recon", {"mega_hub": 4096}),
