@@ -496,9 +496,13 @@ __device__ inline void wave_sync() {
 // S and T lane-uniform in and out). Even lanes run the S chain, odd lanes the T chain, so
 // one fp64 add per element advances both sums: a wave64 v_add_f64 occupies the SIMD for the
 // same cycles whatever the EXEC mask, and two separate chains cost two. The LDS reads of
-// the next 8 elements are issued before the dependent adds of the current 8.
+// the next B elements are issued before the dependent adds of the current B (B = 16: the adds
+// of one batch cover the LDS latency of the next).
+#ifndef FU_CHAIN_B
+#define FU_CHAIN_B 16  // measured: 8 -> 8.75, 16 -> 7.2, 32 -> 6.4 ns per element (32 costs registers)
+#endif
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
-  constexpr int B = 8;
+  constexpr int B = FU_CHAIN_B;
   const bool odd = threadIdx.x & 1;
   const double *src = odd ? es : xs;
   double acc = odd ? T : S;

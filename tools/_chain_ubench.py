@@ -1,13 +1,13 @@
 """Exact-chain speed: one star hub of L leaves (kernel 4's mega-hub path), device us/round."""
 import sys, os, json
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "simgrid-flow-updating-implementation_amd"))
+sys.path.insert(0, sys.argv[1] if len(sys.argv) > 1 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "simgrid-flow-updating-implementation_amd"))
 import numpy as np
 import fu
 for L in (100_000, 1_000_000):
     hub = L
     g = fu.Graph.from_edges(L + 1, np.full(L, hub, dtype=np.int32), np.arange(L, dtype=np.int32))
     v = fu.uniform_values(g.n, seed=1)
-    out = {"leaves": L}
+    out = {"pkg": sys.argv[1] if len(sys.argv) > 1 else "", "leaves": L}
     for name, opts in (("chain", {}), ("diag5", {"diag": 5})):
         e = fu.CollectAll(g, v, kernel="recon")
         e.run(5)
