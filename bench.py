@@ -1,31 +1,40 @@
 #!/usr/bin/env python3
 """Headline benchmark: directed-edge flow updates/s + % HBM roofline; rounds to 1e-9 error.
 
-Workload (BASELINE.json configs[1]): Erdos-Renyi G(n=1,000,000, m=4,000,000), self-loops
-dropped, deduplicated, symmetrised (E ~ 8.0e6 directed edges); node values U[0,100)
-(SplitMix64, seed 0); collect-all generation-synchronous rounds in fp64 on one MI355X.
-A "step" = one round = Peer.on_receive for every directed edge + Peer.avg_and_send for
-every node (flowupdating-collectall.py:93-128) = one launch of the round kernel.
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--workload auto|er|rgg-dist|pairwise|...]
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+N = 1 (default workload "er", BASELINE.json configs[1]): Erdos-Renyi G(n=1,000,000,
+m=4,000,000), self-loops dropped, deduplicated, symmetrised (E ~ 8.0e6 directed edges); node
+values U[0,100) (SplitMix64, seed 0); collect-all generation-synchronous rounds in fp64 on one
+MI355X. A step = one round = Peer.on_receive for every directed edge + Peer.avg_and_send for
+every node (flowupdating-collectall.py:93-128). The timed region is rounds 0 .. K-1 of the job
+from the zero state, exactly the first K rounds of the BASELINE 1000-round run.
 
-At N > 1 (torch.distributed.run, one process per GPU) every rank runs its own ER-1M
-instance (graph seed 1 + rank), the weak-scaling "independent graphs" mode: the ER graph
-has no locality, so partitioning it would put ~7/8 of its edges on the halo.
-Ranks synchronise with a barrier around the timed region; time = max over ranks; value =
-edge updates of all ranks / that time. torch.distributed (gloo, CPU) is used only for the
-barrier and the max; the hot path is libfu.so.
+N > 1 (default workload "rgg-dist", BASELINE.json configs[4], weak scaling): one random
+geometric graph of 2^23 nodes per GPU (avg degree 8), cut into x-slabs, one rank per GPU,
+estimates-only RCCL halo exchange every round (fu_dist.hip). Without WORLD_SIZE in the
+environment, `--gpus N` starts the N ranks itself (torch.distributed.run, 127.0.0.1) before
+anything touches a GPU; a box with fewer than N visible GPUs is an error, never a silent
+1-GPU line.
 
-Printed by rank 0: ONE JSON line (contract in the task statement), with `roofline` (the
-round kernel's algorithmic bytes 24E + 28N per launch / average launch time from HIP
-events on the library's stream, against 8 TB/s) and `cpu_baseline` (the C port of the
-oracle on the host, single thread, on a bounded sample of the same workload).
+Setup outside the timed region: graph generation, handle creation, one autotune pass
+(fu_tune: the candidate kernels timed on real rounds at the unpacked width), W warmup rounds
+(in chunks, so the autotuner also sees every packing width the warmup reaches), fu_reset.
+Timed: HIP events on the engine's stream around round 0 and every chunk, one host sync at the
+end, between barriers; value = edge updates of all ranks / max-over-ranks wall time.
+
+Printed by rank 0: ONE JSON line, with `roofline` (the round kernel's algorithmic bytes
+24E + 28N per launch, §8(d), / the mean device time of rounds 1 .. K-1 from those events,
+against 8 TB/s; `traffic` from the PMC passes in profiles/ when they match this command) and
+`cpu_baseline` (the C port of the oracle on the host, single thread, bounded sample).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,35 +44,134 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "simgrid-flow-updating-implementation_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md)
+METRIC = "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000, help="timed rounds")
+    ap.add_argument("--steps", type=int, default=1000, help="timed rounds (ticks for pairwise)")
     ap.add_argument("--warmup", type=int, default=400,
-                    help="untimed rounds first: the autotuner times the candidate kernels at every "
-                         "packing width the run reaches (0, 32, 16, 8 bits), then fu_reset")
-    ap.add_argument("--n", type=int, default=1_000_000)
+                    help="untimed rounds after the autotune pass (the autotuner also times the "
+                         "candidates at every packing width these reach), then fu_reset")
+    ap.add_argument("--n", type=int, default=0,
+                    help="nodes (er: 1e6; rgg-dist: per GPU, 2^23; rmat: scale, 24; rr: 65536)")
     ap.add_argument("--m", type=int, default=4_000_000)
-    ap.add_argument("--workload", default="er", choices=["er", "rgg", "rmat", "rr", "rgg-dist"],
-                    help="er = the headline ER-1M (default); others are exploratory: rgg "
-                         "(--n nodes, avg deg 8), rmat (scale = --n, edge factor 16), rr (d = 8), "
-                         "rgg-dist (ONE random geometric graph of --n nodes per GPU, partitioned "
-                         "into slabs across the ranks, RCCL halo exchange every round)")
+    ap.add_argument("--workload", default="auto",
+                    choices=["auto", "er", "rgg", "rmat", "rr", "rgg-dist", "pairwise"],
+                    help="auto = er at N = 1, rgg-dist at N > 1; rgg / rmat / rr = exploratory "
+                         "single-GPU graphs; pairwise = RR-64K tick replay (BASELINE configs[2])")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--layout", default="auto", choices=["auto", "given", "degree"],
                     help="device node numbering: degree = relabelled by degree (hot estimates "
                          "share cache lines; outputs keep the caller's numbering); auto = "
                          "degree for rmat, given otherwise")
-    ap.add_argument("--tile-edges", type=int, default=0, help="kernel 4 tile (2048/1024/512); 0 = default")
-    ap.add_argument("--pack-every", type=int, default=0, help="rounds between packing plans; 0 = engine default (16)")
     ap.add_argument("--conv-rounds", type=int, default=1000,
                     help="rounds of the (untimed) convergence run for rounds-to-1e-9")
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target length of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-conv", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """--gpus N without a launcher: start N rank processes (one per GPU) as children and
+    return their exit status. Runs before this process touches HIP."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr=127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    print(f"[bench] starting {args.gpus} ranks: {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
+def chunk_bounds(steps: int, nchunk: int = 10):
+    """Round 0 alone (the timeout fire on zero state), then rounds 1..K-1: one chunk up to
+    100 rounds, else nchunk chunks (each event mark costs the stream ~6 us)."""
+    if steps <= 1:
+        return [0, steps]
+    rest = steps - 1
+    k = 1 if steps <= 100 else min(nchunk, rest)
+    return [0] + [1 + rest * q // k for q in range(k + 1)]
+
+
+def main():
+    args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    world = int(env_world or "1")
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world != args.gpus:
+        print(f"[bench] error: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
+
+    import fu
+
+    print(f"[bench] rank {rank}/{world} (local {local})", file=sys.stderr, flush=True)
+    ndev = fu.device_count()
+    if ndev < local_world or ndev == 0:
+        # never share a GPU between ranks or report a scaling line for GPUs that do not exist
+        print(f"[bench] error: {local_world} rank(s) on this node need {local_world} GPU(s), "
+              f"{ndev} visible", file=sys.stderr, flush=True)
+        sys.exit(3)
+
+    wl = args.workload
+    if wl == "auto":
+        wl = "er" if world == 1 else "rgg-dist"
+    if wl == "rgg-dist":
+        return run_dist(args, world, rank, local, dist)
+    if world > 1:
+        print(f"[bench] error: workload {wl} is single-GPU (use rgg-dist at N > 1)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if wl == "pairwise":
+        return run_pairwise(args)
+    return run_single(args, wl)
+
+
+def timed_rounds(eng, steps: int):
+    """Rounds 0..steps-1 from the zero state; HIP event marks on the engine's stream around
+    round 0 and each chunk, one host sync at the end. Returns (wall_s, per-chunk device ms,
+    bounds)."""
+    b = chunk_bounds(steps)
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.mark(0)
+    for k in range(len(b) - 1):
+        eng.run(b[k + 1] - b[k])
+        eng.mark(k + 1)
+    eng.synchronize()
+    wall = time.perf_counter() - t0
+    dev = [eng.elapsed(k, k + 1) for k in range(len(b) - 1)]
+    return wall, dev, b
+
+
+def roofline(alg_bytes: int, dev_ms, b, traffic=None, kernel=""):
+    """Dominant kernel = the round kernel of rounds >= 1: its mean launch time from the
+    events; round 0 (k_round0 + k_round0_flows) is reported beside it."""
+    steps = b[-1]
+    r1 = sum(dev_ms[1:]) / max(1, steps - 1) if steps > 1 else dev_ms[0]
+    achieved = alg_bytes / (r1 * 1e-3) / 1e9
+    whole = sum(dev_ms) / max(1, steps)
+    return {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg_bytes,
+            "kernel": kernel, "avg_launch_us": r1 * 1e3, "launch_window": f"rounds 1-{steps - 1}",
+            "round0_us": dev_ms[0] * 1e3, "whole_region_avg_round_us": whole * 1e3,
+            "whole_region_frac": alg_bytes / (whole * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
 
 def round_kernels(kinfo):
@@ -82,114 +190,69 @@ def round_kernels(kinfo):
     return k
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch
-        import torch.distributed as dist
+def pmc_traffic(n, E, kernel_selected, steps):
+    """HBM bytes per round from profiles/pmc_traffic.json (tools/pmc.sh + tools/make_pmc_traffic.py),
+    only when it was measured on this graph, kernel and timed window."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    for rec in pmc if isinstance(pmc, list) else [pmc]:
+        if rec.get("n") == n and rec.get("E") == E and rec.get("kernel_selected") == kernel_selected \
+                and rec.get("rounds_timed") == steps:
+            return rec.get("bytes_per_launch")
+    return None
 
-        dist.init_process_group("gloo", init_method="env://", world_size=world, rank=rank)
 
+def run_single(args, wl):
     import fu
 
-    # one rank per GPU; on a box with fewer GPUs than ranks (a functional check of the N > 1
-    # path) ranks share devices round-robin
-    ndev = fu.device_count()
-    if ndev > 0:
-        local = local % ndev
-
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
-    def allmax(x: float) -> float:
-        if dist is None:
-            return x
-        t = torch.tensor([x], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item())
-
-    if args.workload == "rgg-dist":
-        return run_dist(args, world, rank, local, dist, barrier, allmax)
     t_gen = time.perf_counter()
-    if args.workload == "er":
-        g = fu.Graph.erdos_renyi(args.n, args.m, seed=1 + rank)
-        wl = f"er:n={args.n},m={args.m} collect-all generation-synchronous rounds"
-    elif args.workload == "rgg":
-        g = fu.Graph.random_geometric(args.n, avg_deg=8.0, seed=1 + rank)
-        wl = f"rgg:n={args.n},deg=8 collect-all generation-synchronous rounds"
-    elif args.workload == "rmat":
-        g = fu.Graph.rmat(args.n, 16, seed=1 + rank)
-        wl = f"rmat:scale={args.n},ef=16 collect-all generation-synchronous rounds"
+    if wl == "er":
+        n = args.n or 1_000_000
+        g = fu.Graph.erdos_renyi(n, args.m, seed=1)
+        desc = f"er:n={n},m={args.m} collect-all generation-synchronous rounds"
+    elif wl == "rgg":
+        n = args.n or (1 << 20)
+        g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
+        desc = f"rgg:n={n},deg=8 collect-all generation-synchronous rounds"
+    elif wl == "rmat":
+        scale = args.n or 24
+        g = fu.Graph.rmat(scale, 16, seed=1)
+        desc = f"rmat:scale={scale},ef=16 collect-all generation-synchronous rounds"
     else:
-        g = fu.Graph.random_regular(args.n, 8, seed=1 + rank)
-        wl = f"rr:n={args.n},d=8 collect-all generation-synchronous rounds"
+        n = args.n or 65536
+        g = fu.Graph.random_regular(n, 8, seed=1)
+        desc = f"rr:n={n},d=8 collect-all generation-synchronous rounds"
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
-    print(f"[bench] graph {wl}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
-    layout = args.layout if args.layout != "auto" else ("degree" if args.workload == "rmat" else "given")
-    eng = fu.CollectAll(g, v, device=local, kernel=args.kernel, layout=layout)
-    if args.tile_edges:
-        eng.set_option("tile_edges", args.tile_edges)
-    if args.pack_every:
-        eng.set_option("pack_every", args.pack_every)
-    # with kernel "auto" the warmup rounds also pick the kernel for each packing width; run in
-    # chunks so the host sees each plan's width (an asynchronous copy) while the rounds run
-    # (a pass needs 9 rounds per candidate within one call)
+    print(f"[bench] graph {desc}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
+    layout = args.layout if args.layout != "auto" else ("degree" if wl == "rmat" else "given")
+    eng = fu.CollectAll(g, v, device=0, kernel=args.kernel, layout=layout)
+    t_setup = time.perf_counter()
+    if args.kernel == "auto":
+        eng.tune()  # untimed: one pass over the candidates at the unpacked width
+    # warmup in chunks: the host sees each packing plan's width between calls, so the
+    # autotuner also covers every width the warmup reaches (winners kept across fu_reset)
     for w0 in range(0, args.warmup, 64):
         eng.run(min(64, args.warmup - w0))
         eng.synchronize()
-    eng.reset()           # the timed region is rounds 0 .. steps-1 from the zero state
-    eng.synchronize()
+    eng.reset()
+    t_setup = time.perf_counter() - t_setup
 
-    # Timed in <= 10 chunks (HIP events on the engine's own stream) to show how the round
-    # time evolves: the packed estimate table engages as the estimates converge, and the
-    # autotuner re-runs (on real rounds, inside the timed region) when its width changes.
-    nchunk = min(10, args.steps)
-    bounds = [args.steps * k // nchunk for k in range(nchunk + 1)]
-    barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    chunk_ms, chunk_pack = [], []
-    for k in range(nchunk):
-        chunk_ms.append(eng.run_timed(bounds[k + 1] - bounds[k]))
-        chunk_pack.append(eng.pack_widths()[2])
-    eng.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    wall = allmax(t1 - t0)
-    kern_ms = allmax(sum(chunk_ms))
+    wall, dev_ms, b = timed_rounds(eng, args.steps)
     kinfo = eng.info()
-    phases = [{"rounds": [bounds[k], bounds[k + 1]],
-               "us_per_round": chunk_ms[k] * 1e3 / max(1, bounds[k + 1] - bounds[k]),
-               "pack_width_after": chunk_pack[k]} for k in range(nchunk)]
-
-    edges_total = g.E  # every rank has its own graph (seed 1 + rank): sum their edges
-    if dist is not None:
-        te = torch.tensor([float(g.E)], dtype=torch.float64)
-        dist.all_reduce(te)
-        edges_total = int(te.item())
-    value = edges_total * args.steps / wall
-    ms_per_step = wall * 1e3 / args.steps
-    # roofline of the dominant round kernel (one launch per round): its average launch time
-    # is the mean round time over the second half of the timed region, where the autotuned
-    # kernel runs alone (plus the packing plan every 16 rounds, so this is conservative);
-    # the whole-region average (incl. the unpacked early rounds and autotune passes) beside it
+    phases = [{"rounds": [b[k], b[k + 1]], "us_per_round": dev_ms[k] * 1e3 / max(1, b[k + 1] - b[k])}
+              for k in range(len(b) - 1)]
+    pack_after = eng.pack_widths()[2]
+    value = g.E * args.steps / wall
     alg_bytes = 24 * g.E + 28 * g.n
-    avg_round_s = kern_ms / 1e3 / args.steps
-    tail = phases[len(phases) // 2:]
-    dom_s = sum(p["us_per_round"] * (p["rounds"][1] - p["rounds"][0]) for p in tail) * 1e-6 / \
-        max(1, sum(p["rounds"][1] - p["rounds"][0] for p in tail))
-    achieved = alg_bytes / dom_s / 1e9
+    kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
+    roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, args.steps), round_kernels(kinfo))
 
-    # rounds to 1e-9 vs the per-component means (untimed)
-    rounds_to = None
-    final_err = None
-    if not args.no_conv:
+    rounds_to = final_err = n_comp = None
+    if not args.no_conv:  # rounds to 1e-9 vs the per-component means (untimed)
         tgt, comp = fu.component_means(g.rowptr, g.col, v)
         eng.reset()
         eng.set_targets(tgt)
@@ -198,87 +261,45 @@ def main():
         rounds_to = int(below[0]) + 1 if len(below) else None
         final_err = float(tr[-1])
         n_comp = int(comp.max()) + 1
-
-    out = None
-    if rank == 0:
-        cpu = None
-        if world == 1 and args.cpu_seconds > 0:
-            cpu = cpu_baseline(g, v, args.cpu_seconds)
-        traffic = None
-        pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc_path):
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            if pmc.get("n") == g.n and pmc.get("E") == g.E and pmc.get("kernel") == args.kernel and \
-                    pmc.get("kernel_selected") == kinfo["kernel"]:
-                traffic = pmc.get("bytes_per_launch")  # per round, all of the round's launches
-        out = {
-            "metric": "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error",
-            "value": value,
-            "unit": "edge-updates/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": ms_per_step,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f64",
-            "data": f"synthetic (seeded {args.workload} graph, U[0,100) values)",
-            "config": {
-                "workload": wl,
-                "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": "1+rank",
-                "value_seed": 0, "rounds_timed": args.steps, "kernel": args.kernel, "layout": layout,
-                "kernel_selected": kinfo["kernel"] + ("+nt" if kinfo["nt"] else ""),
-                "tile_selected": kinfo["tile"],
-                "autotune_passes": kinfo["tune_passes"],
-                "autotune_us_per_round": kinfo["tune_us_per_round"],
-                "autotune_winner_by_width": kinfo["tune_winner_by_width"],
-                "phases": phases,
-                "parallelism": "independent graph per GPU" if world > 1 else "single GPU",
-            },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": achieved,
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": achieved / HBM_PEAK_GBS,
-                "traffic": traffic,
-                "alg_bytes_per_launch": alg_bytes,
-                "kernel": round_kernels(kinfo),
-                "avg_launch_us": dom_s * 1e6,
-                "launch_window": "rounds %d-%d" % (tail[0]["rounds"][0], tail[-1]["rounds"][1]),
-                "whole_region_avg_round_us": avg_round_s * 1e6,
-                "whole_region_frac": alg_bytes / avg_round_s / 1e9 / HBM_PEAK_GBS,
-            },
-            "cpu_baseline": cpu,
-            "rounds_to_1e-9": rounds_to,
-            "err_after_conv_rounds": final_err,
-            "conv_rounds": args.conv_rounds,
-            "components": None if args.no_conv else n_comp,
-            "graph_gen_s": t_gen,
-        }
-        print(json.dumps(out), flush=True)
+    cpu = cpu_baseline(g, v, args.cpu_seconds) if args.cpu_seconds > 0 else None
+    out = {
+        "metric": METRIC, "value": value, "unit": "edge-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": f"synthetic (seeded {wl} graph, U[0,100) values)",
+        "config": {
+            "workload": desc, "n": g.n, "E_directed": g.E, "max_deg": g.max_deg, "graph_seed": 1,
+            "value_seed": 0, "rounds_timed": f"0-{args.steps - 1} from the zero state",
+            "kernel": args.kernel, "layout": layout, "kernel_selected": kname,
+            "tile_selected": kinfo["tile"], "autotune_passes": kinfo["tune_passes"],
+            "autotune_us_per_round": kinfo["tune_us_per_round"],
+            "autotune_winner_by_width": kinfo["tune_winner_by_width"],
+            "pack_width_after": pack_after, "setup_s": t_setup, "phases": phases,
+            "parallelism": "single GPU",
+        },
+        "roofline": roof, "cpu_baseline": cpu, "rounds_to_1e-9": rounds_to,
+        "err_after_conv_rounds": final_err, "conv_rounds": args.conv_rounds,
+        "components": n_comp, "graph_gen_s": t_gen,
+    }
+    print(json.dumps(out), flush=True)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
 
 
-def run_dist(args, world, rank, local, dist, barrier, allmax):
-    """BASELINE config 5 (weak scaling): RGG with --n nodes per GPU, one global graph split
-    into slabs (fu_part_gen_rgg, no rank builds the global graph), kernel 4 with the
-    estimates-only RCCL halo. value = all ranks' edge updates / max-over-ranks time."""
-    import fu  # noqa: F401
+def run_dist(args, world, rank, local, dist):
+    """BASELINE config 5 (weak scaling): RGG with --n nodes per GPU (2^23 by default), one
+    global graph cut into x-slabs (fu_part_gen_rgg: no rank builds the global graph), kernel 4
+    with the estimates-only RCCL halo. value = all ranks' edge updates / max-over-ranks time."""
+    import torch
+
     from fu.dist import DistCollectAll, RggPart, unique_id
 
-    n_total = args.n * world
+    per = args.n or (1 << 23)
+    n_total = per * world
     t = time.perf_counter()
     part = RggPart(n_total, avg_deg=8.0, seed=1, nparts=world, part=rank)
     v = part.values(seed=0)
     t_gen = time.perf_counter() - t
     if world > 1:
-        import torch
-
         buf = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             buf = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
@@ -286,56 +307,126 @@ def run_dist(args, world, rank, local, dist, barrier, allmax):
         uid = bytes(buf.tolist())
     else:
         uid = unique_id()
-    eng = DistCollectAll(part.to_plan(), v, uid, device=local, kernel="auto")
-    eng.run(args.warmup)
+    eng = DistCollectAll(part.to_plan(), v, uid, device=local, kernel=args.kernel)
+    if args.kernel == "auto":
+        eng.tune()  # collective: the same rounds on every rank
+    if args.warmup:
+        eng.run(args.warmup)
+    eng.reset()
     eng.synchronize()
-    barrier()
-    eng.synchronize()
-    t0 = time.perf_counter()
-    kern_ms = eng.run_timed(args.steps)
-    eng.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    wall = allmax(t1 - t0)
-    kern_ms = allmax(kern_ms)
-    e_tot = part.e_local
-    if dist is not None:
-        import torch
 
-        te = torch.tensor([float(part.e_local), float(part.n_local), float(part.n_ghost_a)],
-                          dtype=torch.float64)
-        dist.all_reduce(te)
-        e_tot = int(te[0].item())
-        n_tot, halo = int(te[1].item()), int(te[2].item())
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    wall, dev_ms, b = timed_rounds(eng, args.steps)
+    barrier()
+    t3 = torch.tensor([wall, sum(dev_ms[1:]), float(part.e_local), float(part.n_local),
+                       float(part.n_ghost_a)], dtype=torch.float64)
+    if dist is not None:
+        mx = t3[:2].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t3[2:].clone()
+        dist.all_reduce(sm)
+        wall, dev1 = float(mx[0]), float(mx[1])
+        e_tot, n_tot, halo = (int(x) for x in sm.tolist())
     else:
-        n_tot, halo = part.n_local, part.n_ghost_a
-    alg = 24 * e_tot + 28 * n_tot
+        dev1 = sum(dev_ms[1:])
+        e_tot, n_tot, halo = part.e_local, part.n_local, part.n_ghost_a
     kinfo = eng.info()
     if rank == 0:
-        avg_s = kern_ms / 1e3 / args.steps
-        achieved = alg / avg_s / 1e9 / world  # per GPU, against one GPU's peak
+        alg = (24 * e_tot + 28 * n_tot) // world  # per GPU, per round
+        r1 = dev1 / max(1, args.steps - 1)
+        achieved = alg / (r1 * 1e-3) / 1e9
         print(json.dumps({
-            "metric": "directed-edge flow updates/sec + % HBM roofline; rounds to 1e-9 error",
-            "value": e_tot * args.steps / wall, "unit": "edge-updates/s", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-            "data": "synthetic (seeded RGG, U[0,100) values)",
-            "config": {"workload": f"rgg-dist:n={n_total} ({args.n} per GPU), deg=8, slabs, "
-                                   "RCCL estimates-only halo", "E_directed": e_tot,
+            "metric": METRIC, "value": e_tot * args.steps / wall, "unit": "edge-updates/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded RGG, U[0,100) values)",
+            "config": {"workload": f"rgg-dist:n={n_total} ({per} per GPU), deg=8, x-slabs, "
+                                   "RCCL estimates-only halo every round",
+                       "n_total": n_total, "E_directed": e_tot,
+                       "rounds_timed": f"0-{args.steps - 1} from the zero state",
                        "kernel_selected": kinfo["kernel"], "tile_selected": kinfo["tile"],
                        "halo_estimates_per_round": halo, "parallelism": f"graph partition x{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                         "alg_bytes_per_launch": alg // world, "avg_launch_us": avg_s * 1e6},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "per_gpu": True,
+                         "alg_bytes_per_launch": alg, "avg_launch_us": r1 * 1e3,
+                         "launch_window": f"rounds 1-{args.steps - 1}, max over ranks (halo included)"},
             "cpu_baseline": None, "graph_gen_s": t_gen}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
 
 
+def pairwise_bytes(events, rowptr, tasks):
+    """Algorithmic bytes of a slice of replay events (per event type):
+    RECV 32 (message in 16, est + flow 16); FIRE_PW 8k + 56 (k flows summed, est, v, then
+    flow/est/last writes and a 16-B message out; 136 B at k = 8 with its receive);
+    FIRE_CA 48k + 16."""
+    kind = events[:, 0]
+    k_pw = events[kind == 2, 2].astype(np.int64)
+    k_ca = events[kind == 1, 1].astype(np.int64)
+    return int(32 * np.sum(kind == 0) + np.sum(8 * k_pw + 56) + np.sum(48 * k_ca + 16))
+
+
+def run_pairwise(args):
+    """BASELINE config 3: pairwise mode on a 64K-node random regular graph (d = 8), the
+    SimGrid event order (Peer.loop, mailbox rendez-vous; App. B) replayed on the GPU by the
+    persistent dataflow kernel. A step = one tick (PW:69-84 for every actor); the timed ticks
+    start after the 51-tick timeout that starts the exchanges (PW:86-91) and the warmup."""
+    import fu
+
+    n = args.n or 65536
+    g = fu.Graph.random_regular(n, 8, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    t0_tick = 51 + args.warmup
+    ticks = t0_tick + args.steps
+    t = time.perf_counter()
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", ticks, "rand:3")
+    t_build = time.perf_counter() - t
+    a = tr.arrays()
+    tto, tasks, ev = a["tick_task_off"], a["tasks"], a["events"]
+    e0, e1 = int(tasks[tto[t0_tick], 1]) if tto[t0_tick] < len(tasks) else len(ev), len(ev)
+    win = ev[e0:e1]
+    upd = int(np.sum(win[:, 0] == 2))
+    alg = pairwise_bytes(win, a["rowptr"], tasks)
+    rep = fu.Replay(tr, v, persistent=True)
+    rep.run(t0_tick)
+    t = time.perf_counter()
+    ms = rep.run_timed(ticks)
+    wall = time.perf_counter() - t
+    rep.close()
+    cpu = None
+    if args.cpu_seconds > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import coracle
+
+        t = time.perf_counter()
+        coracle.replay(a["rowptr"], v, tto, tasks, ev, a["out_ids"], tr.n_msgs)
+        dt = time.perf_counter() - t
+        upd_all = int(np.sum(ev[:, 0] == 2))
+        cpu = {"value": upd_all / dt, "unit": "flow-updates/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/fu_oracle.c replay of the same trace, all {ticks} ticks ({dt:.2f} s, 1 thread)"}
+    print(json.dumps({
+        "metric": METRIC, "value": upd / wall, "unit": "flow-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded random regular graph, U[0,100) values)",
+        "config": {"workload": f"pairwise tick replay: rr:n={n},d=8, tie order rand:3, ticks "
+                               f"{t0_tick}-{ticks - 1}, persistent dataflow kernel",
+                   "events": int(len(win)), "pairwise_updates": upd, "trace_build_s": t_build},
+        "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": alg, "kernel": "k_replay_persist",
+                     "avg_launch_us": ms * 1e3, "launch_window": f"one launch, {args.steps} ticks"},
+        "cpu_baseline": cpu}), flush=True)
+
+
 def cpu_baseline(g, v, seconds):
     """C port of the oracle (oracle/fu_oracle.c) on the host, 1 thread, bounded sample:
-    the same ER-1M graph and values, steady-state rounds, about `seconds` of CPU work."""
+    the same graph and values, steady-state rounds, about `seconds` of CPU work."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import coracle
 
@@ -360,13 +451,10 @@ def cpu_baseline(g, v, seconds):
     coracle.ca_rounds(g.rowptr, g.col, g.rev, v, rounds_mt, a, f, nthreads=mt)
     dt_mt = time.perf_counter() - t
     return {
-        "value": g.E * rounds / dt,
-        "unit": "edge-updates/s",
-        "cores": 1,
-        "cores_available": os.cpu_count(),
-        "kind": "port",
-        "sample": f"{rounds} steady-state collect-all rounds on the same ER-1M graph "
-                  f"({dt:.1f} s, oracle/fu_oracle.c, gcc -O2, single thread like SimGrid's DES)",
+        "value": g.E * rounds / dt, "unit": "edge-updates/s", "cores": 1,
+        "cores_available": os.cpu_count(), "kind": "port",
+        "sample": f"{rounds} collect-all rounds on the same graph ({dt:.1f} s, oracle/fu_oracle.c, "
+                  f"gcc -O2, single thread like SimGrid's DES)",
         "multicore": {"value": g.E * rounds_mt / dt_mt, "cores": mt,
                       "sample": f"{rounds_mt} rounds ({dt_mt:.1f} s), OpenMP across nodes"},
     }

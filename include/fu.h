@@ -132,6 +132,15 @@ int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *e
 /* Same, timed with HIP events on the handle's stream: *ms = elapsed device time of the
  * whole region (synchronises). */
 int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms);
+/* Kernel "auto": one autotune pass now, at the current packing width, on real rounds
+ * (1 warm + 8 timed per candidate, ~55 rounds; round 0 first if none ran). The rounds
+ * advance the state: call fu_reset before a run that must start from zero. The winner is
+ * kept across fu_reset. Synchronises. Lets a caller tune outside a timed region. */
+int fu_tune(fu_handle *h);
+/* Record HIP event `slot` (0..63) on the handle's stream (asynchronous). */
+int fu_mark(fu_handle *h, int32_t slot);
+/* *ms = device time between two recorded marks (waits for `to`). */
+int fu_mark_elapsed(fu_handle *h, int32_t from, int32_t to, float *ms);
 /* max_i |a_i - target_i| on the current estimates (synchronises). */
 int fu_max_err(fu_handle *h, double *out);
 /* Per-node estimate = last_avg (CA:114, CA:56-63). */

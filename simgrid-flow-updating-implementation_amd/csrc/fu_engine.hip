@@ -2512,6 +2512,7 @@ struct fu_handle {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
+  hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
@@ -3265,6 +3266,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                              h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
                              h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
       }
+#ifdef FU_DIAG
       if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
         hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
                            h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
@@ -3278,7 +3280,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
           hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 1>), dim3(h->st_ntiles), dim3(kBlock), 0,
                              h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
                              h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-      } else if (h->st_ntiles) {
+      } else
+#endif
+      if (h->st_ntiles) {
         if (check)
           hipLaunchKernelGGL((k_round_staged<true, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
                              h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
@@ -3363,6 +3367,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                   \
     else FU_RECON_G(C, N, D, 512, 64);                                                      \
   } while (0)
+#ifdef FU_DIAG
       if (h->diag == 1) FU_RECON(false, false, 1);
       else if (h->diag == 2) FU_RECON(false, false, 2);
       else if (h->diag == 3) FU_RECON(false, false, 3);
@@ -3370,7 +3375,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       else if (h->diag == 5) FU_RECON(false, false, 5);
       else if (h->diag == 6) FU_RECON(false, false, 6);
       else if (h->diag == 12) FU_RECON(false, false, 12);
-      else if (check) {
+      else
+#endif
+      if (check) {
         if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
       } else {
         if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
@@ -3682,9 +3689,14 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->pipe_bpc = (int)value;
     return FU_OK;
   }
-  if (!std::strcmp(key, "diag")) {
+  if (!std::strcmp(key, "diag")) {  // timing-only ablations (wrong results): tools builds only
+#ifdef FU_DIAG
     h->diag = (int)value;
     return FU_OK;
+#else
+    (void)value;
+    return fail(FU_ERR_ARG, "fu_set_option: 'diag' exists only in a -DFU_DIAG build (make DIAG=1)");
+#endif
   }
   if (!std::strcmp(key, "nt")) {
     h->nt = value != 0;
@@ -3805,7 +3817,9 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   const std::vector<TuneCand> cands = tune_cands(h);
   constexpr int kTimed = 8;
   auto active = [&](size_t c) {
-    return h->tune_out[c] < 2 && !(cands[c].kernel == 6 && width != 0) && !(h->dist && cands[c].kernel != 4);
+    // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
+    // candidate is dropped and none stops early on rank-local timings
+    return (h->dist || h->tune_out[c] < 2) && !(cands[c].kernel == 6 && width != 0) && !(h->dist && cands[c].kernel != 4);
   };
   int32_t need = 0;
   for (size_t c = 0; c < cands.size(); ++c) need += active(c) ? 1 + kTimed : 0;
@@ -3815,7 +3829,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   for (size_t c = 0; c < cands.size(); ++c) {
     // a candidate more than 1.3x slower than the winner in two passes sits out the later
     // ones (its last ns per round stays reported)
-    if (h->tune_out[c] >= 2) continue;
+    if (!h->dist && h->tune_out[c] >= 2) continue;
     h->tune_ms[c] = 0.f;
     if (!active(c)) continue;
     if (cands[c].kernel == 9) {
@@ -3843,7 +3857,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
-    if (best < 1e30f) {
+    if (best < 1e30f && !h->dist) {
       HIP_TRY(hipEventSynchronize(h->ev1));
       float wms = 0.f;
       HIP_TRY(hipEventElapsedTime(&wms, h->ev0, h->ev1));
@@ -3948,6 +3962,40 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
   HIP_TRY(hipEventElapsedTime(ms, h->ev2, h->ev3));
   return FU_OK;
   FU_TRY_END
+}
+
+int fu_tune(fu_handle *h) {
+  FU_TRY_BEGIN
+  if (!h) return fail(FU_ERR_ARG, "fu_tune: NULL handle");
+  if (!h->autotune) return fail(FU_ERR_STATE, "fu_tune: the kernel is pinned (option kernel != 0)");
+  if (int rc = set_device(h)) return rc;
+  if (h->rounds == 0)
+    if (int rc = launch_round(h, nullptr)) return rc;  // round 0 is not a tuning candidate
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  poll_pack_width(h);
+  const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
+  int32_t budget = INT32_MAX;
+  if (int rc = autotune_kernel(h, &budget, w)) return rc;
+  h->tuned_width = w;
+  return FU_OK;
+  FU_TRY_END
+}
+
+int fu_mark(fu_handle *h, int32_t slot) {
+  if (!h || slot < 0 || slot >= 64) return fail(FU_ERR_ARG, "fu_mark: slot must be in [0, 64)");
+  if (int rc = set_device(h)) return rc;
+  if (!h->marks[slot]) HIP_TRY(hipEventCreate(&h->marks[slot]));
+  HIP_TRY(hipEventRecord(h->marks[slot], h->stream));
+  return FU_OK;
+}
+
+int fu_mark_elapsed(fu_handle *h, int32_t from, int32_t to, float *ms) {
+  if (!h || !ms || from < 0 || from >= 64 || to < 0 || to >= 64 || !h->marks[from] || !h->marks[to])
+    return fail(FU_ERR_ARG, "fu_mark_elapsed: unrecorded slot");
+  if (int rc = set_device(h)) return rc;
+  HIP_TRY(hipEventSynchronize(h->marks[to]));
+  HIP_TRY(hipEventElapsedTime(ms, h->marks[from], h->marks[to]));
+  return FU_OK;
 }
 
 int fu_max_err(fu_handle *h, double *out) {
@@ -4097,6 +4145,8 @@ int fu_destroy(fu_handle *h) {
   if (h->ev2) hipEventDestroy(h->ev2);
   if (h->ev3) hipEventDestroy(h->ev3);
   if (h->ev_pw) hipEventDestroy(h->ev_pw);
+  for (hipEvent_t e : h->marks)
+    if (e) hipEventDestroy(e);
   if (h->ev_fork) hipEventDestroy(h->ev_fork);
   if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->h_pw) hipHostFree(h->h_pw);

@@ -64,6 +64,9 @@ _SIGS = {
     "fu_set_targets": ([vp, vp], ctypes.c_int),
     "fu_run_collectall": ([vp, i32, i32, vp], ctypes.c_int),
     "fu_run_collectall_timed": ([vp, i32, P(f32)], ctypes.c_int),
+    "fu_tune": ([vp], ctypes.c_int),
+    "fu_mark": ([vp, i32], ctypes.c_int),
+    "fu_mark_elapsed": ([vp, i32, i32, P(f32)], ctypes.c_int),
     "fu_max_err": ([vp, P(f64)], ctypes.c_int),
     "fu_get_estimates": ([vp, vp], ctypes.c_int),
     "fu_get_flows": ([vp, vp], ctypes.c_int),

@@ -238,6 +238,21 @@ class DistCollectAll:
         L.call("fu_run_collectall_timed", self._h, int(rounds), ctypes.byref(ms))
         return float(ms.value)
 
+    def tune(self):
+        """One autotune pass (collective: every rank calls it; same rounds on each)."""
+        L.call("fu_tune", self._h)
+
+    def reset(self):
+        L.call("fu_reset", self._h)
+
+    def mark(self, slot: int):
+        L.call("fu_mark", self._h, int(slot))
+
+    def elapsed(self, a: int, b: int) -> float:
+        ms = L.f32()
+        L.call("fu_mark_elapsed", self._h, int(a), int(b), ctypes.byref(ms))
+        return float(ms.value)
+
     def set_targets(self, target_local):
         self._target = np.ascontiguousarray(target_local, dtype=np.float64)
         L.call("fu_set_targets", self._h, L.ptr(self._target))

@@ -112,6 +112,21 @@ class CollectAll:
         L.call("fu_run_collectall_timed", self._h, int(rounds), ctypes.byref(ms))
         return float(ms.value)
 
+    def tune(self):
+        """One autotune pass now (kernel "auto"), outside any timed region: ~55 real rounds
+        at the current packing width; the state advances, so reset() before a timed run."""
+        L.call("fu_tune", self._h)
+
+    def mark(self, slot: int):
+        """Record HIP event `slot` (0..63) on the engine's stream (asynchronous)."""
+        L.call("fu_mark", self._h, int(slot))
+
+    def elapsed(self, a: int, b: int) -> float:
+        """Device milliseconds between marks a and b (waits for b)."""
+        ms = L.f32()
+        L.call("fu_mark_elapsed", self._h, int(a), int(b), ctypes.byref(ms))
+        return float(ms.value)
+
     def max_err(self) -> float:
         out = L.f64()
         L.call("fu_max_err", self._h, ctypes.byref(out))

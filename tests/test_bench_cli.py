@@ -1,0 +1,50 @@
+"""bench.py's multi-GPU contract, on the CPU: `--gpus N` without a launcher starts N rank
+processes itself, and a node with fewer visible GPUs than ranks is an error (never a silent
+one-GPU line). Also the timed-region chunking and the pairwise byte model."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_gpus2_forks_two_ranks_and_fails_without_gpus():
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                        "--warmup", "0", "--no-conv", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode != 0
+    assert "[bench] rank 0/2" in p.stderr and "[bench] rank 1/2" in p.stderr
+    assert "need 2 GPU(s), 0 visible" in p.stderr
+    assert '"metric"' not in p.stdout  # no JSON line for GPUs that do not exist
+
+
+def test_world_size_must_match_gpus():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "2"],
+                       capture_output=True, text=True, timeout=120, env=env, cwd=ROOT)
+    assert p.returncode == 2 and "WORLD_SIZE=1 but --gpus 4" in p.stderr
+
+
+@pytest.mark.parametrize("steps", [1, 2, 5, 20, 1000])
+def test_chunk_bounds(steps):
+    b = bench.chunk_bounds(steps)
+    assert b[0] == 0 and b[-1] == steps and all(x < y for x, y in zip(b, b[1:]))
+    if steps > 1:
+        assert b[1] == 1  # round 0 timed alone
+        assert len(b) - 2 <= (1 if steps <= 100 else 10)
+
+
+def test_pairwise_bytes_model():
+    # RECV, FIRE_PW over 8 flows, FIRE_CA over 3 neighbours
+    ev = np.array([[0, 1, 5, 0], [2, 1, 8, 7], [1, 3, 0, 0]], dtype=np.int32)
+    assert bench.pairwise_bytes(ev, None, None) == 32 + (8 * 8 + 56) + (48 * 3 + 16)
+    # receive + pairwise fire at degree 8 = SURVEY §8(d)'s 136 B per exchange (+16 B of state)
+    assert 32 + 8 * 8 + 56 == 152
