@@ -253,8 +253,9 @@ int fu_dist_unique_id(uint8_t *id_out /* FU_UNIQUE_ID_BYTES */);
  *     order that peer stores them in its ghost flow slots;
  *   recv_f_off[nranks+1]: ghost flow slots per peer (contiguous, peer order);
  *   send_a_off / send_a_idx, recv_a_off: the same for estimates of boundary nodes.
- * rev == NULL (with n_ghost_f = 0 and an empty flow plan) = estimates-only halo: kernel 4
- * rebuilds flows locally, so only boundary estimates move; kernels 1-3 are refused. */
+ * The round kernels rebuild the neighbours' flows from estimates (flow reconstruction), so
+ * the halo carries estimates only: rev must be NULL, n_ghost_f 0 and the flow plan empty
+ * (send_f_off / recv_f_off all zero; the parameters stay for ABI stability). */
 int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                    const int32_t *col, const int32_t *rev, const double *value,
                    int32_t n_ghost_a, int64_t n_ghost_f, int32_t nranks, int32_t rank,
@@ -262,6 +263,19 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                    const int64_t *recv_f_off, const int64_t *send_a_off,
                    const int32_t *send_a_idx, const int64_t *recv_a_off,
                    const uint8_t *unique_id, int32_t device, fu_handle **out);
+
+/* Test transport (one process, e.g. all ranks on one GPU): the same rank handle without a
+ * communicator. After each round the handle packs its boundary estimates; the caller runs
+ * one round on every rank, then fu_dist_exchange_local(hs, nranks) copies the packed slots
+ * into the peers' ghost slots (device copies, the order RCCL uses). The error all-reduce is
+ * left to the caller. This exercises the ghost-slot reads of the round kernels and the pack
+ * kernel without a multi-GPU box. */
+int fu_dist_create_local(int32_t n_local, int64_t e_local, const int64_t *rowptr,
+                         const int32_t *col, const double *value, int32_t n_ghost_a,
+                         int32_t nranks, int32_t rank, const int64_t *send_a_off,
+                         const int32_t *send_a_idx, const int64_t *recv_a_off, int32_t device,
+                         fu_handle **out);
+int fu_dist_exchange_local(fu_handle **hs, int32_t nranks);
 
 /* Partition-aware random geometric graph: rank `part` of `nparts` generates only its slab
  * of cell columns (plus the two halo columns) of the graph fu_graph_gen_rgg(n_total, radius,

@@ -65,242 +65,11 @@ __device__ inline void block_max_to(unsigned long long x, unsigned long long *ds
 // ------------------------------------------------------------------------------------
 // Round 0: the timeout fire on zero state (CA:33-34, CA:87-91 -> CA:105-128)
 // ------------------------------------------------------------------------------------
-// SPLIT: kernels >= 4 keep flows as split words (see st_f); kernels 1-3 as doubles
-template <bool SPLIT>
 __global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict__ rowptr,
-                                                   const double *__restrict__ v,
-                                                   double *__restrict__ f,
-                                                   double *__restrict__ a) {
-  int i = blockIdx.x * kBlock + threadIdx.x;
+                                                   const double *__restrict__ v, double *__restrict__ a) {
+  const int i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  int b = rowptr[i], e = rowptr[i + 1];
-  double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
-  a[i] = ai;
-  double fv = (0.0 + ai) - 0.0;
-  if constexpr (!SPLIT)
-    for (int k = b; k < e; ++k) f[k] = fv;  // kernels 1-3 (split flows: k_round0_flows)
-}
-
-// Round 0's flows of kernels >= 4, one thread per edge (a hub's row is not one thread's
-// loop): f[k] = (0.0 + a_0[row of k]) - 0.0 (CA:117 on zero state), split words.
-__global__ __launch_bounds__(kBlock) void k_round0_flows(int n, long long E, const int *__restrict__ rowptr,
-                                                         const double *__restrict__ a, double *__restrict__ f) {
-  const long long k = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (k >= E) return;
-  int lo = 0, hi = n - 1;  // row i with rowptr[i] <= k < rowptr[i + 1] (non-empty rows only)
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (rowptr[mid] <= k) lo = mid; else hi = mid - 1;
-  }
-  const double fv = (0.0 + a[lo]) - 0.0;
-  unsigned *w = reinterpret_cast<unsigned *>(f);
-  const long long j = ((k & ~31LL) << 1) | (k & 31);
-  w[j] = (unsigned)__double2hiint(fv);
-  w[j + 32] = (unsigned)__double2loint(fv);
-}
-
-// ------------------------------------------------------------------------------------
-// Variant 1: one thread per node, gathers straight from global memory
-// ------------------------------------------------------------------------------------
-template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void k_round_tpn(
-    int n, const int *__restrict__ rowptr, const int *__restrict__ col,
-    const int *__restrict__ rev, const double *__restrict__ v,
-    const double *__restrict__ f_old, const double *__restrict__ a_old,
-    double *__restrict__ f_new, double *__restrict__ a_new,
-    const double *__restrict__ target, unsigned long long *__restrict__ err) {
-  int i = blockIdx.x * kBlock + threadIdx.x;
-  unsigned long long eb = 0;
-  if (i < n) {
-    int b = rowptr[i], e = rowptr[i + 1];
-    double S = 0.0, T = 0.0;
-    for (int k = b; k < e; ++k) {
-      S = S + (-f_old[rev[k]]);
-      T = T + a_old[col[k]];
-    }
-    double a = ((v[i] - S) + T) / (double)(e - b + 1);
-    a_new[i] = a;
-    for (int k = b; k < e; ++k) f_new[k] = ((-f_old[rev[k]]) + a) - a_old[col[k]];
-    if (CHECK) eb = err_bits(a, target[i]);
-  }
-  if (CHECK) block_max_to(eb, err);
-}
-
-// ------------------------------------------------------------------------------------
-// Variant 2: LDS tiles. A light tile = a contiguous node range with <= kTileNodes nodes
-// and <= kTileEdges edges. Its edges are gathered edge-parallel into LDS (coalesced
-// col/rev, independent gathers), then each node sums its row sequentially from LDS, and
-// the new flows are written edge-parallel (coalesced). A heavy tile = one node with more
-// than hub_threshold edges. The whole block gathers it in chunks, and wave 0 keeps the
-// exact left-to-right sum in a lane-uniform dependency chain (bitwise parity for hubs).
-// tiles[t] = {node_begin, node_end}; node_end < 0 marks a heavy tile (node = begin).
-// ------------------------------------------------------------------------------------
-template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void k_round_tile(
-    const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
-    const int *__restrict__ col, const int *__restrict__ rev, const double *__restrict__ v,
-    const double *__restrict__ f_old, const double *__restrict__ a_old,
-    double *__restrict__ f_new, double *__restrict__ a_new,
-    const double *__restrict__ target, unsigned long long *__restrict__ err) {
-  __shared__ double s_fr[kTileEdges];
-  __shared__ double s_er[kTileEdges];
-  __shared__ unsigned char s_own[kTileEdges];
-  __shared__ int s_rp[kTileNodes + 1];
-  __shared__ double s_a[kTileNodes];
-  const int t = threadIdx.x;
-  const int4 tl = tiles[blockIdx.x];
-  unsigned long long eb = 0;
-
-  if (tl.y < 0) {
-    // ---------------- heavy node: block-chunked gather, wave-0 sequential chain ----------
-    const int i = tl.x;
-    const int b = rowptr[i], e = rowptr[i + 1];
-    double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += kTileEdges) {
-      const int cn = min(kTileEdges, e - c0);
-      for (int q = t; q < cn; q += kBlock) {
-        s_fr[q] = -f_old[rev[c0 + q]];
-        s_er[q] = a_old[col[c0 + q]];
-      }
-      __syncthreads();
-      if (t < 64) {
-        for (int q = 0; q < cn; ++q) {  // lane-uniform LDS broadcast reads
-          S = S + s_fr[q];
-          T = T + s_er[q];
-        }
-      }
-      __syncthreads();
-    }
-    if (t == 0) {
-      double a = ((v[i] - S) + T) / (double)(e - b + 1);
-      s_a[0] = a;
-      a_new[i] = a;
-      if (CHECK) eb = err_bits(a, target[i]);
-    }
-    __syncthreads();
-    const double a = s_a[0];
-    for (int k = b + t; k < e; k += kBlock) f_new[k] = ((-f_old[rev[k]]) + a) - a_old[col[k]];
-    if (CHECK) block_max_to(eb, err);
-    return;
-  }
-
-  // ---------------- light tile ----------------
-  const int nb = tl.x, nn = tl.y - tl.x;
-  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
-  __syncthreads();
-  const int e0 = s_rp[0];
-  const int ne = s_rp[nn] - e0;
-#pragma unroll 4
-  for (int q = t; q < ne; q += kBlock) {
-    const int k = e0 + q;
-    s_fr[q] = -f_old[rev[k]];
-    s_er[q] = a_old[col[k]];
-  }
-  if (t < nn) {
-    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
-  }
-  __syncthreads();
-  if (t < nn) {
-    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
-    double S = 0.0, T = 0.0;
-    for (int q = qb; q < qe; ++q) {
-      S = S + s_fr[q];
-      T = T + s_er[q];
-    }
-    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
-    s_a[t] = a;
-    a_new[nb + t] = a;
-    if (CHECK) eb = err_bits(a, target[nb + t]);
-  }
-  __syncthreads();
-  for (int q = t; q < ne; q += kBlock) f_new[e0 + q] = (s_fr[q] + s_a[s_own[q]]) - s_er[q];
-  if (CHECK) block_max_to(eb, err);
-}
-
-// ------------------------------------------------------------------------------------
-// Variant 3: push / inbox. Message (flow, estimate) from j to i lives at i's own row slot
-// for j (the FlowUpdatingMsg of CA:121, stored where its receiver reads it). A node reads
-// its inbox row contiguously and scatters its new messages to inbox_new[rev[e]]. No col
-// and no random reads; one random 16-byte store per directed edge.
-// ------------------------------------------------------------------------------------
-template <bool CHECK>
-__global__ __launch_bounds__(kBlock) void k_round_push(
-    const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
-    const int *__restrict__ rev, const double *__restrict__ v,
-    const double2 *__restrict__ in_old, double2 *__restrict__ in_new,
-    double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err) {
-  __shared__ double2 s_m[kTileEdges];
-  __shared__ unsigned char s_own[kTileEdges];
-  __shared__ int s_rp[kTileNodes + 1];
-  __shared__ double s_a[kTileNodes];
-  const int t = threadIdx.x;
-  const int4 tl = tiles[blockIdx.x];
-  unsigned long long eb = 0;
-
-  if (tl.y < 0) {
-    const int i = tl.x;
-    const int b = rowptr[i], e = rowptr[i + 1];
-    double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += kTileEdges) {
-      const int cn = min(kTileEdges, e - c0);
-      for (int q = t; q < cn; q += kBlock) s_m[q] = in_old[c0 + q];
-      __syncthreads();
-      if (t < 64) {
-        for (int q = 0; q < cn; ++q) {
-          const double2 m = s_m[q];
-          S = S + (-m.x);
-          T = T + m.y;
-        }
-      }
-      __syncthreads();
-    }
-    if (t == 0) {
-      double a = ((v[i] - S) + T) / (double)(e - b + 1);
-      s_a[0] = a;
-      a_new[i] = a;
-      if (CHECK) eb = err_bits(a, target[i]);
-    }
-    __syncthreads();
-    const double a = s_a[0];
-    for (int k = b + t; k < e; k += kBlock) {
-      const double2 m = in_old[k];
-      in_new[rev[k]] = make_double2(((-m.x) + a) - m.y, a);
-    }
-    if (CHECK) block_max_to(eb, err);
-    return;
-  }
-
-  const int nb = tl.x, nn = tl.y - tl.x;
-  for (int q = t; q <= nn; q += kBlock) s_rp[q] = rowptr[nb + q];
-  __syncthreads();
-  const int e0 = s_rp[0];
-  const int ne = s_rp[nn] - e0;
-  for (int q = t; q < ne; q += kBlock) s_m[q] = in_old[e0 + q];
-  if (t < nn) {
-    for (int q = s_rp[t] - e0; q < s_rp[t + 1] - e0; ++q) s_own[q] = (unsigned char)t;
-  }
-  __syncthreads();
-  if (t < nn) {
-    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
-    double S = 0.0, T = 0.0;
-    for (int q = qb; q < qe; ++q) {
-      const double2 m = s_m[q];
-      S = S + (-m.x);
-      T = T + m.y;
-    }
-    const double a = ((v[nb + t] - S) + T) / (double)(qe - qb + 1);
-    s_a[t] = a;
-    a_new[nb + t] = a;
-    if (CHECK) eb = err_bits(a, target[nb + t]);
-  }
-  __syncthreads();
-  for (int q = t; q < ne; q += kBlock) {
-    const double2 m = s_m[q];
-    const double a = s_a[s_own[q]];
-    in_new[rev[e0 + q]] = make_double2(((-m.x) + a) - m.y, a);
-  }
-  if (CHECK) block_max_to(eb, err);
+  a[i] = ((v[i] - 0.0) + 0.0) / (double)(rowptr[i + 1] - rowptr[i] + 1);
 }
 
 // ------------------------------------------------------------------------------------
@@ -467,6 +236,43 @@ __device__ __forceinline__ void st_f_full(double *F, int e, double v) {
   st_wt(w + i, (unsigned)__double2hiint(v));
 }
 
+// Round 0's flows, one thread per edge: f_0[e] = (0.0 + a_0[row]) - 0.0 into F[0]
+// (CA:117 on zero state) and f_{-1} = -0.0 into F[1], so that round 1's reconstruction
+// reproduces (0.0 + a) - 0.0 (split words). A block owns kR0E consecutive edges: the host
+// listed the row of every block's first edge (blk_row), the block's rows' pointers go to
+// LDS, and each edge's row is a short binary search there (a hub's edges all land in one
+// row; a block whose rows span more than kR0E, runs of isolated nodes, searches rowptr).
+constexpr int kR0E = 1024;
+__global__ __launch_bounds__(kBlock) void k_round0_flows(long long E, const int *__restrict__ rowptr,
+                                                         const int *__restrict__ blk_row,
+                                                         const double *__restrict__ a, double *__restrict__ F0,
+                                                         double *__restrict__ F1) {
+  __shared__ int s_r[2];
+  __shared__ int s_rp[kR0E + 1];
+  const long long e0 = (long long)blockIdx.x * kR0E;
+  const int t = threadIdx.x;
+  if (t < 2) s_r[t] = blk_row[blockIdx.x + t];  // rows holding edges e0 and e0 + kR0E (host)
+  __syncthreads();
+  const int r0 = s_r[0], span = s_r[1] - s_r[0] + 1;
+  const bool lds = span <= kR0E;
+  if (lds)
+    for (int q = t; q <= span; q += kBlock) s_rp[q] = rowptr[r0 + q];
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kR0E / kBlock; ++u) {
+    const long long k = e0 + t + u * kBlock;
+    if (k < E) {
+      int lo = 0, hi = span - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if ((lds ? s_rp[mid] : rowptr[r0 + mid]) <= k) lo = mid; else hi = mid - 1;
+      }
+      st_f_full(F0, (int)k, (0.0 + a[r0 + lo]) - 0.0);
+      st_f_full(F1, (int)k, -0.0);
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------
 // Variant 4: flow reconstruction ("recon"). Node j computed, in round r-1,
 //     f_{r-1}[j->i] = ((-f_{r-2}[i->j]) + a_{r-1}[j]) - a_{r-2}[i]        (CA:99, CA:117)
@@ -528,175 +334,6 @@ __device__ __forceinline__ void chain_sum(const double *xs, const double *es, in
   T = __shfl(acc, 1);
 }
 
-// ------------------------------------------------------------------------------------
-// Mega hubs: the exact left-to-right sums of avg_and_send (CA:106, CA:110) in parallel.
-// Python's sum is the chain s_{k+1} = fl(s_k + x_k) from s_0 = 0: inherently sequential,
-// and one wave running it for a 406K-edge R-MAT hub needs ~3 ms per round. The chain is
-// decomposed instead (host prototype and adversarial checks: tools/exact_scan_proto.c):
-//   * an approximate prefix p_k (any summation order) gives a speculative key of s_{k+1}:
-//     its ulp exponent ue (u = 2^ue) and sign;
-//   * a step whose key differs from the previous step's is a BOUNDARY: it is done later as
-//     one exact fp64 add in a short serial pass;
-//   * every other step keeps s a multiple of u, so s_{k+1} = u (m_k + t_k) with
-//     t_k = round(x_k / u), ties to the even m_k + t_k: t_k depends on m_k only through its
-//     parity. A step is a 2-state transducer (t0, t1, q0, q1); compositions stay in that form,
-//     plus the min / max of the partial increments, so a RUN of such steps is one RunSum;
-//   * the serial pass walks pieces of 2048 elements: head run, then per boundary its exact
-//     add and the run after it, VERIFYING each run in O(1): every result must satisfy
-//     2^52 < |m| < 2^53 (the exact sum was inside the binade, so fl rounded at u). A piece
-//     that fails (speculation wrong, > kMaxBnd boundaries, zeros / subnormals) is redone
-//     element by element. The result is the chain's bits in every case.
-// ------------------------------------------------------------------------------------
-constexpr int kPieceT = 8;                // elements per thread
-constexpr int kPiece = kBlock * kPieceT;  // elements per piece (one block)
-constexpr int kMaxBnd = 32;               // boundaries listed per piece and chain
-constexpr int kKeySpecial = -1000000;     // zero, subnormal, inf, nan
-constexpr long long kRunLim = 1LL << 56;  // |t|, |mn|, |mx| bound of a verifiable run
-
-struct RunSum {
-  long long t0, t1, mn, mx;  // increment for start parity 0 / 1; min / max partial increment
-  int len, q;                // steps; q bit0 / bit1 = end parity for start parity 0 / 1, bit2 = bad
-};
-struct BndSum {
-  double x;  // the boundary element
-  int key, pad;
-  RunSum run;  // the run after it (up to the next boundary or the piece end)
-};
-struct PieceSum {
-  int first_key, nb, pad0, pad1;  // key the head run assumes; boundaries (> kMaxBnd: dense)
-  RunSum head;
-  BndSum b[kMaxBnd];
-  long long pad_end;
-};
-static_assert(sizeof(PieceSum) % 16 == 0, "PieceSum is copied in 16-byte words");
-constexpr int kPieceWords = (int)(sizeof(PieceSum) / 16);
-
-__device__ __forceinline__ int ulp_key(double x) {
-  const unsigned long long b = (unsigned long long)__double_as_longlong(x);
-  const int E = (int)((b >> 52) & 0x7ff);
-  return (E == 0 || E == 0x7ff) ? kKeySpecial : ((E - 1075) * 2) | (int)(b >> 63);
-}
-__device__ __forceinline__ RunSum run_id() { return RunSum{0, 0, 0, 0, 0, 2}; }
-__device__ __forceinline__ RunSum run_cat(const RunSum &a, const RunSum &b) {  // a, then b
-  if (b.len == 0) return a;
-  if (a.len == 0) return b;
-  const int a0 = a.q & 1, a1 = (a.q >> 1) & 1, b0 = b.q & 1, b1 = (b.q >> 1) & 1;
-  RunSum r;
-  r.t0 = a.t0 + (a0 ? b.t1 : b.t0);
-  r.t1 = a.t1 + (a1 ? b.t1 : b.t0);
-  // b's partial increments start at a.t0 or a.t1: conservative bounds over both
-  r.mn = min(a.mn, min(a.t0, a.t1) + b.mn);
-  r.mx = max(a.mx, max(a.t0, a.t1) + b.mx);
-  r.len = a.len + b.len;
-  r.q = (a0 ? b1 : b0) | ((a1 ? b1 : b0) << 1) | ((a.q | b.q) & 4);
-  // |values| <= 2^56 in, <= 2^57 out: no overflow; a run that large can never verify
-  if (r.mn < -kRunLim || r.mx > kRunLim) r.q |= 4;
-  return r;
-}
-__device__ __forceinline__ RunSum run_step(double x, int ue) {
-  const double y = ldexp(x, -ue);  // exact (a power-of-two scaling)
-  RunSum r;
-  r.len = 1;
-  if (!(fabs(y) < 0x1p54)) {  // the result cannot stay in the binade
-    r.t0 = r.t1 = r.mn = r.mx = 0;
-    r.q = 2 | 4;
-    return r;
-  }
-  const double fl = floor(y), fr = y - fl;  // both exact
-  const long long f = (long long)fl;
-  long long t0, t1;
-  if (fr < 0.5) t0 = t1 = f;
-  else if (fr > 0.5) t0 = t1 = f + 1;
-  else {  // tie: the even m + t
-    t0 = (f & 1) ? f + 1 : f;
-    t1 = (f & 1) ? f : f + 1;
-  }
-  r.t0 = t0;
-  r.t1 = t1;
-  r.mn = min(t0, t1);
-  r.mx = max(t0, t1);
-  r.q = (int)(t0 & 1) | ((int)((t1 + 1) & 1) << 1);
-  return r;
-}
-// Applies a run to m (units 2^ue), verifying every result stays strictly inside the binade.
-__device__ __forceinline__ bool run_apply(const RunSum &r, long long &m) {
-  if (r.len == 0) return true;
-  if (r.q & 4) return false;
-  constexpr long long lo = 1LL << 52, hi = 1LL << 53;
-  if (m > 0) {
-    if (!(m + r.mn > lo && m + r.mx < hi)) return false;
-  } else {
-    if (!(m + r.mx < -lo && m + r.mn > -hi)) return false;
-  }
-  m += (m & 1) ? r.t1 : r.t0;
-  return true;
-}
-__device__ __forceinline__ long long key_m(double s, int key) {
-  return key == kKeySpecial ? 0 : (long long)ldexp(s, -(key >> 1));
-}
-
-// Serial pass of one chain over pieces [p0, p1) of a hub (one wave, lane-uniform). buf:
-// this wave's LDS buffer (a PieceSum, reused as 64 doubles by the element-wise fallback).
-// comp: 0 = fr (S), 1 = er (T); xy: the hub's (fr, er) pairs; d: its degree.
-__device__ double hub_serial_pass(const PieceSum *__restrict__ hsum, int p0, int p1, int comp,
-                                  const double2 *__restrict__ xy, int d, PieceSum *buf,
-                                  unsigned long long *__restrict__ redo) {
-  const int lane = threadIdx.x & 63;
-  double s = 0.0;
-  int key = kKeySpecial;
-  long long m = 0;
-  const int4 *src = reinterpret_cast<const int4 *>(hsum);
-  int4 *dst = reinterpret_cast<int4 *>(buf);
-  int4 w0 = make_int4(0, 0, 0, 0), w1 = w0;
-  auto fetch = [&](int p) {
-    const int4 *q = src + ((size_t)p * 2 + comp) * kPieceWords;
-    w0 = q[lane];
-    if (lane + 64 < kPieceWords) w1 = q[lane + 64];
-  };
-  if (p0 < p1) fetch(p0);
-  for (int p = p0; p < p1; ++p) {
-    wave_sync();
-    dst[lane] = w0;
-    if (lane + 64 < kPieceWords) dst[lane + 64] = w1;
-    wave_sync();
-    if (p + 1 < p1) fetch(p + 1);
-    const double s0 = s;
-    const int nb = buf->nb;
-    bool ok = nb <= kMaxBnd;
-    if (ok && buf->head.len) {
-      ok = key != kKeySpecial && key == buf->first_key && run_apply(buf->head, m);
-      if (ok) s = ldexp((double)m, key >> 1);
-    }
-    for (int j = 0; ok && j < nb; ++j) {
-      s = s + buf->b[j].x;  // the boundary step: one exact fp64 add
-      key = ulp_key(s);
-      m = key_m(s, key);
-      if (buf->b[j].run.len) {
-        ok = key != kKeySpecial && key == buf->b[j].key && run_apply(buf->b[j].run, m);
-        if (ok) s = ldexp((double)m, key >> 1);
-      }
-    }
-    if (!ok) {  // element by element from the piece start (64 at a time through LDS)
-      if (lane == 0) atomicAdd(redo, 1ull);
-      s = s0;
-      double *xs = reinterpret_cast<double *>(buf);
-      const int kb = (p - p0) * kPiece, ke = min(d, kb + kPiece);
-      for (int c0 = kb; c0 < ke; c0 += 64) {
-        const int k = c0 + lane;
-        const double2 v2 = k < ke ? xy[k] : make_double2(0.0, 0.0);
-        wave_sync();
-        xs[lane] = comp ? v2.y : v2.x;
-        wave_sync();
-        const int cn = min(64, ke - c0);
-        for (int q = 0; q < cn; ++q) s = s + xs[q];
-      }
-      key = ulp_key(s);
-      m = key_m(s, key);
-    }
-  }
-  return s;
-}
-
 template <typename T>
 __device__ inline T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);
@@ -715,11 +352,10 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
     const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, const int *__restrict__ perm,
+    unsigned long long *__restrict__ err,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
-    const int *__restrict__ hrows, const PieceSum *__restrict__ hsum, const int *__restrict__ hub_p0,
-    unsigned long long *__restrict__ hub_redo, int hub_sep) {
+    const int *__restrict__ hrows, int hub_sep) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -733,92 +369,6 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   const int4 tl = tiles[blockIdx.x];
   unsigned long long eb = 0;
 
-  if constexpr (PART != 1 && TE == kTileEdges && TN == kTileNodes) {
-  if (tl.y == -2) {
-    // ---------------- degree bin: R rows of similar degree, one chain per row ----------
-    // Rows perm[tl.x .. tl.x + R) (sorted by degree, longest first). Each iteration stages
-    // C = TE / R positions of every row in LDS, loaded along row segments (coalesced).
-    // Then thread r runs row r's exact left-to-right chain over its C values. Element
-    // (r, k) lives at r*C + (k ^ sw(r)): the XOR swizzle keeps the column reads of the
-    // chain conflict-free without padding.
-    const int R = tl.z, C = tl.w;
-    const int lgC = 31 - __clz(C);
-    // LDS reuse (no extra footprint): node ids and degrees in s_own's 2 KB, row starts in
-    // s_rp, a_{r-2} of each row in s_a until the chains end, then a_r.
-    int *s_node = reinterpret_cast<int *>(s_own);
-    int *s_deg = s_node + kBlock;
-    int *s_rb = s_rp;
-    double *s_own2 = s_a;
-    if (t < R) {
-      const int node = perm[tl.x + t];
-      s_node[t] = node;
-      const int rb = rowptr[node];
-      s_rb[t] = rb;
-      s_deg[t] = rowptr[node + 1] - rb;
-      s_own2[t] = a_prev2[node];
-    }
-    __syncthreads();
-    auto sw = [&](int r) { return C >= 32 ? (r & 31) : ((r >> (5 - lgC)) & (C - 1)); };
-    const int maxd = s_deg[0];
-    const int my_deg = t < R ? s_deg[t] : 0;
-    double S = 0.0, T = 0.0;
-    for (int c0 = 0; c0 < maxd; c0 += C) {
-#pragma unroll 4
-      for (int q = t; q < R * C; q += kBlock) {
-        const int r = q >> lgC, k = q & (C - 1);
-        if (c0 + k < s_deg[r]) {
-          const int e = s_rb[r] + c0 + k;
-          const double er = ld_est(pp, code_prev, a_prev, col[e]);
-          const int slot = (r << lgC) + (k ^ sw(r));
-          s_x[slot] = recon_fr(ld_f(F, e), er, s_own2[r]);
-          s_er[slot] = er;
-        }
-      }
-      __syncthreads();
-      if (t < R) {
-        const int kend = min(C, my_deg - c0);
-        const int base = t << lgC, x = sw(t);
-        for (int k = 0; k < kend; ++k) {
-          S = S + s_x[base + (k ^ x)];
-          T = T + s_er[base + (k ^ x)];
-        }
-      }
-      __syncthreads();
-    }
-    double a_mine = 0.0;
-    if (t < R) {
-      const int node = s_node[t];
-      a_mine = ((v[node] - S) + T) / (double)(my_deg + 1);
-      st_wt(a_new + node, a_mine);
-      if (pc.width) put_code(pc, code_new, node, a_mine);
-      if (CHECK) eb = err_bits(a_mine, target[node]);
-    }
-    __syncthreads();  // every read of s_own2 (aliases s_a) is done
-    if (t < R) s_a[t] = a_mine;
-    __syncthreads();
-    if (maxd <= C) {  // one iteration: fr and er are still in LDS
-      for (int q = t; q < R * C; q += kBlock) {
-        const int r = q >> lgC, k = q & (C - 1);
-        if (k < s_deg[r]) {
-          const int slot = (r << lgC) + (k ^ sw(r));
-          st_f_full(F, s_rb[r] + k, (s_x[slot] + s_a[r]) - s_er[slot]);
-        }
-      }
-    } else {  // long rows: re-read the flow, re-gather the estimate (L2-warm)
-      for (int r = 0; r < R; ++r) {
-        const int rb = s_rb[r], d = s_deg[r];
-        const double own2 = a_prev2[s_node[r]], a = s_a[r];
-        for (int k = t; k < d; k += kBlock) {
-          const double er = ld_est(pp, code_prev, a_prev, col[rb + k]);
-          const double fo = ld_f(F, rb + k);
-          st_f(F, rb + k, (recon_fr(fo, er, own2) + a) - er, fo);
-        }
-      }
-    }
-    if (CHECK) block_max_to(eb, err);
-    return;
-  }
-  }  // if constexpr (default geometry)
 
   if constexpr (PART != 1) {  // heavy tiles (PART 1: light tiles only, 64 VGPRs)
   if (tl.y == -4) {
@@ -903,22 +453,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int d = e - b;
     double S = 0.0, T = 0.0;
     constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
-    if (hsum) {
-      // parallel exact sums: k_hub_sum summarised the pieces; wave 0 runs the serial pass
-      // of S, wave 1 that of T, each in its own LDS buffer
-      static_assert(2 * sizeof(PieceSum) <= sizeof(double) * TE, "LDS for the serial pass");
-      PieceSum *bufs = reinterpret_cast<PieceSum *>(s_x);
-      if (t < 128 && DIAG != 5) {
-        const double r = hub_serial_pass(hsum, hub_p0[blockIdx.x], hub_p0[blockIdx.x + 1], t >> 6, xy, d,
-                                         bufs + (t >> 6), hub_redo);
-        if ((t & 63) == 0) s_a[t >> 6] = r;
-      }
-      __syncthreads();
-      S = s_a[0];
-      T = s_a[1];
-      if (DIAG == 5) S = T = 0.0;
-      __syncthreads();
-    } else if (t < 64) {
+    if (t < 64) {
       double2 nx[PL];
 #pragma unroll
       for (int u = 0; u < PL; ++u) nx[u] = t + 64 * u < d ? xy[t + 64 * u] : make_double2(0.0, 0.0);
@@ -1104,279 +639,143 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 }
 
 // ------------------------------------------------------------------------------------
-// Variant 7: kernel 4's light tiles at WAVE granularity ("wave"). Same arithmetic and
-// state as kernel 4 (flow reconstruction, packed gathers); each 64-lane wave owns one tile
-// of <= TN nodes / <= TE edges and its own LDS slice, so there is no block barrier: a wave
-// that finishes its loads proceeds without waiting for the other three, and more tiles are
-// in flight per CU. Phase C keeps each edge's er and f_{r-2} in the registers that loaded
-// them. Heavy rows (degree > min(hub_threshold, TE)) run through kernel 4's heavy path in
-// a separate launch before this one.
-// ------------------------------------------------------------------------------------
-
-__device__ inline void wave_max_to(unsigned long long x, unsigned long long *dst) {
-  for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long y = __shfl_xor(x, off, 64);
-    x = x > y ? x : y;
-  }
-  if ((threadIdx.x & 63) == 0 && x && x > __hip_atomic_load(dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(dst, x);
-}
-
-template <bool CHECK, int TE, int TN>
-__global__ __launch_bounds__(kBlock) void k_round_wave(
-    const int4 *__restrict__ wtiles, int nwt, const int *__restrict__ rowptr,
-    const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
-    const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
-    double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, const void *__restrict__ code_prev,
-    void *__restrict__ code_new, PackCtl *__restrict__ ctl, int rslot) {
-  static_assert(TE % 64 == 0 && TN <= 64 && TE <= 512, "wave tile geometry");
-  constexpr int kW = kBlock / 64;
-  constexpr int kPer = TE / 64;
-  __shared__ double s_x[kW][TE];   // f_{r-2}, then fr after phase B
-  __shared__ double s_er[kW][TE];  // a_{r-1}[col e]
-  __shared__ unsigned short s_own[kW][TE];
-  __shared__ int s_rp[kW][TN + 1];
-  __shared__ double s_a[kW][TN];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const PackCtl pp = ctl[rslot ^ 1];
-  const PackCtl pc = ctl[2];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
-  const int tile = blockIdx.x * kW + w;
-  if (tile >= nwt) return;  // no block barrier below: waves are independent
-  const int4 tl = wtiles[tile];
-  const int nb = tl.x, nn = tl.y - tl.x;
-  const int e0 = tl.z, ne = tl.w - tl.z;
-  int c[kPer];
-  double x[kPer], g[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = lane + k * 64;
-    c[k] = q < ne ? col[e0 + q] : 0;
-    x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
-  }
-  const int rp = lane <= nn ? rowptr[nb + lane] : 0;
-  const int rp_last = (TN == 64 && lane == 0 && nn == 64) ? rowptr[nb + 64] : 0;
-  const double vv = lane < nn ? v[nb + lane] : 0.0;
-  const double own2 = lane < nn ? a_prev2[nb + lane] : 0.0;
-  if (pp.width == 0) {
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? a_prev[c[k]] : 0.0;
-  } else {
-    unsigned cd[kPer];
-    if (pp.width == 8) {
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<8>(code_prev, c[k]) : 0u;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<8>(cd[k], pp.base, a_prev, c[k]) : 0.0;
-    } else if (pp.width == 16) {
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<16>(code_prev, c[k]) : 0u;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<16>(cd[k], pp.base, a_prev, c[k]) : 0.0;
-    } else {
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) cd[k] = lane + k * 64 < ne ? ld_code<32>(code_prev, c[k]) : 0u;
-#pragma unroll
-      for (int k = 0; k < kPer; ++k) g[k] = lane + k * 64 < ne ? decode_or<32>(cd[k], pp.base, a_prev, c[k]) : 0.0;
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = lane + k * 64;
-    if (q < ne) {
-      s_x[w][q] = x[k];
-      s_er[w][q] = g[k];
-    }
-  }
-  if (lane <= nn && lane <= TN) s_rp[w][lane] = rp;
-  if (TN == 64 && lane == 0 && nn == 64) s_rp[w][64] = rp_last;
-  wave_sync();
-  // phase B: one lane per node, its row in order (CA:106-113)
-  unsigned long long eb = 0;
-  if (lane < nn) {
-    const int qb = s_rp[w][lane] - e0, qe = s_rp[w][lane + 1] - e0;
-    double S = 0.0, T = 0.0;
-    for (int q = qb; q < qe; ++q) {
-      const double er = s_er[w][q];
-      const double fr = recon_fr(s_x[w][q], er, own2);
-      s_x[w][q] = fr;
-      s_own[w][q] = (unsigned short)lane;
-      S = S + fr;
-      T = T + er;
-    }
-    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
-    s_a[w][lane] = a;
-    st_wt(a_new + nb + lane, a);
-    if (pc.width) put_code(pc, code_new, nb + lane, a);
-    if (CHECK) eb = err_bits(a, target[nb + lane]);
-  }
-  wave_sync();
-  // phase C: new flows, coalesced, in place (CA:117-118); er from the loading registers
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = lane + k * 64;
-    if (q < ne) st_f(F, e0 + q, (s_x[w][q] + s_a[w][s_own[w][q]]) - g[k], x[k]);
-  }
-  if (CHECK) wave_max_to(eb, err);
-}
-
-// ------------------------------------------------------------------------------------
-// Variant 8: LDS-staged slices ("stage"). The a_{r-1}[col e] gather is the part of a round
+// Kernel 8, "stage": LDS-staged slices. The a_{r-1}[col e] gather is the part of a round
 // that does not stream: on ER every gather is a random L2 request (8 M per round), and the
-// fp64 table (8 MB) does not fit an XCD's 4 MB L2. Kernel 8 splits it into two launches:
+// fp64 table (8 MB) does not fit an XCD's 4 MB L2. Kernel 8 splits a round into two launches:
 //   * k_stage: the estimate table (codes, or doubles while unpacked) is cut into slices of
-//     64 KB; a block copies slice s into LDS, then streams the slice-s column offsets of its
-//     edge groups (u16) and writes the looked-up table elements to G, in the same
-//     (group, slice, tile, position) order: coalesced reads and writes, gathers from LDS.
-//   * k_round_staged: kernel 4's light tile (flow reconstruction, CA:98-99 + CA:105-128),
-//     where each edge's estimate comes from G (contiguous runs of the tile) through a u32
-//     {index in the group's G region, position in the tile} instead of col + gather.
-// The layout depends on the table's element width (slice = 65536 / bytes nodes). The host
-// builds it for the width it last saw; a table wider than the layout is still handled (the
-// stage launch gathers it from global memory), so correctness never depends on the host's
-// view of the device-side packing plan. Rows above the tile limit run as kernel 4 heavy
-// tiles in a launch of their own. Results are bitwise those of kernel 4.
+//     128 KB. A block copies slice s into LDS, then streams a contiguous range of the
+//     slice's column offsets (u16) and writes the looked-up elements to G: coalesced reads,
+//     16-byte lane-contiguous stores, random accesses only in LDS. G is slice-major: slice
+//     s's region holds, tile by tile, the edges whose neighbour lies in slice s.
+//   * k_round_staged: kernel 4's light tile (flow reconstruction, CA:98-99 + CA:105-128)
+//     where each edge's estimate comes from G: the tile's edges of one slice are one
+//     contiguous run of G, found through a u16 {position in the tile, run} per edge and
+//     the tile's per-run offsets.
+// One layout per table element width (1, 2, 4, 8 bytes; slice = 128 KB / width nodes). The
+// device picks the layout from the table's actual packing width; a table wider than the
+// layout is read from global memory by the stage launch, so correctness never depends on
+// the host's view of the asynchronous packing plan. Rows above the tile limit run as
+// kernel 4 heavy tiles in a launch of their own. Results are bitwise those of kernel 4.
 // ------------------------------------------------------------------------------------
-constexpr int kStageThreads = 512;
-constexpr int kStageLds = 65536;  // bytes of table per slice
+constexpr int kStageThreads = 1024;   // one block per CU (the slice takes 128 KB of its LDS)
+constexpr int kStageLds = 131072;     // bytes of table per slice
 constexpr int kStageTE = 1024, kStageTN = 128;
+constexpr int kStageU = 4;            // steps per lane in flight
+constexpr int kStageRuns = 64;        // slice runs per tile the u16 index can address
 
-// The slice layouts (element bytes 1, 2, 4, 8) passed by value to the stage and round
-// launches; the device picks the layout from the table's actual packing width, so the
-// choice never depends on the host having seen the (asynchronous) packing plan.
 struct StageArgs {
-  int P[4], Q[4];
-  const int *aoff[4];
-  const int2 *aitem[4];
-  const unsigned short *colS[4];
-  const unsigned *sidx[4];
-  const int *gbase[4];
-  const unsigned short *sidx16[4];  // compact sidx (null: use sidx)
-  const int *dtab[4];
-  int sel[4];  // layout used for tables of width 8, 16, 32, 0 (0..3)
+  int P[4], Q[4], SN[4], NB[4];        // slices, blocks per slice, nodes per slice, blocks
+  const int4 *brange[4];               // per stage block: {begin, end} in G, slice, 0
+  const unsigned short *colS[4];       // per G element: column offset in its slice (pads: 0)
+  const unsigned short *sidx16[4];     // per light-tile edge, slice order: position | run << 10
+  const int *dtab[4];                  // per light tile: kStageRuns x (G index - m) of each run
+  int sel[4];                          // layout used for tables of width 8, 16, 32, 0
 };
-constexpr int kStageRuns = 64;  // slice runs per tile the compact sidx can address
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
 }
 
-constexpr int kStagePad = 8;      // segment padding: 8 consecutive elements per lane access
-constexpr int kStageItem = 1024;  // elements per stage item (one wave: 2 x 8 per lane)
-constexpr int kStageIU = kStageItem / (64 * kStagePad);
-constexpr int kStageChunk = 256;  // item descriptors staged in LDS at a time
-
-// One stage item (<= 1024 consecutive elements of one padded segment, one wave): lane l
-// loads the column offsets of elements x + 8 (l + 64 u) .. + 7 with one 16-byte load each.
-template <typename T>
-__device__ __forceinline__ void stage_item_load(uint4 (&o)[kStageIU], int2 itm, int lane,
-                                                const unsigned short *__restrict__ colS) {
-#pragma unroll
-  for (int u = 0; u < kStageIU; ++u) {
-    const int k = itm.x + kStagePad * (lane + 64 * u);
-    o[u] = *reinterpret_cast<const uint4 *>(colS + (k < itm.x + itm.y ? k : itm.x));
+// EPL consecutive u16 column offsets (EPL = 16 / sizeof(T): one 16-byte G store per lane)
+template <int EPL>
+struct ColVec {
+  uint4 w[EPL > 8 ? 2 : 1];
+};
+template <int EPL>
+__device__ __forceinline__ void ld_cols(ColVec<EPL> &c, const unsigned short *p) {
+  if constexpr (EPL == 2) c.w[0].x = *reinterpret_cast<const unsigned *>(p);
+  else if constexpr (EPL == 4) {
+    const uint2 v = *reinterpret_cast<const uint2 *>(p);
+    c.w[0].x = v.x;
+    c.w[0].y = v.y;
+  } else if constexpr (EPL == 8) c.w[0] = *reinterpret_cast<const uint4 *>(p);
+  else {
+    c.w[0] = reinterpret_cast<const uint4 *>(p)[0];
+    c.w[1] = reinterpret_cast<const uint4 *>(p)[1];
   }
 }
+template <int EPL>
+__device__ __forceinline__ unsigned col_at(const ColVec<EPL> &c, int j) {
+  const unsigned w = (&c.w[j >> 3].x)[(j >> 1) & 3];
+  return (j & 1) ? w >> 16 : w & 0xFFFFu;
+}
+
+// One batch: kStageU steps of EPL elements per lane, all column loads first (caller), then
+// the LDS (or global) lookups and one 16-byte store per step.
 template <typename T, bool LDS>
-__device__ __forceinline__ void stage_item_store(const uint4 (&o)[kStageIU], int2 itm, int lane,
-                                                 const unsigned char *s_tab, const T *__restrict__ tab,
-                                                 int nb, T *__restrict__ G) {
+__device__ __forceinline__ void stage_load(ColVec<16 / sizeof(T)> (&c)[kStageU], int g, int g1,
+                                           const unsigned short *__restrict__ colS) {
+  constexpr int EPL = 16 / sizeof(T), STEP = kStageThreads * EPL;
 #pragma unroll
-  for (int u = 0; u < kStageIU; ++u) {
-    const int k = itm.x + kStagePad * (lane + 64 * u);
-    const unsigned w4[4] = {o[u].x, o[u].y, o[u].z, o[u].w};
-    T val[kStagePad];
+  for (int u = 0; u < kStageU; ++u)
+    if (g + u * STEP < g1) ld_cols<EPL>(c[u], colS + g + u * STEP);
+}
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_put(const ColVec<16 / sizeof(T)> (&c)[kStageU], int g, int g1,
+                                          const unsigned char *s_tab, const T *__restrict__ tab, int nb,
+                                          T *__restrict__ G) {
+  constexpr int EPL = 16 / sizeof(T), STEP = kStageThreads * EPL;
 #pragma unroll
-    for (int j = 0; j < kStagePad; ++j) {
-      const unsigned off = (w4[j >> 1] >> (16 * (j & 1))) & 0xFFFFu;
-      if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
-      else val[j] = tab[nb + (int)off];
-    }
-    if (k < itm.x + itm.y) {  // 8 consecutive elements, 16-byte aligned stores
-      if constexpr (sizeof(T) == 1) {
-        uint2 v;
-        v.x = val[0] | (val[1] << 8) | (val[2] << 16) | ((unsigned)val[3] << 24);
-        v.y = val[4] | (val[5] << 8) | (val[6] << 16) | ((unsigned)val[7] << 24);
-        *reinterpret_cast<uint2 *>(G + k) = v;
-      } else if constexpr (sizeof(T) == 2) {
-        uint4 v;
-        v.x = val[0] | ((unsigned)val[1] << 16);
-        v.y = val[2] | ((unsigned)val[3] << 16);
-        v.z = val[4] | ((unsigned)val[5] << 16);
-        v.w = val[6] | ((unsigned)val[7] << 16);
-        *reinterpret_cast<uint4 *>(G + k) = v;
-      } else {
+  for (int u = 0; u < kStageU; ++u) {
+    const int gg = g + u * STEP;
+    if (gg < g1) {
+      T val[EPL];
 #pragma unroll
-        for (int j = 0; j < kStagePad; j += 16 / (int)sizeof(T)) {
-          uint4 v;
-          __builtin_memcpy(&v, &val[j], 16);
-          *reinterpret_cast<uint4 *>(G + k + j) = v;
-        }
+      for (int j = 0; j < EPL; ++j) {
+        const unsigned off = col_at<EPL>(c[u], j);
+        if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
+        else val[j] = tab[nb + (int)off];
       }
+      uint4 w;
+      __builtin_memcpy(&w, val, 16);
+      *reinterpret_cast<uint4 *>(G + gg) = w;
     }
   }
 }
 
-// One stage block: slice s of the table (element type T) -> LDS (LDS = false: read from
-// global memory, the table being wider than the layout), then its items, wave w taking
-// items ib + w, ib + w + 8, ... Every load of an item is issued before any of its uses, and
-// the next item's loads are issued before the current item is looked up and stored
-// (two register sets, unrolled by two so no in-flight register is copied).
+// Slice s of the table (element type T) -> LDS (LDS = false: the table is wider than the
+// layout and is read from global memory), then the block's G range [g0, g1), software
+// pipelined: the next batch's column loads are issued before the current batch is looked
+// up and stored (two register sets, so no in-flight register is copied).
 template <typename T, bool LDS>
-__device__ __forceinline__ void stage_body(unsigned char *s_tab, int2 *s_items, int nb, int cnt,
-                                           const int2 *__restrict__ items, int ib, int ie,
+__device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt, int g0, int g1,
                                            const unsigned short *__restrict__ colS,
                                            const T *__restrict__ tab, T *__restrict__ G) {
+  constexpr int EPL = 16 / (int)sizeof(T), BSTEP = kStageU * kStageThreads * EPL;
   constexpr int kW = kStageLds / 16 / kStageThreads;
-  constexpr int NW = kStageThreads / 64;
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int t = threadIdx.x;
   uint4 buf[kW];
   const int bytes = LDS ? cnt * (int)sizeof(T) : 0;
   const int w16 = bytes >> 4;
-  const uint4 *s16 = reinterpret_cast<const uint4 *>(tab + nb);
   if constexpr (LDS) {
+    const uint4 *s16 = reinterpret_cast<const uint4 *>(tab + nb);
 #pragma unroll
     for (int u = 0; u < kW; ++u) {
       const int k = t + u * kStageThreads;
       buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  const int2 z = make_int2(0, 0);
-  bool filled = !LDS;
-  // the block's item descriptors go through LDS in chunks of kStageChunk (one chunk on
-  // ER-1M), so a wave never waits on a descriptor load behind its own column loads
-  for (int cb = ib; cb < ie || !filled; cb += kStageChunk) {
-    const int ce = min(ie, cb + kStageChunk);
-    if (cb > ib) __syncthreads();  // previous chunk consumed
-    for (int i = t; i < ce - cb; i += kStageThreads) s_items[i] = items[cb + i];
-    __syncthreads();
-    int it = w;
-    const int nit = ce - cb;
-    int2 i0 = it < nit ? s_items[it] : z;
-    uint4 o0[kStageIU], o1[kStageIU];
-    stage_item_load<T>(o0, i0, lane, colS);
-    if (!filled) {  // slice stores after the first item's loads are in flight
+  ColVec<EPL> ca[kStageU], cb[kStageU];
+  int g = g0 + t * EPL;
+  stage_load<T, LDS>(ca, g, g1, colS);
+  if constexpr (LDS) {  // slice stores after the first batch's loads are in flight
 #pragma unroll
-      for (int u = 0; u < kW; ++u) {
-        const int k = t + u * kStageThreads;
-        if (k < w16) reinterpret_cast<uint4 *>(s_tab)[k] = buf[u];
-      }
-      const int tb = w16 << 4;
-      if (t < bytes - tb) s_tab[tb + t] = reinterpret_cast<const unsigned char *>(tab + nb)[tb + t];
-      __syncthreads();
-      filled = true;
+    for (int u = 0; u < kW; ++u) {
+      const int k = t + u * kStageThreads;
+      if (k < w16) reinterpret_cast<uint4 *>(s_tab)[k] = buf[u];
     }
-    while (it < nit) {
-      const int2 i1 = it + NW < nit ? s_items[it + NW] : z;
-      stage_item_load<T>(o1, i1, lane, colS);
-      stage_item_store<T, LDS>(o0, i0, lane, s_tab, tab, nb, G);
-      it += NW;
-      if (it >= nit) break;
-      i0 = it + NW < nit ? s_items[it + NW] : z;
-      stage_item_load<T>(o0, i0, lane, colS);
-      stage_item_store<T, LDS>(o1, i1, lane, s_tab, tab, nb, G);
-      it += NW;
-    }
+    const int tb = w16 << 4;
+    if (t < bytes - tb) s_tab[tb + t] = reinterpret_cast<const unsigned char *>(tab + nb)[tb + t];
+    __syncthreads();
+  }
+  for (;;) {
+    if (g >= g1) break;
+    stage_load<T, LDS>(cb, g + BSTEP, g1, colS);
+    stage_put<T, LDS>(ca, g, g1, s_tab, tab, nb, G);
+    g += BSTEP;
+    if (g >= g1) break;
+    stage_load<T, LDS>(ca, g + BSTEP, g1, colS);
+    stage_put<T, LDS>(cb, g, g1, s_tab, tab, nb, G);
+    g += BSTEP;
   }
 }
 
@@ -1386,30 +785,26 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         const PackCtl *__restrict__ ctl, int rslot,
                                                         void *__restrict__ G) {
   __shared__ __align__(16) unsigned char s_tab[kStageLds];
-  __shared__ int2 s_items[kStageChunk];
   const PackCtl pp = ctl[rslot ^ 1];
   const int wb = pp.width ? pp.width / 8 : 8;  // bytes per element of the table gathered
   const int li = sa.sel[width_index(pp.width)];
-  const int P = sa.P[li];
-  if ((int)blockIdx.x >= P * sa.Q[li]) return;
+  if ((int)blockIdx.x >= sa.NB[li]) return;
+  const int4 rg = sa.brange[li][blockIdx.x];
+  if (rg.x >= rg.y) return;  // no slice here (grid rounded to whole XCD rows) or empty region
   const int LB = 1 << li;  // bytes per element the layout was built for
-  const int SN = kStageLds >> li;
-  const int s = blockIdx.x % P;
-  const int nb = s * SN;
+  const int SN = sa.SN[li];
+  const int nb = rg.z * SN;
   const int cnt = min(SN, n - nb);
   const void *src = pp.width ? code_prev : static_cast<const void *>(a_prev);
   const unsigned short *colS = sa.colS[li];
-  const int2 *aitem = sa.aitem[li];
-  // this block's items {first element, count <= kStageItem}
-  const int ib = sa.aoff[li][blockIdx.x], ie = sa.aoff[li][blockIdx.x + 1];
-#define FU_BODY(T)                                                                                  \
-  do {                                                                                              \
-    if ((int)sizeof(T) <= LB)                                                                       \
-      stage_body<T, true>(s_tab, s_items, nb, cnt, aitem, ib, ie, colS, reinterpret_cast<const T *>(src), \
-                          reinterpret_cast<T *>(G));                                                \
-    else                                                                                            \
-      stage_body<T, false>(s_tab, s_items, nb, cnt, aitem, ib, ie, colS, reinterpret_cast<const T *>(src), \
-                           reinterpret_cast<T *>(G));                                               \
+#define FU_BODY(T)                                                                                    \
+  do {                                                                                                \
+    if ((int)sizeof(T) <= LB)                                                                         \
+      stage_body<T, true>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),         \
+                          reinterpret_cast<T *>(G));                                                  \
+    else                                                                                              \
+      stage_body<T, false>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),        \
+                           reinterpret_cast<T *>(G));                                                 \
   } while (0)
   if (wb == 1) FU_BODY(unsigned char);
   else if (wb == 2) FU_BODY(unsigned short);
@@ -1423,7 +818,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
 // the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
 template <bool CHECK, int TE, int TN, int DIAG = 0>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
-    const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
+    const int4 *__restrict__ tiles, int ntl,
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const StageArgs sa, const void *__restrict__ G, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
@@ -1431,9 +826,9 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     unsigned long long *__restrict__ err, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot) {
   static_assert(TE % kBlock == 0 && TN <= kBlock, "tile geometry");
+  static_assert(TE <= 1024, "the u16 staged index holds a 10-bit tile position");
   const PackCtl pp = ctl[rslot ^ 1];
   const int lsel = sa.sel[width_index(pp.width)];
-  const unsigned *__restrict__ sidx = sa.sidx[lsel];
   const PackCtl pc = ctl[2];
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
   __shared__ double s_x[TE];
@@ -1443,20 +838,19 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   __shared__ double s_a[TN];
   const int t = threadIdx.x;
   unsigned long long eb = 0;
-  // XCD-aware order: block b runs on XCD b % 8; consecutive tiles (one edge group, whose G
-  // region the tiles share) go to the same XCD, so that region is fetched into one L2
+  // XCD-aware order: block b runs on XCD b % 8; consecutive tiles go to the same XCD, so
+  // the G runs that neighbouring tiles share in every slice region meet in one L2
   const int xcd = blockIdx.x & 7, per = ntl >> 3, rem = ntl & 7;
   const int tile = DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3);
   const int4 tl = tiles[tile];
-  const int gb = sa.gbase[lsel][tile];
   const int nb = tl.x, nn = tl.y - tl.x;
   const int e0 = tl.z, ne = tl.w - tl.z;
   constexpr int kPer = TE / kBlock;
   const unsigned short *__restrict__ s16 = sa.sidx16[lsel];
-  unsigned si[kPer];  // position in the tile (low 16 bits) | G index in the group (high 16)
+  unsigned si[kPer];  // position in the tile
   double x[kPer], g[kPer];
   int gi[kPer];
-  if (s16) {  // compact: u16 position | run << 10; G index = gbase + m + D[run] (lane run holds D)
+  {  // u16 position | run << 10; G index = m + D[run] (lane `run` holds D)
     const int dl = sa.dtab[lsel][(size_t)tile * kStageRuns + (t & 63)];
     unsigned short c16[kPer];
 #pragma unroll
@@ -1470,18 +864,8 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
       const int q = t + k * kBlock;
       const int dd = __shfl(dl, (int)(c16[k] >> 10));
       si[k] = c16[k] & 1023u;
-      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : gb + q + dd) : -1;
+      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : q + dd) : -1;
     }
-  } else {
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int q = t + k * kBlock;
-      si[k] = q < ne ? sidx[e0 + q] : 0u;
-      x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k)
-      gi[k] = t + k * kBlock < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + t + k * kBlock : gb + (int)(si[k] >> 16)) : -1;
   }
   const int rp = t <= nn ? rowptr[nb + t] : 0;
   const double vv = t < nn ? v[nb + t] : 0.0;
@@ -1549,287 +933,6 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   if (CHECK) block_max_to(eb, err);
 }
 
-// ------------------------------------------------------------------------------------
-// Variant 9: persistent, software-pipelined round ("pipe"). Kernels 4 and 8 run one tile
-// per block through load -> gather -> LDS -> row chains -> store, so a block's memory
-// latency is exposed once per tile and the chip runs short of bytes in flight (kernel 4
-// without its gather still only streams 5.4 TB/s). Here a block owns a list of light tiles
-// (1024 edges / 128 nodes, on its XCD) and keeps two of them ahead of the one it computes:
-// while tile i is staged in LDS and summed, the estimate loads of tile i+1 and the stream
-// loads (edges, flows, node arrays) of tile i+2 are in flight. LDS is double-buffered by
-// tile parity, so two barriers per tile suffice. Rows above the tile limit (hubs) get
-// blocks of their own at the front of the grid (kernel 4's exact chunked chain).
-// MODE 0: per edge col -> a_{r-1}[col] (or its packed code); MODE 1: the staged runs of
-// kernel 8 (sidx -> G). Arithmetic identical to kernel 4 (CA:98-99, CA:105-128).
-// ------------------------------------------------------------------------------------
-constexpr int kPipeTE = 1024, kPipeTN = 128, kPipeKP = kPipeTE / kBlock;
-constexpr int kPipeChunk = 64;  // max tiles per block (host sizes the grid accordingly)
-
-struct PipeStream {
-  int nb, nn, e0, ne, gb;
-  unsigned c[kPipeKP];  // MODE 0: col; MODE 1: sidx
-  double x[kPipeKP];    // f_{r-2}
-  int rp;
-  double vv, own2;
-};
-
-// Every load of the pipeline is unconditional, with indices clamped into the arrays, so
-// the loop body is straight-line code and the compiler can wait for exactly the loads an
-// instruction consumes (a guarded load makes it fall back to waiting for all of them,
-// prefetches included). Lanes past the tile read valid but unused elements.
-template <int MODE>
-__device__ inline void pipe_load(PipeStream &s, int it, int m, const int4 *s_tl, const int *s_gb,
-                                 const int *__restrict__ rowptr, const unsigned *__restrict__ cidx,
-                                 const double *__restrict__ F, const double *__restrict__ v,
-                                 const double *__restrict__ a_prev2, int elast) {
-  const int t = threadIdx.x;
-  const int itc = it < m ? it : 0;
-  const int4 tl = s_tl[itc];
-  const bool live = it < m;
-  s.nb = tl.x;
-  s.nn = live ? tl.y - tl.x : -1;
-  s.e0 = tl.z;
-  s.ne = live ? tl.w - tl.z : 0;
-  s.gb = MODE ? s_gb[itc] : 0;
-#pragma unroll
-  for (int k = 0; k < kPipeKP; ++k) {
-    const int e = min(s.e0 + t + k * kBlock, elast);
-    s.c[k] = cidx[e];
-    s.x[k] = ld_f(F, e);
-  }
-  const int nn = tl.y - tl.x;
-  s.rp = rowptr[s.nb + min(t, nn)];
-  const int i = s.nb + min(t, max(nn - 1, 0));
-  s.vv = v[i];
-  s.own2 = a_prev2[i];
-}
-
-// raw estimate words of one tile (W = 0: the double's bits; else the W-bit code)
-template <int MODE, int W>
-__device__ inline void pipe_gather(unsigned long long (&raw)[kPipeKP], const PipeStream &s,
-                                   const void *__restrict__ tab, const double *__restrict__ a_prev) {
-#pragma unroll
-  for (int k = 0; k < kPipeKP; ++k) {
-    const int gi = MODE ? s.gb + (int)(s.c[k] >> 16) : (int)s.c[k];
-    if constexpr (W == 0) raw[k] = reinterpret_cast<const unsigned long long *>(MODE ? tab : a_prev)[gi];
-    else if constexpr (W == 8) raw[k] = reinterpret_cast<const unsigned char *>(tab)[gi];
-    else if constexpr (W == 16) raw[k] = reinterpret_cast<const unsigned short *>(tab)[gi];
-    else raw[k] = reinterpret_cast<const unsigned *>(tab)[gi];
-  }
-}
-
-struct PipeLds {
-  double x[2][kPipeTE];
-  double er[2][kPipeTE];
-  unsigned char own[2][kPipeTE];
-  int rp[2][kPipeTN + 1];
-  double a[2][kPipeTN];
-  int4 tl[kPipeChunk];
-  int gb[kPipeChunk];
-};
-
-// One pipeline step: compute tile `it` (stream registers sa, estimate words ga) while the
-// estimates of tile it+1 (stream sb, into gb) and the stream of tile it+2 (into sc) load.
-// The caller unrolls the step over the 3 x 2 register sets (period 6), so no register is
-// ever copied while a load into it is in flight (a copy would wait for that load).
-template <bool CHECK, int MODE, int W>
-__device__ inline void pipe_step(
-    PipeLds &L, int it, int m, PipeStream &sa, const PipeStream &sb, PipeStream &sc,
-    unsigned long long (&ga)[kPipeKP], unsigned long long (&gb)[kPipeKP], unsigned long long &eb,
-    const int *__restrict__ rowptr, const int *__restrict__ col, const unsigned *__restrict__ cidx,
-    const void *__restrict__ tab, const double *__restrict__ v, double *__restrict__ F,
-    const double *__restrict__ a_prev, const double *__restrict__ a_prev2, double *__restrict__ a_new,
-    const double *__restrict__ target, void *__restrict__ code_new, const PackCtl &pp,
-    const PackCtl &pc, int elast) {
-  constexpr int KP = kPipeKP;
-  const int t = threadIdx.x;
-  const int bf = it & 1;
-  pipe_gather<MODE, W>(gb, sb, tab, a_prev);                                       // tile it+1
-  pipe_load<MODE>(sc, it + 2, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);  // tile it+2
-  bool any_esc = false;
-#pragma unroll
-  for (int k = 0; k < KP; ++k) {
-    const int q = t + k * kBlock;
-    double er;
-    if constexpr (W == 0) {
-      er = __longlong_as_double((long long)ga[k]);
-    } else {
-      constexpr unsigned long long esc = W == 32 ? 0xFFFFFFFFull : (1ull << W) - 1ull;
-      er = dkey_inv(pp.base + ga[k]);
-      any_esc |= q < sa.ne && ga[k] == esc;
-    }
-    if (q < sa.ne) {
-      L.x[bf][q] = sa.x[k];
-      L.er[bf][MODE ? (int)(sa.c[k] & 0xFFFFu) : q] = er;
-    }
-  }
-  if constexpr (W != 0) {
-    // escapes (rare): the double, through the edge's column, written over the LDS slot. The
-    // load completes inside the branch (explicit wait), so the common path never waits for
-    // it, and with it for every prefetch issued before it.
-    if (__builtin_expect(__any(any_esc), 0)) {
-      constexpr unsigned long long esc = W == 32 ? 0xFFFFFFFFull : (1ull << W) - 1ull;
-#pragma unroll
-      for (int k = 0; k < KP; ++k) {
-        const int q = t + k * kBlock;
-        if (q < sa.ne && ga[k] == esc) {
-          const int pos = MODE ? (int)(sa.c[k] & 0xFFFFu) : q;
-          L.er[bf][pos] = a_prev[MODE ? col[sa.e0 + pos] : (int)sa.c[k]];
-        }
-      }
-      __builtin_amdgcn_s_waitcnt(0);  // vmcnt(0) expcnt(0) lgkmcnt(0)
-    }
-  }
-  if (t <= sa.nn) L.rp[bf][t] = sa.rp;
-  __syncthreads();
-  if (t < sa.nn) {  // phase B (CA:106-113)
-    const int qb = L.rp[bf][t] - sa.e0, qe = L.rp[bf][t + 1] - sa.e0;
-    double S = 0.0, T = 0.0;
-    for (int q = qb; q < qe; ++q) {
-      const double e_ = L.er[bf][q];
-      const double fr = recon_fr(L.x[bf][q], e_, sa.own2);
-      L.x[bf][q] = fr;
-      L.own[bf][q] = (unsigned char)t;
-      S = S + fr;
-      T = T + e_;
-    }
-    const double a = ((sa.vv - S) + T) / (double)(qe - qb + 1);
-    L.a[bf][t] = a;
-    st_wt(a_new + sa.nb + t, a);
-    if (pc.width) put_code(pc, code_new, sa.nb + t, a);
-    if (CHECK) {
-      const unsigned long long b2 = err_bits(a, target[sa.nb + t]);
-      eb = b2 > eb ? b2 : eb;
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < KP; ++k) {  // phase C (CA:117-118)
-    const int q = t + k * kBlock;
-    if (q < sa.ne) {
-      st_f(F, sa.e0 + q, (L.x[bf][q] + L.a[bf][L.own[bf][q]]) - L.er[bf][q], sa.x[k]);
-    }
-  }
-}
-
-template <bool CHECK, int MODE, int W>
-__device__ inline unsigned long long pipe_tiles(
-    PipeLds &L, int m, const int *__restrict__ rowptr, const int *__restrict__ col,
-    const unsigned *__restrict__ cidx, const void *__restrict__ tab, const double *__restrict__ v,
-    double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
-    double *__restrict__ a_new, const double *__restrict__ target, void *__restrict__ code_new,
-    const PackCtl &pp, const PackCtl &pc, int elast) {
-  unsigned long long eb = 0;
-  PipeStream s0, s1, s2;
-  unsigned long long g0[kPipeKP], g1[kPipeKP];
-  pipe_load<MODE>(s0, 0, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);
-  pipe_load<MODE>(s1, 1, m, L.tl, L.gb, rowptr, cidx, F, v, a_prev2, elast);
-  pipe_gather<MODE, W>(g0, s0, tab, a_prev);
-#define FU_STEP(K, SA, SB, SC, GA, GB)                                                             \
-  if (it + K >= m) break;                                                                          \
-  pipe_step<CHECK, MODE, W>(L, it + K, m, SA, SB, SC, GA, GB, eb, rowptr, col, cidx, tab, v, F,    \
-                            a_prev, a_prev2, a_new, target, code_new, pp, pc, elast)
-  for (int it = 0; it < m; it += 6) {
-    FU_STEP(0, s0, s1, s2, g0, g1);
-    FU_STEP(1, s1, s2, s0, g1, g0);
-    FU_STEP(2, s2, s0, s1, g0, g1);
-    FU_STEP(3, s0, s1, s2, g1, g0);
-    FU_STEP(4, s1, s2, s0, g0, g1);
-    FU_STEP(5, s2, s0, s1, g1, g0);
-  }
-#undef FU_STEP
-  return eb;
-}
-
-template <bool CHECK, int MODE>
-__global__ __launch_bounds__(kBlock) void k_round_pipe(
-    const int4 *__restrict__ tiles, const int *__restrict__ tgbase, int ntl,
-    const int4 *__restrict__ heavy, int nheavy, const int *__restrict__ rowptr,
-    const int *__restrict__ col, const StageArgs sa, const void *__restrict__ G,
-    const double *__restrict__ v, double *__restrict__ F, const double *__restrict__ a_prev,
-    const double *__restrict__ a_prev2, double *__restrict__ a_new,
-    const double *__restrict__ target, unsigned long long *__restrict__ err,
-    const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
-    int rslot, int elast) {
-  constexpr int TE = kPipeTE;
-  __shared__ PipeLds L;
-  const PackCtl pp = ctl[rslot ^ 1];
-  const PackCtl pc = ctl[2];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
-  const int t = threadIdx.x;
-  unsigned long long eb = 0;
-
-  if ((int)blockIdx.x < nheavy) {
-    // ---------------- heavy row: kernel 4's exact chunked chain ----------------
-    // chunks of TE in the two LDS buffers: wave 0 chains chunk c while waves 1-3 stage c + 1
-    const int4 tl = heavy[blockIdx.x];
-    const int i = tl.x, b = tl.z, e = tl.w;
-    const double own2 = a_prev2[i];
-    double S = 0.0, T = 0.0;
-    const int nch = (e - b + TE - 1) / TE;
-    auto stage = [&](int c, int tid, int nthr) {
-      const int c0 = b + c * TE, cn = min(TE, e - c0);
-      for (int q = tid; q < cn; q += nthr) {
-        const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
-        L.x[c & 1][q] = recon_fr(ld_f(F, c0 + q), er, own2);
-        L.er[c & 1][q] = er;
-      }
-    };
-    if (nch > 0) stage(0, t, kBlock);
-    __syncthreads();
-    for (int c = 0; c < nch; ++c) {
-      if (t >= 64) {
-        if (c + 1 < nch) stage(c + 1, t - 64, kBlock - 64);
-      } else {
-        chain_sum(L.x[c & 1], L.er[c & 1], min(TE, e - (b + c * TE)), S, T);
-      }
-      __syncthreads();
-    }
-    if (t == 0) {
-      const double a = ((v[i] - S) + T) / (double)(e - b + 1);
-      L.a[0][0] = a;
-      st_wt(a_new + i, a);
-      if (pc.width) put_code(pc, code_new, i, a);
-      if (CHECK) eb = err_bits(a, target[i]);
-    }
-    __syncthreads();
-    const double a = L.a[0][0];
-    for (int k = b + t; k < e; k += kBlock) {
-      const double er = ld_est(pp, code_prev, a_prev, col[k]);
-      const double fo = ld_f(F, k);
-      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
-    }
-    if (CHECK) block_max_to(eb, err);
-    return;
-  }
-
-  // ---------------- light tiles: this block's list (XCD-aware) ----------------
-  const int bid = (int)blockIdx.x - nheavy, nbl = (int)gridDim.x - nheavy;  // nbl % 8 == 0
-  const int x = bid & 7, j = bid >> 3, nbx = nbl >> 3;
-  const int per = ntl >> 3, rem = ntl & 7;
-  const int lo = x * per + min(x, rem), hi = lo + per + (x < rem ? 1 : 0);
-  const int m = j < hi - lo ? (hi - lo - j + nbx - 1) / nbx : 0;
-  if (t < m) {
-    L.tl[t] = tiles[lo + j + t * nbx];
-    if (MODE) L.gb[t] = sa.gbase[sa.sel[width_index(pp.width)]][lo + j + t * nbx];
-  }
-  if (t == 0 && m == 0) {  // keep the clamped prefetch of an empty list in bounds
-    L.tl[0] = make_int4(0, 0, 0, 0);
-    L.gb[0] = 0;
-  }
-  __syncthreads();
-  const unsigned *cidx = MODE ? sa.sidx[sa.sel[width_index(pp.width)]] : reinterpret_cast<const unsigned *>(col);
-  const void *tab = MODE ? G : code_prev;
-#define FU_TILES(W_)                                                                                  \
-  pipe_tiles<CHECK, MODE, W_>(L, m, rowptr, col, cidx, tab, v, F, a_prev, a_prev2, a_new, target,     \
-                              code_new, pp, pc, elast)
-  if (pp.width == 0) eb = FU_TILES(0);
-  else if (pp.width == 8) eb = FU_TILES(8);
-  else if (pp.width == 16) eb = FU_TILES(16);
-  else eb = FU_TILES(32);
-#undef FU_TILES
-  if (CHECK) block_max_to(eb, err);
-}
 
 // Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
 // reconstruction of kernel 4), so k_round_recon's hub block only runs the chain.
@@ -1855,217 +958,6 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
   hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
 }
 
-// Mega hubs, parallel exact sums: stage launch. One block per piece of kPiece elements of a
-// hub row ({hub, offset in hubxy, length, first edge}): (fr, er) of every edge into hubxy
-// (CA:98-99 + kernel 4's flow reconstruction, coalesced), and the piece's approximate sums
-// (any order: they only steer the speculation) into psum.
-__global__ __launch_bounds__(kBlock) void k_hub_stage_p(
-    const int4 *__restrict__ piece, const int4 *__restrict__ hubs, const int *__restrict__ col,
-    const double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
-    const void *__restrict__ code_prev, const PackCtl *__restrict__ ctl, int rslot,
-    double2 *__restrict__ hubxy, double2 *__restrict__ psum) {
-  __shared__ double2 s_w[kBlock / 64];
-  const int4 pc = piece[blockIdx.x];
-  const int t = threadIdx.x;
-  const double own2 = a_prev2[hubs[pc.x].x];
-  const PackCtl pp = ctl[rslot ^ 1];
-  int cc[kPieceT];
-  double fo[kPieceT], er[kPieceT];
-#pragma unroll
-  for (int i = 0; i < kPieceT; ++i) {
-    const int o = t + kBlock * i;
-    cc[i] = o < pc.z ? col[pc.w + o] : 0;
-    fo[i] = o < pc.z ? ld_f(F, pc.w + o) : 0.0;
-  }
-#pragma unroll
-  for (int i = 0; i < kPieceT; ++i) er[i] = t + kBlock * i < pc.z ? ld_est(pp, code_prev, a_prev, cc[i]) : 0.0;
-  double sx = 0.0, sy = 0.0;
-#pragma unroll
-  for (int i = 0; i < kPieceT; ++i) {
-    const int o = t + kBlock * i;
-    if (o < pc.z) {
-      const double fr = recon_fr(fo[i], er[i], own2);
-      hubxy[pc.y + o] = make_double2(fr, er[i]);
-      sx += fr;
-      sy += er[i];
-    }
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    sx += __shfl_down(sx, off);
-    sy += __shfl_down(sy, off);
-  }
-  if ((t & 63) == 0) s_w[t >> 6] = make_double2(sx, sy);
-  __syncthreads();
-  if (t == 0) {
-    double2 r = s_w[0];
-    for (int w = 1; w < kBlock / 64; ++w) {
-      r.x += s_w[w].x;
-      r.y += s_w[w].y;
-    }
-    psum[blockIdx.x] = r;
-  }
-}
-
-// (hasb, run) element of the reverse segmented scan over threads: the composition from a
-// thread's start up to (and including the head of) the first thread with a boundary.
-struct SegRun {
-  RunSum r;
-  int f;
-};
-__device__ __forceinline__ SegRun seg_cat(const SegRun &x, const SegRun &y) {  // x earlier
-  if (x.f) return x;
-  return SegRun{run_cat(x.r, y.r), y.f};
-}
-__device__ __forceinline__ SegRun shfl_down_seg(const SegRun &a, int off) {
-  SegRun b;
-  b.r.t0 = __shfl_down(a.r.t0, off);
-  b.r.t1 = __shfl_down(a.r.t1, off);
-  b.r.mn = __shfl_down(a.r.mn, off);
-  b.r.mx = __shfl_down(a.r.mx, off);
-  b.r.len = __shfl_down(a.r.len, off);
-  b.r.q = __shfl_down(a.r.q, off);
-  b.f = __shfl_down(a.f, off);
-  return b;
-}
-
-// Mega hubs, parallel exact sums: summary launch. One block per piece; for each chain
-// (comp 0 = fr -> S, 1 = er -> T) it writes the piece's PieceSum (see the helpers above).
-__global__ __launch_bounds__(kBlock) void k_hub_sum(const int4 *__restrict__ piece,
-                                                    const int *__restrict__ hub_p0,
-                                                    const double2 *__restrict__ psum,
-                                                    const double2 *__restrict__ hubxy,
-                                                    PieceSum *__restrict__ hsum) {
-  __shared__ double2 s_pre;
-  __shared__ double s_wd[kBlock / 64];
-  __shared__ int s_wi[kBlock / 64];
-  __shared__ SegRun s_agg[kBlock / 64];
-  __shared__ int s_lastkey[kBlock];
-  const int4 pc = piece[blockIdx.x];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t < 64) {  // approximate sum of the hub's earlier pieces
-    double ax = 0.0, ay = 0.0;
-    for (int q = hub_p0[pc.x] + t; q < (int)blockIdx.x; q += 64) {
-      const double2 v = psum[q];
-      ax += v.x;
-      ay += v.y;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      ax += __shfl_down(ax, off);
-      ay += __shfl_down(ay, off);
-    }
-    if (t == 0) s_pre = make_double2(ax, ay);
-  }
-  const int nv = max(0, min(kPieceT, pc.z - t * kPieceT));
-  double2 v[kPieceT];
-#pragma unroll
-  for (int i = 0; i < kPieceT; ++i) v[i] = i < nv ? hubxy[pc.y + t * kPieceT + i] : make_double2(0.0, 0.0);
-  __syncthreads();
-  for (int comp = 0; comp < 2; ++comp) {
-    PieceSum *out = hsum + (size_t)blockIdx.x * 2 + comp;
-    const double pre = comp ? s_pre.y : s_pre.x;
-    double x[kPieceT];
-#pragma unroll
-    for (int i = 0; i < kPieceT; ++i) x[i] = comp ? v[i].y : v[i].x;
-    // approximate prefix: thread sums, block exclusive scan, then in-thread order
-    double ls = 0.0;
-#pragma unroll
-    for (int i = 0; i < kPieceT; ++i)
-      if (i < nv) ls += x[i];
-    double inc = ls;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = __shfl_up(inc, off);
-      if (lane >= off) inc += y;
-    }
-    if (lane == 63) s_wd[w] = inc;
-    __syncthreads();
-    double p = pre + (inc - ls);
-    for (int u = 0; u < w; ++u) p += s_wd[u];
-    int key[kPieceT];
-#pragma unroll
-    for (int i = 0; i < kPieceT; ++i) {
-      p += x[i];
-      key[i] = ulp_key(p);
-    }
-    if (nv) s_lastkey[t] = key[nv - 1];
-    __syncthreads();
-    const int key_in = t ? s_lastkey[t - 1] : ulp_key(pre);
-    // first walk: boundaries, the head run (before the thread's first boundary)
-    SegRun g{run_id(), 0};
-    int nbl = 0;
-    {
-      int prev = key_in;
-#pragma unroll
-      for (int i = 0; i < kPieceT; ++i) {
-        if (i < nv) {
-          const bool bnd = key[i] == kKeySpecial || prev == kKeySpecial || key[i] != prev;
-          if (bnd) {
-            g.f = 1;
-            ++nbl;
-          } else if (!g.f) {
-            g.r = run_cat(g.r, run_step(x[i], key[i] >> 1));
-          }
-          prev = key[i];
-        }
-      }
-    }
-    // reverse segmented scan: g = this thread's start up to the first boundary at or after it
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const SegRun y = shfl_down_seg(g, off);
-      if (lane + off < 64) g = seg_cat(g, y);
-    }
-    // boundary counts: exclusive scan
-    int ninc = nbl;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(ninc, off);
-      if (lane >= off) ninc += y;
-    }
-    if (lane == 0) s_agg[w] = g;
-    if (lane == 63) s_wi[w] = ninc;
-    __syncthreads();
-    SegRun suf{run_id(), 0};  // later waves, combined
-    for (int u = kBlock / 64 - 1; u > w; --u) suf = seg_cat(s_agg[u], suf);
-    g = seg_cat(g, suf);
-    SegRun gnext = shfl_down_seg(g, 1);  // the next thread's g (exclusive)
-    if (lane == 63) gnext = suf;
-    int jb = ninc - nbl, nbt = 0;
-    for (int u = 0; u < kBlock / 64; ++u) {
-      if (u < w) jb += s_wi[u];
-      nbt += s_wi[u];
-    }
-    if (t == 0) {
-      out->first_key = ulp_key(pre);
-      out->nb = nbt;
-      out->head = g.r;  // the piece start up to its first boundary
-    }
-    if (nbl && nbt <= kMaxBnd) {  // second walk: each boundary and the run after it
-      int prev = key_in, j = jb - 1;
-      RunSum rr = run_id();
-#pragma unroll
-      for (int i = 0; i < kPieceT; ++i) {
-        if (i < nv) {
-          const bool bnd = key[i] == kKeySpecial || prev == kKeySpecial || key[i] != prev;
-          if (bnd) {
-            if (j >= jb) out->b[j].run = rr;
-            ++j;
-            out->b[j].x = x[i];
-            out->b[j].key = key[i];
-            rr = run_id();
-          } else if (j >= jb) {
-            rr = run_cat(rr, run_step(x[i], key[i] >> 1));
-          }
-          prev = key[i];
-        }
-      }
-      out->b[j].run = run_cat(rr, gnext.r);
-    }
-    __syncthreads();  // s_wd / s_wi / s_agg / s_lastkey are reused by the next chain
-  }
-}
 
 // Mega hubs: the flows of every hub edge (CA:117-118) once the hub blocks have written a_r,
 // with many blocks (the hub block's own loop would hold one CU for d / 256 iterations on
@@ -2087,10 +979,6 @@ __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__re
   st_f(F, k, (p2.x + a) - p2.y, ld_f(F, k));
 }
 
-__global__ void k_fill_split(long long cnt, double val, double *__restrict__ p) {
-  long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (q < cnt) st_f_full(p, (int)q, val);
-}
 // split-word flows -> doubles (fu_get_flows of kernels >= 4)
 __global__ void k_unsplit(long long cnt, const double *__restrict__ src, double *__restrict__ dst) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
@@ -2099,227 +987,6 @@ __global__ void k_unsplit(long long cnt, const double *__restrict__ src, double 
 __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) p[q] = val;
-}
-
-// ------------------------------------------------------------------------------------
-// Variant 5: column split ("split"). Identical arithmetic to variant 4. The neighbour
-// estimates a_{r-1}[col e] are gathered by a separate launch in which each group of XCDs
-// owns one half of the estimate table (4 MB instead of 8 MB for ER-1M, so it stays in the
-// XCD's L2). The gather launch reads a part-major copy of col: the edges of every row with
-// col < split first, then the rest, so each part's stream is contiguous. It writes G in the
-// same part-major order. The compute launch then reads G coalesced and never gathers.
-// Rows must be sorted by neighbour id, so that the part-0 edges of a row are its prefix
-// and the row order of the sums is unchanged. Placement (blockIdx % 8 -> XCD) is used
-// for locality only, never for correctness.
-// ------------------------------------------------------------------------------------
-constexpr int kGatherChunk = 2048;  // edges per gather block (8 per thread)
-
-__global__ __launch_bounds__(kBlock) void k_gather_split(const int *__restrict__ col_pm,
-                                                         long long e0_count, long long e_total,
-                                                         const double *__restrict__ a_prev,
-                                                         double *__restrict__ G) {
-  const int b = blockIdx.x;
-  const int part = (b & 7) >> 2;              // XCD group 0..3 -> part 0, 4..7 -> part 1
-  const long long chunk = (long long)(b >> 3) * 4 + (b & 3);
-  const long long pb = part ? e0_count : 0, pe = part ? e_total : e0_count;
-  const long long base = pb + chunk * kGatherChunk;
-  if (base >= pe) return;
-  constexpr int kPer = kGatherChunk / kBlock;
-  int c[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const long long e = base + threadIdx.x + k * kBlock;
-    c[k] = e < pe ? ld_stream(col_pm + e) : -1;
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const long long e = base + threadIdx.x + k * kBlock;
-    if (c[k] >= 0) G[e] = a_prev[c[k]];
-  }
-}
-
-// Kernel 6: gather only part 0 (low half of the estimate table), every block, every XCD.
-__global__ __launch_bounds__(kBlock) void k_gather_part0(const int *__restrict__ col_pm,
-                                                         long long e0_count,
-                                                         const double *__restrict__ a_prev,
-                                                         double *__restrict__ G) {
-  constexpr int kPer = kGatherChunk / kBlock;
-  const long long base = (long long)blockIdx.x * kGatherChunk;
-  int c[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const long long e = base + threadIdx.x + k * kBlock;
-    c[k] = e < e0_count ? ld_stream(col_pm + e) : -1;
-  }
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const long long e = base + threadIdx.x + k * kBlock;
-    if (c[k] >= 0) G[e] = a_prev[c[k]];
-  }
-}
-
-// part-major index of canonical edge k (0-based position inside row t of the tile)
-__device__ inline int split_index(int k, int split_t, int p0, int p1) {
-  return k < split_t ? p0 + k : p1 + (k - split_t);
-}
-
-// GATHER1 (kernel 6): part-1 estimates are gathered here from a_prev (high half of the
-// table, 4 MB for ER-1M) instead of being read from G; only part 0 went through G.
-template <bool CHECK, bool GATHER1 = false>
-__global__ __launch_bounds__(kBlock) void k_round_split(
-    const int4 *__restrict__ tiles, const int2 *__restrict__ tiles_g, const int *__restrict__ rowptr,
-    const int *__restrict__ rowptr0, long long e0_count, const double *__restrict__ v,
-    double *__restrict__ F, const double *__restrict__ G, const double *__restrict__ a_prev2,
-    double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, PackCtl *__restrict__ ctl, int rslot,
-    const int *__restrict__ col_pm = nullptr, const double *__restrict__ a_prev = nullptr) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot].width = 0;  // a_r is not packed
-  __shared__ double s_x[kTileEdges];  // f_{r-2} on load, fr after phase B (canonical order)
-  __shared__ double s_g[kTileEdges];  // a_{r-1}[col] in part-major order: part 0 | part 1
-  __shared__ unsigned char s_own[kTileEdges];
-  __shared__ int s_rp[kTileNodes + 1];
-  __shared__ int s_rp0[kTileNodes + 1];
-  __shared__ double s_a[kTileNodes];
-  const int t = threadIdx.x;
-  const int4 tl = tiles[blockIdx.x];
-  const int2 tg = tiles_g[blockIdx.x];  // {rowptr0[node_begin], rowptr0[node_end]}
-  unsigned long long eb = 0;
-
-  if (tl.y < 0) {
-    // ---------------- heavy node ----------------
-    const int i = tl.x;
-    const int b = tl.z, e = tl.w;
-    const int split_i = tg.y - tg.x;
-    const int p0 = tg.x, p1 = (int)(e0_count + (b - tg.x));
-    const double own2 = a_prev2[i];
-    double S = 0.0, T = 0.0;
-    for (int c0 = b; c0 < e; c0 += kTileEdges) {
-      const int cn = min(kTileEdges, e - c0);
-      for (int q = t; q < cn; q += kBlock) {
-        const int gi = split_index(c0 - b + q, split_i, p0, p1);
-        const double er = (GATHER1 && c0 - b + q >= split_i) ? a_prev[col_pm[gi]] : G[gi];
-        s_x[q] = recon_fr(ld_f(F, c0 + q), er, own2);
-        s_g[q] = er;
-      }
-      __syncthreads();
-      if (t < 64) chain_sum(s_x, s_g, cn, S, T);
-      __syncthreads();
-    }
-    if (t == 0) {
-      const double a = ((v[i] - S) + T) / (double)(e - b + 1);
-      s_a[0] = a;
-      st_wt(a_new + i, a);
-      if (CHECK) eb = err_bits(a, target[i]);
-    }
-    __syncthreads();
-    const double a = s_a[0];
-    for (int k = b + t; k < e; k += kBlock) {
-      const int gi = split_index(k - b, split_i, p0, p1);
-      const double er = (GATHER1 && k - b >= split_i) ? a_prev[col_pm[gi]] : G[gi];
-      const double fo = ld_f(F, k);
-      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
-    }
-    if (CHECK) block_max_to(eb, err);
-    return;
-  }
-
-  // ---------------- light tile ----------------
-  const int nb = tl.x, nn = tl.y - tl.x;
-  const int e0 = tl.z, ne = tl.w - tl.z;
-  const int g0b = tg.x, n0 = tg.y - tg.x;   // part-0 edges of the tile: G[g0b, g0b + n0)
-  const long long g1b = e0_count + (e0 - g0b);  // part-1 edges: G[g1b, g1b + ne - n0)
-  constexpr int kPer = kTileEdges / kBlock;
-  double x[kPer], g[kPer];
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    x[k] = 0.0;
-    g[k] = 0.0;
-    if (q < ne) {
-      x[k] = ld_f(F, e0 + q);
-      if (GATHER1) g[k] = q < n0 ? G[g0b + q] : a_prev[col_pm[g1b + (q - n0)]];
-      else g[k] = q < n0 ? G[g0b + q] : G[g1b + (q - n0)];
-    }
-  }
-  const int rp = t <= nn ? rowptr[nb + t] : 0;
-  const int rp0 = t <= nn ? rowptr0[nb + t] : 0;
-  const int rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
-  const int rp0_last = (t == 0 && nn == kBlock) ? rowptr0[nb + kBlock] : 0;
-  const double vv = t < nn ? v[nb + t] : 0.0;
-  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    if (q < ne) {
-      s_x[q] = x[k];
-      s_g[q] = g[k];
-    }
-  }
-  if (t <= nn) {
-    s_rp[t] = rp;
-    s_rp0[t] = rp0;
-  }
-  if (t == 0 && nn == kBlock) {
-    s_rp[kBlock] = rp_last;
-    s_rp0[kBlock] = rp0_last;
-  }
-  __syncthreads();
-  if (t < nn) {
-    const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
-    const int split_t = s_rp0[t + 1] - s_rp0[t];
-    const int p0 = s_rp0[t] - g0b;                         // LDS index of the row's part 0
-    const int p1 = n0 + ((s_rp[t] - s_rp0[t]) - (e0 - g0b));  // LDS index of the row's part 1
-    double S = 0.0, T = 0.0;
-    for (int q = qb; q < qe; ++q) {
-      const double er = s_g[split_index(q - qb, split_t, p0, p1)];
-      const double fr = recon_fr(s_x[q], er, own2);
-      s_x[q] = fr;
-      s_own[q] = (unsigned char)t;
-      S = S + fr;
-      T = T + er;
-    }
-    const double a = ((vv - S) + T) / (double)(qe - qb + 1);
-    s_a[t] = a;
-    st_wt(a_new + nb + t, a);
-    if (CHECK) eb = err_bits(a, target[nb + t]);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    if (q < ne) {
-      const int o = s_own[q];
-      const int qb = s_rp[o] - e0;
-      const int split_t = s_rp0[o + 1] - s_rp0[o];
-      const int p0 = s_rp0[o] - g0b;
-      const int p1 = n0 + ((s_rp[o] - s_rp0[o]) - (e0 - g0b));
-      const double er = s_g[split_index(q - qb, split_t, p0, p1)];
-      st_f(F, e0 + q, (s_x[q] + s_a[o]) - er, x[k]);
-    }
-  }
-  if (CHECK) block_max_to(eb, err);
-}
-
-// round 0 for the push layout: message i->j = (a_i, a_i) stored at inbox[rev[e]]
-__global__ __launch_bounds__(kBlock) void k_round0_push(int n, const int *__restrict__ rowptr,
-                                                        const int *__restrict__ rev,
-                                                        const double *__restrict__ v,
-                                                        double2 *__restrict__ in_new,
-                                                        double *__restrict__ a) {
-  int i = blockIdx.x * kBlock + threadIdx.x;
-  if (i >= n) return;
-  int b = rowptr[i], e = rowptr[i + 1];
-  double ai = ((v[i] - 0.0) + 0.0) / (double)(e - b + 1);
-  a[i] = ai;
-  double fv = (0.0 + ai) - 0.0;
-  for (int k = b; k < e; ++k) in_new[rev[k]] = make_double2(fv, ai);
-}
-
-// flows of the push layout in CSR order: f[e] = inbox[rev[e]].x
-__global__ void k_push_flows(long long E, const int *__restrict__ rev,
-                             const double2 *__restrict__ in, double *__restrict__ f) {
-  long long e = (long long)blockIdx.x * kBlock + threadIdx.x;
-  if (e < E) f[e] = in[rev[e]].x;
 }
 
 __global__ __launch_bounds__(kBlock) void k_max_err(int n, const double *__restrict__ a,
@@ -2487,6 +1154,7 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
   }
 }
 
+
 template <typename T>
 int dmalloc(T **p, size_t count) {
   if (count == 0) count = 1;
@@ -2510,129 +1178,88 @@ struct fu_handle {
   std::vector<int32_t> h_new_of_old;
   std::vector<int64_t> h_orig_rowptr;
   hipStream_t stream = nullptr;
+  hipStream_t stream2 = nullptr;            // kernel 4's heavy tiles, concurrently (fork_heavy)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
+  hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
   int32_t max_deg = 0;
-  int *rowptr = nullptr, *col = nullptr, *rev = nullptr;
+  int *rowptr = nullptr, *col = nullptr;
+  int *blk_row = nullptr;  // round 0: row of edge b * kR0E for every block b, then of edge E - 1
   double *v = nullptr;
-  double *f[2] = {nullptr, nullptr};
-  double *a[3] = {nullptr, nullptr, nullptr};  // a[2]: third estimate buffer (kernel 4)
-  double2 *inbox[2] = {nullptr, nullptr};
+  double *f[2] = {nullptr, nullptr};           // F[r & 1]: f_{r-2} in, f_r out (split words)
+  double *a[3] = {nullptr, nullptr, nullptr};  // A[r % 3] = a_r
   double *target = nullptr;
   unsigned long long *err = nullptr;
   int errcap = 0;
   double *ftmp = nullptr;
-  int cur = 0;
   int64_t rounds = 0;
-  int kernel = 4;
+  int kernel = 4;        // 4 = recon (LDS tiles), 8 = stage (LDS-staged slices + recon tiles)
+  int geo = 1;           // kernel 4 tile geometry (kGeoEdges x kGeoNodes)
   int hub_threshold = 64;
-  int nt = 0;  // non-temporal loads/stores for streamed arrays (kernel 4)
-  bool autotune = true;  // kernel "auto": time kernels 4 (+nt), 6, 5 on real rounds, keep the best
+  int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
+  int wave_heavy = 1;    // kernel 4: heavy rows one per wave
+  int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
+  int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
+  bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
   bool tuned = false;
-  float tune_ms[12] = {};  // per candidate (autotune_kernel order)
-  int tune_out[12] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
+  float tune_ms[8] = {};  // per candidate (tune_cands order), ms per round of the last pass
+  int tune_out[8] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
   int tuned_width = 0;    // packing width the last pass ran under
   int tune_cache[4] = {-1, -1, -1, -1};  // winner per packing width (0, 8, 16, 32), kept across fu_reset
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
-  hipEvent_t ev_pw = nullptr;
   bool pw_pending = false;
-  int diag = 0;  // timing-only ablations of kernel 4 (wrong results; tools/ only)
+  int diag = 0;  // timing-only ablations (-DFU_DIAG builds only; wrong results)
   std::vector<int64_t> h_rowptr;
-  std::vector<int32_t> h_col;  // host copy (column-split preparation)
-  // kernel 5 (column split)
-  int *colpm = nullptr, *rowptr0 = nullptr;
-  double *G = nullptr;
-  int4 *tiles_s = nullptr;
-  int2 *tiles_g = nullptr;
-  int ntiles_s = 0;
-  int64_t e0_count = 0;
-  int4 *tiles = nullptr;  // 2048-edge tiles (kernels 2, 3)
-  int ntiles = 0;
-  // kernel 4 tiles per geometry (0 = 2048x256, 1 = 1024x128, 2 = 1024x256, 3 = 512x64 edges x
-  // nodes); all four are built up front so autotuning can switch geometry between rounds
+  std::vector<int32_t> h_col;
+  // kernel 4 tiles per geometry (all four built up front so autotuning can switch between
+  // rounds): mega hubs, heavy rows, then light tiles
   int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
   int ntiles_geo[4] = {0, 0, 0, 0};
-  int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles (hubs, heavy rows, bins)
-  int fork_heavy = 1;                 // option "fork_heavy": heavy tiles on stream2, concurrently
-  hipStream_t stream2 = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int geo = 0;
-  // kernel 7 (wave tiles): per wave geometry (0 = 256 edges x 32 nodes, 1 = 512 x 64) the
-  // light wave tiles and the heavy rows (kernel 4 heavy-path tiles) of that geometry
-  int4 *wtiles[2] = {nullptr, nullptr};
-  int nwtiles[2] = {0, 0};
-  int4 *wheavy[2] = {nullptr, nullptr};
-  int nwheavy[2] = {0, 0};
-  int wgeo = 1;
-  int *perm = nullptr;  // degree-sorted heavy rows (kernel 4 bins)
-  // kernel 4 mega hubs (degree > mega_hub): first tiles of every geometry ({i, -3, b, e})
-  int mega_hub = 8192;  // degree above which a row is a mega hub (option "mega_hub")
-  int wave_heavy = 1;   // kernel 4: heavy rows one per wave (option "wave_heavy")
+  int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
   std::vector<int32_t> h_hrows;
-  int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first
+  int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first (per geometry)
   int n_hub = 0;
   int64_t hub_total = 0;
-  // parallel exact hub sums (option "hub_scan", default off: on converged R-MAT rounds the
-  // flow sums wander across binades, ~10% of their steps are boundaries, and the serial
-  // pass loses to the one-wave chain): pieces of kPiece edges
-  int hub_scan = 0;
-  int n_piece = 0;
-  int4 *hub_piece = nullptr;  // {hub, offset in hubxy, length, first edge}
-  int *hub_p0 = nullptr;      // first piece of each hub (n_hub + 1)
-  double2 *psum = nullptr;    // approximate (fr, er) sums per piece
-  PieceSum *hsum = nullptr;   // run summaries per piece and chain
-  unsigned long long *hub_redo = nullptr;  // pieces the serial pass redid element by element
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
-  int bins = 0;         // kernel 4 (geometry 0): degree bins for rows above hub_threshold
-  // kernel 4 packed estimate table (see PackCtl): code[r & 1] = codes of a_r
+  // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
   unsigned char *code[2] = {nullptr, nullptr};
   PackCtl *pctl = nullptr;  // [0], [1]: per code table; [2]: current encoding plan
   int *psample = nullptr;   // gather targets sampled for the plan
   int n_psample = 0;
   int pack = 1;             // 0 = off
   int pack_every = 16;      // rounds between encoding plans
-  int tile_edges = 2048;  // 2048 (256 nodes), 1024 (128 or 256 nodes), 512 (64 nodes)
+  int tile_edges = 1024;    // option shadow of geo
   int tile_nodes = 0;
   bool has_target = false;
-  // kernel 8 (LDS-staged slices): light tiles of kStageTE x kStageTN in edge groups, heavy
-  // rows as kernel 4 heavy tiles, and one slice layout per table element width
+  // kernel 8 (LDS-staged slices): light tiles of kStageTE x kStageTN, heavy rows as kernel 4
+  // heavy tiles, one slice layout per table element width
   struct StageLayout {
-    int P = 0, Q = 0;              // slices, blocks per slice
-    int *aoff = nullptr;           // per stage block: first entry in aitem
-    int2 *aitem = nullptr;         // stage items {first element, count}, grouped by block
-    unsigned short *colS = nullptr;  // per staged element: column offset within its slice
-    unsigned *sidx = nullptr;      // per tile edge (slice order): G index in group << 16 | position
-    // compact form (when every tile's edges fall into <= 64 slice runs): per edge u16 =
-    // position | run << 10, and per tile the run offsets D (G index = gbase + m + D[run])
-    unsigned short *sidx16 = nullptr;
-    int *dtab = nullptr;           // kStageRuns per light tile
-    int *gbase = nullptr;          // per light tile: its group's first staged element
+    int P = 0, Q = 0, SN = 0, NB = 0;     // slices, blocks per slice, nodes per slice, blocks (P = 0: not built)
+    int4 *brange = nullptr;               // per stage block: {begin, end} in G, slice, 0
+    unsigned short *colS = nullptr;       // per G element: column offset in its slice
+    unsigned short *sidx16 = nullptr;     // per light-tile edge (slice order): position | run << 10
+    int *dtab = nullptr;                  // per light tile: kStageRuns run offsets (G index - m)
   };
-  StageLayout st[4];            // element bytes 1, 2, 4, 8
+  StageLayout st[4];                      // element bytes 1, 2, 4, 8
   bool st_ready = false;
-  int st_ngroups = 0;
-  int4 *st_tiles = nullptr;     // light tiles
-  int *st_gbase = nullptr;      // per light tile: first edge of its group
+  std::string st_why;                     // why no layout could be built (kernel 8 unavailable)
+  int4 *st_tiles = nullptr;               // light tiles
   int st_ntiles = 0;
-  int4 *st_heavy = nullptr;     // rows above the tile limit ({i, -1, b, e})
+  int4 *st_heavy = nullptr;               // rows above the tile limit ({i, -1, b, e})
   int st_nheavy = 0;
-  void *stG = nullptr;          // staged estimates, 8 B per light edge
-  int seen_width = 0;           // packing width the host last saw (layout choice)
-  int st_force = -1;            // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
-  int st_compact = 1;           // option "stage_compact": kernel 8 reads the u16 sidx
-  std::vector<int4> h_light;    // host copies (layout construction)
-  std::vector<int32_t> h_gstart;
-  int n_cu = 256;               // compute units (kernel 9 grid)
-  int pipe_bpc = 4;             // kernel 9/10: persistent blocks per CU (4 fit at 1024x128 tiles)
-  // multi-GPU (fu_dist.hip)
-  void *dist = nullptr;
+  void *stG = nullptr;                    // staged estimates, 8 B per G element
+  int seen_width = 0;                     // packing width the host last saw
+  int st_force = -1;                      // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
+  std::vector<int4> h_light;              // host copy (layout construction)
+  int n_cu = 256;
+  void *dist = nullptr;  // multi-GPU (fu_dist.hip)
 };
 
 extern "C" int fu__dist_round_hook(fu_handle *h, int phase);
@@ -2640,15 +1267,19 @@ extern "C" void fu__dist_free(fu_handle *h);
 
 namespace {
 
+constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
+constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
-                     std::vector<int4> *host_out = nullptr, bool mega = false, int *nheavy = nullptr) {
+// Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
+// block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
+// {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
   while (i < n) {
     int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    if (mega && d > h->mega_hub) {
+    if (d > h->mega_hub) {
       hubs.push_back(make_int4(i, -3, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
       ++i;
       continue;
@@ -2668,11 +1299,9 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
     }
     light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
-  // mega hubs, then heavy tiles first so their long sequential chains start early; heavy
-  // rows of up to mega_hub go four to a block (one per wave) when wave_heavy is on, longest
-  // first (the row list hrows is shared by every geometry)
+  // mega hubs, then heavy tiles first so their long sequential chains start early
   std::vector<int4> all(hubs);
-  if (mega && h->wave_heavy && !heavy.empty()) {
+  if (h->wave_heavy && !heavy.empty()) {
     std::vector<int32_t> rows;
     for (const int4 &hv : heavy) rows.push_back(hv.x);
     std::stable_sort(rows.begin(), rows.end(), [&](int32_t x, int32_t y) {
@@ -2685,9 +1314,8 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
   } else {
     all.insert(all.end(), heavy.begin(), heavy.end());
   }
-  if (nheavy) *nheavy = (int)all.size();
+  *nheavy = (int)all.size();
   all.insert(all.end(), light.begin(), light.end());
-  if (host_out) *host_out = all;
   if (*dst) hipFree(*dst);
   *dst = nullptr;
   *count = (int)all.size();
@@ -2696,111 +1324,13 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count,
   return FU_OK;
 }
 
-// Kernel 4 tiles with degree bins: rows of degree > hub_threshold sorted by degree
-// (descending, ties by id) and grouped R per block (R = TE / C, C = the power of two >= the
-// bin's first degree, capped at TE); then light tiles of contiguous low-degree rows.
-int build_tiles_binned(fu_handle *h) {
-  const int32_t n = h->n;
-  std::vector<int32_t> heavy;
-  for (int32_t i = 0; i < n; ++i)
-    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->hub_threshold) heavy.push_back(i);
-  auto deg = [&](int32_t i) { return h->h_rowptr[i + 1] - h->h_rowptr[i]; };
-  std::stable_sort(heavy.begin(), heavy.end(), [&](int32_t x, int32_t y) { return deg(x) > deg(y); });
-  std::vector<int4> all;
-  size_t q = 0;
-  while (q < heavy.size()) {
-    const int64_t d = deg(heavy[q]);
-    int C = 1;
-    while (C < d && C < kTileEdges) C <<= 1;
-    const int R = std::max(1, std::min(kBlock, kTileEdges / C));
-    const int r = (int)std::min<size_t>(R, heavy.size() - q);
-    all.push_back(make_int4((int)q, -2, r, kTileEdges / R));
-    q += r;
-  }
-  // light tiles over the remaining rows (heavy rows are skipped inside build_tiles_geom)
-  std::vector<int4> light;
-  int32_t i = 0;
-  while (i < n) {
-    if (deg(i) > h->hub_threshold) { ++i; continue; }
-    int32_t b = i;
-    int64_t eb = h->h_rowptr[b];
-    while (i < n && i - b < kTileNodes && deg(i) <= h->hub_threshold && h->h_rowptr[i + 1] - eb <= kTileEdges) ++i;
-    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
-  }
-  all.insert(all.end(), light.begin(), light.end());
-  if (h->tiles_geo[0]) hipFree(h->tiles_geo[0]);
-  if (h->perm) hipFree(h->perm);
-  h->tiles_geo[0] = nullptr;
-  h->perm = nullptr;
-  h->ntiles_geo[0] = (int)all.size();
-  h->nheavy_geo[0] = (int)(all.size() - light.size());
-  if (int rc = dmalloc(&h->tiles_geo[0], all.size())) return rc;
-  if (int rc = dmalloc(&h->perm, std::max<size_t>(1, heavy.size()))) return rc;
-  HIP_TRY(hipMemcpy(h->tiles_geo[0], all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
-  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->perm, heavy.data(), sizeof(int32_t) * heavy.size(), hipMemcpyHostToDevice));
-  return FU_OK;
-}
-
-constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
-constexpr int kGeoNodes[4] = {256, 128, 256, 64};
-
-constexpr int kWaveEdges[2] = {256, 512};
-constexpr int kWaveNodes[2] = {32, 64};
-
-// Kernel 7 tiles: light rows (degree <= min(hub_threshold, TE)) in contiguous wave tiles of
-// <= TN nodes / <= TE edges; the other rows as kernel 4 heavy-path tiles {i, -1, b, e}.
-int build_wave_tiles(fu_handle *h, int wg) {
-  const int te = kWaveEdges[wg], tn = kWaveNodes[wg];
-  const int64_t lim = std::min<int64_t>(h->hub_threshold, te);
-  std::vector<int4> light, heavy;
-  const int32_t n = h->n;
-  int32_t i = 0;
-  while (i < n) {
-    const int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    if (d > lim) {
-      heavy.push_back(make_int4(i, -1, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
-      ++i;
-      continue;
-    }
-    const int32_t b = i;
-    const int64_t eb = h->h_rowptr[b];
-    while (i < n && i - b < tn) {
-      const int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
-      if (di > lim || h->h_rowptr[i + 1] - eb > te) break;
-      ++i;
-    }
-    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
-  }
-  for (int4 **p : {&h->wtiles[wg], &h->wheavy[wg]}) {
-    if (*p) hipFree(*p);
-    *p = nullptr;
-  }
-  h->nwtiles[wg] = (int)light.size();
-  h->nwheavy[wg] = (int)heavy.size();
-  if (int rc = dmalloc(&h->wtiles[wg], std::max<size_t>(1, light.size()))) return rc;
-  if (int rc = dmalloc(&h->wheavy[wg], std::max<size_t>(1, heavy.size()))) return rc;
-  if (!light.empty()) HIP_TRY(hipMemcpy(h->wtiles[wg], light.data(), sizeof(int4) * light.size(), hipMemcpyHostToDevice));
-  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->wheavy[wg], heavy.data(), sizeof(int4) * heavy.size(), hipMemcpyHostToDevice));
-  return FU_OK;
-}
-
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
-  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_piece,
-                  (void *)h->hub_p0, (void *)h->psum, (void *)h->hsum})
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy})
     if (p) hipFree(p);
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
-  h->hub_piece = nullptr;
-  h->hub_p0 = nullptr;
-  h->psum = nullptr;
-  h->hsum = nullptr;
-  h->n_piece = 0;
-  if (!h->hub_redo) {
-    if (int rc = dmalloc(&h->hub_redo, 1)) return rc;
-    HIP_TRY(hipMemset(h->hub_redo, 0, sizeof(unsigned long long)));
-  }
   std::vector<int4> rows;
   std::vector<int32_t> off;
   int64_t tot = 0;
@@ -2820,39 +1350,14 @@ int build_hubs(fu_handle *h) {
   if (int rc = dmalloc(&h->hubxy, (size_t)tot)) return rc;
   HIP_TRY(hipMemcpy(h->hub_rows, rows.data(), sizeof(int4) * rows.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->hub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
-  std::vector<int4> pcs;
-  std::vector<int32_t> p0;
-  for (size_t q = 0; q < rows.size(); ++q) {
-    p0.push_back((int32_t)pcs.size());
-    const int d = rows[q].z - rows[q].y;
-    for (int k = 0; k < d; k += kPiece)
-      pcs.push_back(make_int4((int)q, rows[q].w + k, std::min(kPiece, d - k), rows[q].y + k));
-  }
-  p0.push_back((int32_t)pcs.size());
-  h->n_piece = (int)pcs.size();
-  if (int rc = dmalloc(&h->hub_piece, pcs.size())) return rc;
-  if (int rc = dmalloc(&h->hub_p0, p0.size())) return rc;
-  if (int rc = dmalloc(&h->psum, pcs.size())) return rc;
-  if (int rc = dmalloc(&h->hsum, 2 * pcs.size())) return rc;
-  HIP_TRY(hipMemcpy(h->hub_piece, pcs.data(), sizeof(int4) * pcs.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->hub_p0, p0.data(), sizeof(int32_t) * p0.size(), hipMemcpyHostToDevice));
   return FU_OK;
 }
 
 int build_tiles(fu_handle *h) {
   h->h_hrows.clear();
-  if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles, &h->ntiles)) return rc;
-  for (int wg = 0; wg < 2; ++wg)
-    if (int rc = build_wave_tiles(h, wg)) return rc;
-  for (int g = 0; g < 4; ++g) {
-    if (g == 0 && h->bins) {
-      if (int rc = build_tiles_binned(h)) return rc;
-      continue;
-    }
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], nullptr, true,
-                                  &h->nheavy_geo[g]))
+  for (int g = 0; g < 4; ++g)
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g]))
       return rc;
-  }
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
   if (int rc = dmalloc(&h->hrows, std::max<size_t>(1, h->h_hrows.size()))) return rc;
@@ -2861,79 +1366,25 @@ int build_tiles(fu_handle *h) {
   return build_hubs(h);
 }
 
-// Current estimate / flow buffers (kernel 4 rotates A[r % 3] and F[r & 1]).
-inline double *cur_a(fu_handle *h) {
-  if (h->kernel >= 4) return h->a[(int)((h->rounds + 2) % 3)];
-  return h->a[h->cur];
-}
-inline double *cur_f(fu_handle *h) {
-  if (h->kernel >= 4) return h->f[(int)((h->rounds + 1) & 1)];
-  return h->f[h->cur];
-}
+// Current estimate / flow buffers (A[r % 3] and F[r & 1] of the last round r).
+inline double *cur_a(fu_handle *h) { return h->a[(int)((h->rounds + 2) % 3)]; }
+inline double *cur_f(fu_handle *h) { return h->f[(int)((h->rounds + 1) & 1)]; }
 
-// Kernel 5 preparation: split node id (edge-balanced), part-major col, rowptr0, tiles.
-int ensure_split(fu_handle *h) {
-  if (h->G) return FU_OK;
-  const int32_t n = h->n;
-  const int64_t E = h->E;
-  for (int32_t i = 0; i < n; ++i)
-    for (int64_t k = h->h_rowptr[i] + 1; k < h->h_rowptr[i + 1]; ++k)
-      if (h->h_col[k - 1] >= h->h_col[k])
-        return fail(FU_ERR_GRAPH, "kernel 5 (column split) needs rows sorted by neighbour id");
-  // split id: smallest s with rowptr[s] >= E/2 (symmetric graph: in-degree == degree)
-  int32_t split = (int32_t)(std::lower_bound(h->h_rowptr.begin(), h->h_rowptr.end(), E / 2) - h->h_rowptr.begin());
-  if (split > n) split = n;
-  std::vector<int32_t> rp0(n + 1, 0);
-  for (int32_t i = 0; i < n; ++i) {
-    auto b = h->h_col.begin() + h->h_rowptr[i], e = h->h_col.begin() + h->h_rowptr[i + 1];
-    rp0[i + 1] = rp0[i] + (int32_t)(std::lower_bound(b, e, split) - b);
-  }
-  const int64_t E0 = rp0[n];
-  std::vector<int32_t> pm(E > 0 ? E : 1);
-  for (int32_t i = 0; i < n; ++i) {
-    const int64_t b = h->h_rowptr[i], s0 = rp0[i + 1] - rp0[i];
-    for (int64_t k = 0; k < s0; ++k) pm[rp0[i] + k] = h->h_col[b + k];
-    const int64_t d = h->h_rowptr[i + 1] - b, p1 = E0 + (b - rp0[i]);
-    for (int64_t k = s0; k < d; ++k) pm[p1 + (k - s0)] = h->h_col[b + k];
-  }
-  std::vector<int4> tv;
-  if (int rc = build_tiles_geom(h, kTileEdges, kTileNodes, &h->tiles_s, &h->ntiles_s, &tv)) return rc;
-  std::vector<int2> tg(tv.size());
-  for (size_t q = 0; q < tv.size(); ++q) {
-    const int4 t = tv[q];
-    tg[q] = t.y < 0 ? make_int2(rp0[t.x], rp0[t.x + 1]) : make_int2(rp0[t.x], rp0[t.y]);
-  }
-  if (int rc = dmalloc(&h->colpm, (size_t)E)) return rc;
-  if (int rc = dmalloc(&h->rowptr0, (size_t)n + 1)) return rc;
-  if (int rc = dmalloc(&h->tiles_g, tg.size())) return rc;
-  if (int rc = dmalloc(&h->G, (size_t)E)) return rc;
-  if (E) HIP_TRY(hipMemcpy(h->colpm, pm.data(), sizeof(int32_t) * E, hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->rowptr0, rp0.data(), sizeof(int32_t) * (n + 1), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->tiles_g, tg.data(), sizeof(int2) * tg.size(), hipMemcpyHostToDevice));
-  h->e0_count = E0;
-  return FU_OK;
-}
+// ---- kernel 8 preparation -------------------------------------------------------------
+constexpr int kStageMaxP = 512;  // slices per layout (more: layout not built)
 
-// Kernel 8 preparation: light tiles, edge groups and the four slice layouts.
-constexpr int kStageMaxP = 512;      // slices per layout (more: layout not built)
-constexpr int kStageGroupEdges = 60000;  // G index within a group is u16 (room for padding)
-
-// Light tiles (kStageTE x kStageTN), their edge groups and the heavy rows (kernels 8-10).
+// Light tiles (kStageTE x kStageTN) and the rows above the tile limit (kernel 8).
 int ensure_light(fu_handle *h) {
   if (h->st_tiles) return FU_OK;
   const int32_t n = h->n;
   const auto &rp = h->h_rowptr;
   const int64_t lim = std::min<int64_t>(h->hub_threshold, kStageTE);
   std::vector<int4> light, heavy;
-  std::vector<int32_t> gstart;  // per group: first light tile
-  int64_t gedges = 0;
-  bool prev_light = false;
   for (int32_t i = 0; i < n;) {
     const int64_t d = rp[i + 1] - rp[i];
     if (d > lim) {
       heavy.push_back(make_int4(i, -1, (int)rp[i], (int)rp[i + 1]));
       ++i;
-      prev_light = false;
       continue;
     }
     const int32_t b = i;
@@ -2942,175 +1393,138 @@ int ensure_light(fu_handle *h) {
       if (di > lim || rp[i + 1] - rp[b] > kStageTE) break;
       ++i;
     }
-    const int64_t te = rp[i] - rp[b];
-    if (!prev_light || gedges + te > kStageGroupEdges) {
-      gstart.push_back((int32_t)light.size());
-      gedges = 0;
-    }
     light.push_back(make_int4(b, i, (int)rp[b], (int)rp[i]));
-    gedges += te;
-    prev_light = true;
   }
-  const int ng = (int)gstart.size();
-  gstart.push_back((int32_t)light.size());
-  std::vector<int32_t> gbase(light.size());
-  for (int g = 0; g < ng; ++g)
-    for (int t = gstart[g]; t < gstart[g + 1]; ++t) gbase[t] = light[gstart[g]].z;
-  auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
-    if (int rc = dmalloc(dst, std::max<size_t>(1, cnt))) return rc;
-    if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
-    return FU_OK;
-  };
   h->h_light = light;
-  h->h_gstart = gstart;
-  if (int rc = up(&h->st_tiles, light.data(), light.size())) return rc;
-  if (int rc = up(&h->st_gbase, gbase.data(), gbase.size())) return rc;
-  if (int rc = up(&h->st_heavy, heavy.data(), heavy.size())) return rc;
+  if (int rc = dmalloc(&h->st_tiles, std::max<size_t>(1, light.size()))) return rc;
+  if (int rc = dmalloc(&h->st_heavy, std::max<size_t>(1, heavy.size()))) return rc;
+  if (!light.empty()) HIP_TRY(hipMemcpy(h->st_tiles, light.data(), sizeof(int4) * light.size(), hipMemcpyHostToDevice));
+  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->st_heavy, heavy.data(), sizeof(int4) * heavy.size(), hipMemcpyHostToDevice));
   h->st_ntiles = (int)light.size();
   h->st_nheavy = (int)heavy.size();
-  h->st_ngroups = ng;
   return FU_OK;
 }
 
-// Kernel 8 / 10: the staged-estimate buffer and the four slice layouts.
+// The staged-estimate buffer G and the four slice layouts (element bytes 1, 2, 4, 8; slice =
+// kStageLds / bytes nodes). G is slice-major: for slice s and block part q (the light tiles
+// cut into Q contiguous parts, one stage block each), the tiles' edges whose neighbour lies
+// in slice s, tile by tile, in position order; each (s, q) region padded to 16 elements (a
+// lane stores 16 bytes) with column offset 0 (never read). A tile's edges of one slice are
+// therefore one contiguous run of G: per edge the round kernel reads u16 {position, run}
+// and per tile the run offsets D (G index = m + D[run], m = index in slice order). A layout
+// is built only if every light tile touches at most kStageRuns slices.
 int ensure_stage(fu_handle *h) {
   if (h->st_ready) return FU_OK;
+  if (!h->st_why.empty()) return fail(FU_ERR_GRAPH, h->st_why);
   if (int rc = ensure_light(h)) return rc;
   const int32_t n = h->n;
-  const int ng = h->st_ngroups;
   const std::vector<int4> &light = h->h_light;
-  const std::vector<int32_t> &gstart = h->h_gstart;
+  const int T = (int)light.size();
   auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
     if (int rc = dmalloc(dst, std::max<size_t>(1, cnt))) return rc;
     if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
     return FU_OK;
   };
-  // Staged index space per layout: group g's region holds its (slice, tile, position)
-  // ordered elements, each (group, slice) segment padded to a multiple of kStagePad so the
-  // stage launch moves 8 consecutive elements per lane with 16-byte column loads; a pad
-  // element's column offset is 0 and its staged word is never read.
-  int64_t gmax = 1;
-  for (int li = 0; li < 4; ++li) {
-    const int64_t SN = kStageLds >> li;
-    const int64_t P = (n + SN - 1) / SN;
+  int64_t gmax = 16;
+  std::string why = "kernel 8 (staged slices): no light tiles";
+  for (int li = 0; li < 4 && T > 0; ++li) {
     auto &L = h->st[li];
-    if (P > kStageMaxP) continue;
-    std::vector<int32_t> segs((size_t)ng * (P + 1));
-    std::vector<int32_t> gpos(ng + 1, 0);
-    std::vector<int32_t> cur(P + 1);
-    for (int g = 0; g < ng; ++g) {  // padded segment sizes -> group regions
-      const int32_t ge0 = light[gstart[g]].z, ge1 = light[gstart[g + 1] - 1].w;
-      std::fill(cur.begin(), cur.end(), 0);
-      for (int32_t e = ge0; e < ge1; ++e) cur[h->h_col[e] / SN + 1]++;
-      int32_t acc = 0;
-      for (int64_t s = 0; s < P; ++s) {
-        segs[(size_t)g * (P + 1) + s] = acc;
-        acc += (cur[s + 1] + kStagePad - 1) / kStagePad * kStagePad;
-      }
-      segs[(size_t)g * (P + 1) + P] = acc;
-      if (acc > 65536) return fail(FU_ERR_GRAPH, "kernel 8: staged group region exceeds 2^16 elements");
-      gpos[g + 1] = gpos[g] + acc;
+    const int64_t SN = std::min<int64_t>(kStageLds >> li, 65536);  // column offsets are u16
+    const int64_t P = (n + SN - 1) / SN;
+    if (P > kStageMaxP) {
+      why = "kernel 8 (staged slices): more than " + std::to_string(kStageMaxP) + " slices";
+      continue;
     }
-    const int64_t total = gpos[ng];
-    gmax = std::max<int64_t>(gmax, total);
-    std::vector<uint16_t> colS(std::max<int64_t>(total, kStagePad), 0);  // >= one 16-B load
-    std::vector<uint32_t> sidx(h->E > 0 ? h->E : 1);
-    std::vector<int32_t> gbase(light.size());
-    std::vector<int32_t> kpos;
-    for (int g = 0; g < ng; ++g) {
-      const int t0 = gstart[g], t1 = gstart[g + 1];
-      const int32_t ge0 = light[t0].z, ge1 = light[t1 - 1].w;
-      for (int64_t s = 0; s <= P; ++s) cur[s] = segs[(size_t)g * (P + 1) + s];
-      kpos.assign(ge1 - ge0, 0);
-      for (int32_t e = ge0; e < ge1; ++e) {  // stable: (slice, tile, position) order
-        const int32_t c = h->h_col[e];
-        const int32_t k = cur[c / SN]++;
-        colS[gpos[g] + k] = (uint16_t)(c % SN);
-        kpos[e - ge0] = k;
-      }
-      for (int t = t0; t < t1; ++t) {  // tile elements in slice order (stable in position)
-        gbase[t] = gpos[g];
-        const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
-        std::vector<int32_t> ord(ne);
-        for (int32_t m = 0; m < ne; ++m) ord[m] = m;
-        std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
-          return h->h_col[e0 + x] / SN < h->h_col[e0 + y] / SN;
-        });
-        for (int32_t m = 0; m < ne; ++m)
-          sidx[e0 + m] = ((uint32_t)kpos[e0 + ord[m] - ge0] << 16) | (uint32_t)ord[m];
-      }
-      for (int64_t s = 0; s <= P; ++s) segs[(size_t)g * (P + 1) + s] += gpos[g];  // absolute
-    }
-    // stage blocks (s, q), blockIdx = s + P * q (slice s on XCD s % 8 when 8 | P); slice
-    // s's padded segments are cut into items of <= kStageItem elements (one wave each), and
-    // its Q blocks take equal shares of the item list
-    const int64_t Q = std::max<int64_t>(1, 512 / P);
-    std::vector<int32_t> aoff(P * Q + 1, 0);
-    std::vector<int2> aitem;
-    std::vector<std::vector<int2>> per_s(P);
-    for (int64_t s = 0; s < P; ++s)
-      for (int g = 0; g < ng; ++g) {
-        const int32_t kb = segs[(size_t)g * (P + 1) + s], ke = segs[(size_t)g * (P + 1) + s + 1];
-        for (int32_t k = kb; k < ke; k += kStageItem) per_s[s].push_back(make_int2(k, std::min(kStageItem, ke - k)));
-      }
-    for (int64_t q = 0; q < Q; ++q)
-      for (int64_t s = 0; s < P; ++s) {  // q outer, s inner: b = s + P q in order
-        const int64_t b = s + P * q, ni = (int64_t)per_s[s].size();
-        aoff[b] = (int32_t)aitem.size();
-        for (int64_t i = ni * q / Q; i < ni * (q + 1) / Q; ++i) aitem.push_back(per_s[s][i]);
-      }
-    aoff[P * Q] = (int32_t)aitem.size();
-    // compact sidx: within a tile's slice-order list, the elements of one slice are
-    // consecutive in the group region, so G index - m is constant per run
-    std::vector<uint16_t> s16;
-    std::vector<int32_t> dt;
-    bool compact = kStageTE <= 1024;
-    if (compact) {
-      s16.assign(h->E > 0 ? h->E : 1, 0);
-      dt.assign(light.size() * kStageRuns, 0);
-      for (size_t t = 0; t < light.size() && compact; ++t) {
-        const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
-        int run = -1;
-        int32_t dprev = 0;
-        int64_t sprev = -1;
-        for (int32_t m = 0; m < ne; ++m) {
-          const uint32_t v = sidx[e0 + m];
-          const int32_t pos = (int32_t)(v & 0xFFFFu), kp = (int32_t)(v >> 16);
-          const int64_t sl = h->h_col[e0 + pos] / SN;
-          if (sl != sprev) {
-            if (++run >= kStageRuns) { compact = false; break; }
-            sprev = sl;
-            dprev = kp - m;
-            dt[t * kStageRuns + run] = dprev;
-          } else if (kp - m != dprev) {
-            compact = false;
-            break;
-          }
-          s16[e0 + m] = (uint16_t)(pos | (run << 10));
+    const int64_t Q = std::max<int64_t>(1, std::min<int64_t>(T, (h->n_cu + P / 2) / P));
+    auto part = [&](int t) { return (int64_t)t * Q / T; };
+    // elements per (slice, part) and runs per tile
+    std::vector<int64_t> cnt(P * Q, 0);
+    std::vector<int32_t> stamp(P, -1);
+    bool ok = true;
+    for (int t = 0; t < T && ok; ++t) {
+      int runs = 0;
+      const int64_t q = part(t);
+      for (int32_t e = light[t].z; e < light[t].w; ++e) {
+        const int32_t s = h->h_col[e] / (int32_t)SN;
+        if (stamp[s] != t) {
+          stamp[s] = t;
+          ++runs;
         }
+        cnt[s * Q + q]++;
+      }
+      ok = runs <= kStageRuns;
+    }
+    if (!ok) {
+      why = "kernel 8 (staged slices): a tile touches more than " + std::to_string(kStageRuns) + " slices";
+      continue;
+    }
+    std::vector<int64_t> off(P * Q + 1, 0);
+    for (int64_t k = 0; k < P * Q; ++k) off[k + 1] = off[k] + (cnt[k] + 15) / 16 * 16;
+    const int64_t total = off[P * Q];
+    if (total >= (int64_t)INT32_MAX - 16) {
+      why = "kernel 8 (staged slices): staged index exceeds 2^31";
+      continue;
+    }
+    std::vector<uint16_t> colS(std::max<int64_t>(total, 16), 0);
+    std::vector<uint16_t> s16(h->E > 0 ? h->E : 1, 0);
+    std::vector<int32_t> dt((size_t)T * kStageRuns, 0);
+    std::vector<int64_t> cur(off.begin(), off.end() - 1);
+    std::vector<int32_t> ord;
+    for (int t = 0; t < T; ++t) {
+      const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
+      const int64_t q = part(t);
+      ord.resize(ne);
+      for (int32_t m = 0; m < ne; ++m) ord[m] = m;
+      std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
+        return h->h_col[e0 + x] / SN < h->h_col[e0 + y] / SN;
+      });
+      int run = -1;
+      int64_t sprev = -1;
+      for (int32_t m = 0; m < ne; ++m) {
+        const int32_t pos = ord[m];
+        const int32_t c = h->h_col[e0 + pos];
+        const int64_t s = c / SN;
+        const int64_t gidx = cur[s * Q + q]++;
+        colS[gidx] = (uint16_t)(c % SN);
+        if (s != sprev) {
+          ++run;
+          sprev = s;
+          dt[(size_t)t * kStageRuns + run] = (int32_t)(gidx - m);
+        }
+        s16[e0 + m] = (uint16_t)(pos | (run << 10));
       }
     }
-    if (L.sidx16) hipFree(L.sidx16);
-    if (L.dtab) hipFree(L.dtab);
-    L.sidx16 = nullptr;
-    L.dtab = nullptr;
-    if (compact) {
-      if (int rc = up(&L.sidx16, s16.data(), s16.size())) return rc;
-      if (int rc = up(&L.dtab, dt.data(), dt.size())) return rc;
-    }
+    // stage block of region (s, q) at b = 8 (Q (s / 8) + q) + s % 8: the Q blocks of slice s run
+    // on one XCD (blocks are dealt round-robin over the 8 XCDs; placement only, never
+    // correctness), so the slice's Q - 1 re-reads hit that XCD's L2
+    const int64_t NB = 8 * Q * ((P + 7) / 8);
+    std::vector<int4> br(NB, make_int4(0, 0, 0, 0));
+    for (int64_t s2 = 0; s2 < P; ++s2)
+      for (int64_t q = 0; q < Q; ++q) {
+        const int64_t k = s2 * Q + q, b = 8 * (Q * (s2 / 8) + q) + s2 % 8;
+        br[b] = make_int4((int)off[k], (int)off[k + 1], (int)s2, 0);
+      }
+    for (void *p : {(void *)L.brange, (void *)L.colS, (void *)L.sidx16, (void *)L.dtab})
+      if (p) hipFree(p);
+    L = fu_handle::StageLayout{};
+    if (int rc = up(&L.brange, br.data(), br.size())) return rc;
+    if (int rc = up(&L.colS, colS.data(), colS.size())) return rc;
+    if (int rc = up(&L.sidx16, s16.data(), s16.size())) return rc;
+    if (int rc = up(&L.dtab, dt.data(), dt.size())) return rc;
     L.P = (int)P;
     L.Q = (int)Q;
-    if (int rc = up(&L.aoff, aoff.data(), aoff.size())) return rc;
-    if (int rc = up(&L.aitem, aitem.data(), aitem.size())) return rc;
-    if (int rc = up(&L.colS, colS.data(), colS.size())) return rc;
-    if (int rc = up(&L.sidx, sidx.data(), sidx.size())) return rc;
-    if (int rc = up(&L.gbase, gbase.data(), gbase.size())) return rc;
+    L.SN = (int)SN;
+    L.NB = (int)NB;
+    gmax = std::max<int64_t>(gmax, total);
+  }
+  bool any = false;
+  for (int li = 0; li < 4; ++li) any |= h->st[li].P > 0;
+  if (!any) {
+    h->st_why = why;
+    return fail(FU_ERR_GRAPH, why);
   }
   if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)gmax)) return rc;
   HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long) * (size_t)gmax));
-  bool any = false;
-  for (int li = 0; li < 4; ++li) any |= h->st[li].P > 0;
-  if (!any) return fail(FU_ERR_GRAPH, "kernel 8 (staged slices): graph has too many nodes for a slice layout");
   h->st_ready = true;
   return FU_OK;
 }
@@ -3125,14 +1539,13 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
     const auto &L = h->st[li];
     sa.P[li] = L.P ? L.P : 1;
     sa.Q[li] = L.P ? L.Q : 0;
-    sa.aoff[li] = L.aoff;
-    sa.aitem[li] = L.aitem;
+    sa.SN[li] = L.SN;
+    sa.NB[li] = L.NB;
+    sa.brange[li] = L.brange;
     sa.colS[li] = L.colS;
-    sa.sidx[li] = L.sidx;
-    sa.gbase[li] = L.gbase;
-    sa.sidx16[li] = h->st_compact ? L.sidx16 : nullptr;
+    sa.sidx16[li] = L.sidx16;
     sa.dtab[li] = L.dtab;
-    if (L.P) g = std::max<unsigned>(g, (unsigned)(L.P * L.Q));
+    if (L.P) g = std::max<unsigned>(g, (unsigned)L.NB);
   }
   for (int want = 0; want < 4; ++want) {
     int pick = -1;
@@ -3147,300 +1560,139 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
   return sa;
 }
 
-int ensure_a2(fu_handle *h) {
-  if (h->a[2]) return FU_OK;
-  if (int rc = dmalloc(&h->a[2], (size_t)h->na)) return rc;
-  HIP_TRY(hipMemset(h->a[2], 0, sizeof(double) * h->na));
-  return FU_OK;
-}
-
-int ensure_inbox(fu_handle *h) {
-  if (h->inbox[0]) return FU_OK;
-  for (int k = 0; k < 2; ++k)
-    if (int rc = dmalloc(&h->inbox[k], (size_t)h->E)) return rc;
-  return FU_OK;
-}
-
 inline unsigned grid_for(long long work) { return (unsigned)((work + kBlock - 1) / kBlock); }
 
-// One round: state in buffer `cur` -> buffer `cur ^ 1`. err_slot: nullptr = no check.
+// One round: state of round r-1 -> round r. err_slot: nullptr = no check.
 int launch_round(fu_handle *h, unsigned long long *err_slot) {
-  const int src = h->cur, dst = h->cur ^ 1;
   const bool check = err_slot != nullptr;
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 0)) return rc;
   }
-  if (h->kernel >= 4) {
-    const int64_t r = h->rounds;
-    if (r == 0) {
-      hipLaunchKernelGGL(k_round0<true>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
-                         h->rowptr, h->v, h->f[0], h->a[0]);
-      if (h->E)
-        hipLaunchKernelGGL(k_round0_flows, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, h->n,
-                           (long long)h->E, h->rowptr, h->a[0], h->f[0]);
-      if (h->E)  // f_{-1} = -0.0 (split words) so that round 1 reproduces (0.0 + a) - 0.0
-        hipLaunchKernelGGL(k_fill_split, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
-                           -0.0, h->f[1]);
-      HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
-      HIP_TRY(hipMemsetAsync(h->pctl, 0, sizeof(PackCtl) * 3, h->stream));      // no codes yet
-      if (check)
-        hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
-                           h->stream, h->n, h->a[0], h->target, err_slot);
-    } else if (h->kernel == 6) {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      const unsigned gblocks = (unsigned)((h->e0_count + kGatherChunk - 1) / kGatherChunk);
-      if (gblocks)
-        hipLaunchKernelGGL(k_gather_part0, dim3(gblocks), dim3(kBlock), 0, h->stream, h->colpm,
-                           (long long)h->e0_count, ap, h->G);
-      if (check)
-        hipLaunchKernelGGL((k_round_split<true, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
-                           h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
-                           h->G, ap2, an, h->target, err_slot, h->pctl, (int)(r & 1), h->colpm, ap);
-      else
-        hipLaunchKernelGGL((k_round_split<false, true>), dim3(h->ntiles_s), dim3(kBlock), 0, h->stream,
-                           h->tiles_s, h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F,
-                           h->G, ap2, an, h->target, err_slot, h->pctl, (int)(r & 1), h->colpm, ap);
-    } else if (h->kernel == 5) {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      const long long E1 = h->E - h->e0_count;
-      const long long mx = std::max<long long>(h->e0_count, E1);
-      const unsigned gblocks = (unsigned)(8 * ((mx + 4LL * kGatherChunk - 1) / (4LL * kGatherChunk)));
-      if (gblocks)
-        hipLaunchKernelGGL(k_gather_split, dim3(gblocks), dim3(kBlock), 0, h->stream, h->colpm,
-                           (long long)h->e0_count, (long long)h->E, ap, h->G);
-      if (check)
-        hipLaunchKernelGGL(k_round_split<true>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
-                           h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
-                           h->target, err_slot, h->pctl, (int)(r & 1));
-      else
-        hipLaunchKernelGGL(k_round_split<false>, dim3(h->ntiles_s), dim3(kBlock), 0, h->stream, h->tiles_s,
-                           h->tiles_g, h->rowptr, h->rowptr0, (long long)h->e0_count, h->v, F, h->G, ap2, an,
-                           h->target, err_slot, h->pctl, (int)(r & 1));
-    } else if (h->kernel == 9 || h->kernel == 10) {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      const void *cp = h->code[(r - 1) & 1];
-      const bool staged = h->kernel == 10;
-      unsigned sgrid = 1;
-      const StageArgs sa = staged ? stage_args(h, &sgrid) : StageArgs{};
-      if (staged && h->st_ngroups)
-        hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
-                           (int)(r & 1), h->stG);
-      long long nbl = std::max<long long>((h->st_ntiles + kPipeChunk - 1) / kPipeChunk, (long long)h->pipe_bpc * h->n_cu);
-      nbl = std::min<long long>(nbl, ((long long)h->st_ntiles + 7) / 8 * 8);
-      nbl = std::max<long long>(8, (nbl + 7) / 8 * 8);
-      const dim3 grid((unsigned)(nbl + h->st_nheavy));
-#define FU_PIPE(C, M)                                                                                  \
-  hipLaunchKernelGGL((k_round_pipe<C, M>), grid, dim3(kBlock), 0, h->stream, h->st_tiles, h->st_gbase,       \
-                     h->st_ntiles, h->st_heavy, h->st_nheavy, h->rowptr, h->col, sa, h->stG, h->v, F, ap,     \
-                     ap2, an, h->target, err_slot, cp, h->code[r & 1], h->pctl, (int)(r & 1),           \
-                     (int)std::max<int64_t>(0, h->E - 1))
-      if (check) {
-        if (staged) FU_PIPE(true, 1); else FU_PIPE(true, 0);
-      } else {
-        if (staged) FU_PIPE(false, 1); else FU_PIPE(false, 0);
-      }
-#undef FU_PIPE
-    } else if (h->kernel == 8) {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      unsigned sgrid = 1;
-      const StageArgs sa = stage_args(h, &sgrid);
-      const void *cp = h->code[(r - 1) & 1];
-      if (h->st_ngroups && h->diag < 2)
-        hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
-                           (int)(r & 1), h->stG);
-      if (h->st_nheavy) {
-        if (check)
-          hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
-                             h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
-        else
-          hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
-                             h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
-      }
+  const int64_t r = h->rounds;
+  if (r == 0) {
+    // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91); f_{-1} = -0.0 and
+    // a_{-1} = 0.0 so that round 1 reproduces round 0's (0.0 + a) - 0.0
+    hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n, h->rowptr, h->v, h->a[0]);
+    if (h->E)
+      hipLaunchKernelGGL(k_round0_flows, dim3((unsigned)((h->E + kR0E - 1) / kR0E)), dim3(kBlock), 0, h->stream,
+                         (long long)h->E, h->rowptr, h->blk_row, h->a[0], h->f[0], h->f[1]);
+    HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
+    HIP_TRY(hipMemsetAsync(h->pctl, 0, sizeof(PackCtl) * 3, h->stream));      // no codes yet
+    if (check)
+      hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
+                         h->a[0], h->target, err_slot);
+  } else if (h->kernel == 8) {
+    double *F = h->f[r & 1];
+    const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+    double *an = h->a[r % 3];
+    unsigned sgrid = 1;
+    const StageArgs sa = stage_args(h, &sgrid);
+    const void *cp = h->code[(r - 1) & 1];
 #ifdef FU_DIAG
-      if (h->st_ntiles && h->diag == 4) {  // round launch alone (stale G: timing only)
-        hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 4>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                           h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
-                           h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-      } else if (h->st_ntiles && h->diag) {
-        if (h->diag == 3)
-          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 3>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
-                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-        else
-          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN, 1>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
-                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-      } else
+    const bool stage = h->diag < 2;
+#else
+    const bool stage = true;
 #endif
-      if (h->st_ntiles) {
-        if (check)
-          hipLaunchKernelGGL((k_round_staged<true, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
-                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-        else
-          hipLaunchKernelGGL((k_round_staged<false, kStageTE, kStageTN>), dim3(h->st_ntiles), dim3(kBlock), 0,
-                             h->stream, h->st_tiles, h->st_gbase, h->st_ntiles, h->rowptr, h->col, sa, h->stG,
-                             h->v, F, ap, ap2, an, h->target, err_slot, h->code[r & 1], h->pctl, (int)(r & 1));
-      }
-    } else if (h->kernel == 7) {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      const int wg = h->wgeo;
-      if (h->nwheavy[wg]) {
-        if (check)
-          hipLaunchKernelGGL((k_round_recon<true, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
-                             h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
-        else
-          hipLaunchKernelGGL((k_round_recon<false, false, 0, 2048, 256>), dim3(h->nwheavy[wg]), dim3(kBlock), 0,
-                             h->stream, h->wheavy[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
-      }
-      if (h->nwtiles[wg]) {
-        const unsigned blocks = (unsigned)((h->nwtiles[wg] + kBlock / 64 - 1) / (kBlock / 64));
-#define FU_WAVE(C, TE, TN)                                                                          \
-  hipLaunchKernelGGL((k_round_wave<C, TE, TN>), dim3(blocks), dim3(kBlock), 0, h->stream, h->wtiles[wg], \
-                     h->nwtiles[wg], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,         \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1))
-        if (wg == 0) {
-          if (check) FU_WAVE(true, 256, 32); else FU_WAVE(false, 256, 32);
-        } else {
-          if (check) FU_WAVE(true, 512, 64); else FU_WAVE(false, 512, 64);
-        }
-#undef FU_WAVE
-      }
+    if (h->st_ntiles && stage)
+      hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
+                         (int)(r & 1), h->stG);
+    if (h->st_nheavy) {
+      if (check)
+        hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
+                           h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0);
+      else
+        hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
+                           h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0);
+    }
+#define FU_STAGED(C, D)                                                                                  \
+  hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
+                     h->st_tiles, h->st_ntiles, h->rowptr, h->col, sa, h->stG, h->v, F, ap, ap2, an, h->target, \
+                     err_slot, h->code[r & 1], h->pctl, (int)(r & 1))
+    if (h->st_ntiles) {
+#ifdef FU_DIAG
+      if (h->diag == 4) FU_STAGED(false, 4);
+      else if (h->diag == 3) FU_STAGED(false, 3);
+      else if (h->diag) FU_STAGED(false, 1);
+      else
+#endif
+      if (check) FU_STAGED(true, 0);
+      else FU_STAGED(false, 0);
+    }
+#undef FU_STAGED
+  } else {
+    double *F = h->f[r & 1];
+    const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
+    double *an = h->a[r % 3];
+    // heavy tiles (hubs, heavy rows) lead the tile list: they run as their own launch on the
+    // side stream, concurrently with the light tiles' launch (which then keeps kernel 4's
+    // light-path register budget)
+    const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
+    const int hub_sep = h->n_hub ? 1 : 0;  // k_hub_flows writes the hubs' flows after the chains
+    const bool fork = nh > 0 && h->fork_heavy;
+    hipStream_t hs = fork ? h->stream2 : h->stream;
+    if (fork) {
+      HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+      HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+    }
+    if (h->n_hub)
+      hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
+                         (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
+                         h->hubxy);
+#define FU_RECON_G(C, N, D, TE, TN)                                                                       \
+  do {                                                                                                    \
+    if (nh)                                                                                               \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, \
+                         hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
+                         h->hrows, hub_sep);                                                              \
+    if (nl)                                                                                               \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl), dim3(kBlock), 0, h->stream,        \
+                         h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
+                         err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
+                         nullptr, nullptr, 0);                                                            \
+  } while (0)
+#define FU_RECON(C, N, D)                                                                                 \
+  do {                                                                                                    \
+    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                                      \
+    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                                 \
+    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                                 \
+    else FU_RECON_G(C, N, D, 512, 64);                                                                    \
+  } while (0)
+#ifdef FU_DIAG
+    if (h->diag == 1) FU_RECON(false, false, 1);
+    else if (h->diag == 2) FU_RECON(false, false, 2);
+    else if (h->diag == 3) FU_RECON(false, false, 3);
+    else if (h->diag == 4) FU_RECON(false, false, 4);
+    else if (h->diag == 5) FU_RECON(false, false, 5);
+    else if (h->diag == 6) FU_RECON(false, false, 6);
+    else if (h->diag == 12) FU_RECON(false, false, 12);
+    else
+#endif
+    if (check) {
+      if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
     } else {
-      double *F = h->f[r & 1];
-      const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-      double *an = h->a[r % 3];
-      // heavy tiles (hubs, heavy rows, bins) lead the tile list: they run as their own launch
-      // on the side stream, concurrently with the light tiles' launch (which then keeps
-      // kernel 4's light-path register budget: 64 VGPRs, 8 waves per SIMD)
-      const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
-      const int hub_sep = h->n_hub && !(h->geo == 0 && h->bins) ? 1 : 0;  // k_hub_flows after
-      const bool fork = nh > 0 && h->fork_heavy;
-      hipStream_t hs = fork ? h->stream2 : h->stream;
-      if (fork) {
-        HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-      }
-      if (h->n_hub && !(h->geo == 0 && h->bins)) {
-        if (h->hub_scan) {  // pieces: (fr, er) + approximate sums, then the run summaries
-          hipLaunchKernelGGL(k_hub_stage_p, dim3(h->n_piece), dim3(kBlock), 0, hs, h->hub_piece, h->hub_rows,
-                             h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->hubxy, h->psum);
-          hipLaunchKernelGGL(k_hub_sum, dim3(h->n_piece), dim3(kBlock), 0, hs, h->hub_piece, h->hub_p0,
-                             h->psum, h->hubxy, h->hsum);
-        } else {
-          hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub,
-                             h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1],
-                             h->pctl, (int)(r & 1), h->hubxy);
-        }
-      }
-#define FU_RECON_G(C, N, D, TE, TN)                                                         \
-  do {                                                                                      \
-    if (nh)                                                                                 \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, hs, \
-                         h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->perm, \
-                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, \
-                         h->hrows, h->hub_scan ? h->hsum : nullptr, h->hub_p0, h->hub_redo, hub_sep); \
-    if (nl)                                                                                 \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl), dim3(kBlock), 0, h->stream, \
-                         h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
-                         h->perm, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, \
-                         nullptr, nullptr, nullptr, nullptr, 0);                             \
-  } while (0)
-#define FU_RECON(C, N, D)                                                                   \
-  do {                                                                                      \
-    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                        \
-    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                   \
-    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                   \
-    else FU_RECON_G(C, N, D, 512, 64);                                                      \
-  } while (0)
-#ifdef FU_DIAG
-      if (h->diag == 1) FU_RECON(false, false, 1);
-      else if (h->diag == 2) FU_RECON(false, false, 2);
-      else if (h->diag == 3) FU_RECON(false, false, 3);
-      else if (h->diag == 4) FU_RECON(false, false, 4);
-      else if (h->diag == 5) FU_RECON(false, false, 5);
-      else if (h->diag == 6) FU_RECON(false, false, 6);
-      else if (h->diag == 12) FU_RECON(false, false, 12);
-      else
-#endif
-      if (check) {
-        if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
-      } else {
-        if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
-      }
+      if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
+    }
 #undef FU_RECON
 #undef FU_RECON_G
-      if (hub_sep)
-        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                           (long long)h->hub_total, h->hubxy, an, F);
-      if (fork) {
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
-        HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-      }
+    if (hub_sep)
+      hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
+                         (long long)h->hub_total, h->hubxy, an, F);
+    if (fork) {
+      HIP_TRY(hipGetLastError());
+      HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+      HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     }
-  } else if (h->rounds == 0) {
-    if (h->kernel == 3) {
-      hipLaunchKernelGGL(k_round0_push, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
-                         h->rowptr, h->rev, h->v, h->inbox[dst], h->a[dst]);
-    } else {
-      hipLaunchKernelGGL(k_round0<false>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n,
-                         h->rowptr, h->v, h->f[dst], h->a[dst]);
-    }
-    if (check) {
-      hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0,
-                         h->stream, h->n, h->a[dst], h->target, err_slot);
-    }
-  } else if (h->kernel == 1) {
-    if (check)
-      hipLaunchKernelGGL(k_round_tpn<true>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream,
-                         h->n, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src], h->f[dst],
-                         h->a[dst], h->target, err_slot);
-    else
-      hipLaunchKernelGGL(k_round_tpn<false>, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream,
-                         h->n, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src], h->f[dst],
-                         h->a[dst], h->target, err_slot);
-  } else if (h->kernel == 2) {
-    if (check)
-      hipLaunchKernelGGL(k_round_tile<true>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
-                         h->tiles, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src],
-                         h->f[dst], h->a[dst], h->target, err_slot);
-    else
-      hipLaunchKernelGGL(k_round_tile<false>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
-                         h->tiles, h->rowptr, h->col, h->rev, h->v, h->f[src], h->a[src],
-                         h->f[dst], h->a[dst], h->target, err_slot);
-  } else {
-    if (check)
-      hipLaunchKernelGGL(k_round_push<true>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
-                         h->tiles, h->rowptr, h->rev, h->v, h->inbox[src], h->inbox[dst],
-                         h->a[dst], h->target, err_slot);
-    else
-      hipLaunchKernelGGL(k_round_push<false>, dim3(h->ntiles), dim3(kBlock), 0, h->stream,
-                         h->tiles, h->rowptr, h->rev, h->v, h->inbox[src], h->inbox[dst],
-                         h->a[dst], h->target, err_slot);
   }
   HIP_TRY(hipGetLastError());
-  h->cur = dst;
   h->rounds++;
-  // refresh the packing plan from a_r (kernel 4 encodes with it from the next round on);
-  // once the host has seen the narrowest width (8), every 8th time only: the plan and its
-  // width copy stall the stream for ~20 us
+  // refresh the packing plan from a_r (the round kernels encode with it from the next round
+  // on); once the host has seen the narrowest width (8), every 8th time only: the plan and
+  // its width copy stall the stream for ~20 us
   const int every = h->seen_width == 8 ? 8 * h->pack_every : h->pack_every;
-  if (h->kernel >= 4 && h->pack && !h->dist && h->n_psample > 0 && h->rounds % every == 0) {
+  if (h->pack && !h->dist && h->n_psample > 0 && h->rounds % every == 0) {
     hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample, h->pctl);
     HIP_TRY(hipGetLastError());
     if (!h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
@@ -3455,23 +1707,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   return FU_OK;
 }
 
+// Autotune candidates, fixed order (fu_get_info reports per index). Kernel 8 is single-GPU.
 struct TuneCand {
-  int kernel, nt, geo;
+  int kernel, geo;
 };
-// kernel 7 (wave tiles) is not a candidate: slower than kernel 4 at 512x64 everywhere
-// measured; it stays selectable as an option
-// measured on ER-1M / R-MAT: 4+nt, 4 at 1024x256, 5 and 9 never win; they stay options
-static std::vector<TuneCand> tune_cands(const fu_handle *h) {
-  // fixed order (fu_get_info reports per index); kernels 6, 8, 10 are single-GPU only
-  (void)h;
-  return {{4, 0, 0}, {4, 0, 3}, {6, 0, 0}, {8, 0, 0}, {10, 0, 0}, {4, 0, 1}};
-}
+constexpr TuneCand kCands[] = {{4, 0}, {4, 3}, {8, 1}, {4, 1}};
+constexpr int kNCands = (int)(sizeof(kCands) / sizeof(kCands[0]));
 static int width_class(int w) { return w == 8 ? 1 : w == 16 ? 2 : w == 32 ? 3 : 0; }
 static void use_cand(fu_handle *h, const TuneCand &c) {
   h->kernel = c.kernel;
-  h->nt = c.nt;
-  if (h->kernel == 7) h->wgeo = c.geo;
-  else h->geo = c.geo;
+  h->geo = c.geo;
 }
 
 int set_device(fu_handle *h) {
@@ -3491,17 +1736,15 @@ int fu_device_count(int32_t *out) {
   return FU_OK;
 }
 
-// Internal constructor shared by fu_create / fu_dist_create: uploads the local CSR.
+// Internal constructor shared by fu_create / fu_dist_create: uploads the local CSR. The
+// kernels never read a reverse-edge index (flows are reconstructed, kernel 4 §4.1), so only
+// rowptr, col and the values go to the device. a_extra: ghost estimate slots (multi-GPU).
 int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
-                      const int32_t *rev, const double *value, int32_t device,
-                      int64_t f_extra, int32_t a_extra, fu_handle **out) {
+                      const double *value, int32_t device, int32_t a_extra, fu_handle **out) {
   FU_TRY_BEGIN
-  // rev may be NULL only for the estimates-only multi-GPU halo (kernel 4 never reads rev)
-  if (!out || n <= 0 || e < 0 || !rowptr || !value || (e > 0 && !col) || (e > 0 && !rev && f_extra != -1))
+  if (!out || n <= 0 || e < 0 || !rowptr || !value || (e > 0 && !col) || a_extra < 0)
     return fail(FU_ERR_ARG, "fu_create: bad arguments");
-  const bool no_rev = f_extra == -1;
-  if (no_rev) f_extra = 0;
-  if (e + f_extra >= (int64_t)INT32_MAX) return fail(FU_ERR_ARG, "fu_create: more than 2^31-1 edges");
+  if (e >= (int64_t)INT32_MAX - 64) return fail(FU_ERR_ARG, "fu_create: more than 2^31-1 edges");
   if (rowptr[0] != 0 || rowptr[n] != e) return fail(FU_ERR_ARG, "fu_create: rowptr[0] must be 0 and rowptr[n] == e");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(FU_ERR_HIP, "fu_create: no HIP device visible");
@@ -3522,13 +1765,12 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     }
   }
   h->max_deg = md;
-  const int64_t fe = e + f_extra;
   const int32_t na = n + a_extra;
   h->na = na;
   for (int64_t k = 0; k < e; ++k) {
-    if (col[k] < 0 || col[k] >= na || (!no_rev && (rev[k] < 0 || rev[k] >= fe))) {
+    if (col[k] < 0 || col[k] >= na) {
       delete h;
-      return fail(FU_ERR_ARG, "fu_create: col/rev index out of range at edge " + std::to_string(k));
+      return fail(FU_ERR_ARG, "fu_create: col index out of range at edge " + std::to_string(k));
     }
   }
   int rc = FU_OK;
@@ -3555,26 +1797,37 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
   *h->h_pw = 0;
-  if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (!no_rev && (rc = dmalloc(&h->rev, e))) ||
-      (rc = dmalloc(&h->v, n)) || (rc = dmalloc(&h->f[0], (fe + 31) / 32 * 32)) ||
-      (rc = dmalloc(&h->f[1], (fe + 31) / 32 * 32)) ||
-      (rc = dmalloc(&h->a[0], na)) || (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->target, n)) ||
+  const int64_t fe = (e + 31) / 32 * 32;  // split-word flows: whole 32-edge blocks
+  if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (rc = dmalloc(&h->v, n)) ||
+      (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) || (rc = dmalloc(&h->a[0], na)) ||
+      (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->a[2], na)) || (rc = dmalloc(&h->target, n)) ||
       (rc = dmalloc(&h->err, 1)))
     return cleanup(rc);
   h->errcap = 1;
   if (hipMemcpy(h->rowptr, rp32.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice) != hipSuccess ||
       (e && hipMemcpy(h->col, col, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
-      (e && !no_rev && hipMemcpy(h->rev, rev, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(h->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
-  if ((e == 0 && hipMemset(h->col, 0, sizeof(int)) != hipSuccess) ||  // kernels 9/10 read col[0]
-      hipMemset(h->f[0], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
-      hipMemset(h->f[1], 0, sizeof(double) * (fe ? fe : 1)) != hipSuccess ||
-      hipMemset(h->a[0], 0, sizeof(double) * na) != hipSuccess ||
-      hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess)
+  if ((e == 0 && hipMemset(h->col, 0, sizeof(int)) != hipSuccess) ||
+      hipMemset(h->f[0], 0, sizeof(double) * std::max<int64_t>(fe, 1)) != hipSuccess ||
+      hipMemset(h->f[1], 0, sizeof(double) * std::max<int64_t>(fe, 1)) != hipSuccess ||
+      hipMemset(h->a[0], 0, sizeof(double) * na) != hipSuccess || hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess ||
+      hipMemset(h->a[2], 0, sizeof(double) * na) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
+  {  // round 0's per-block rows
+    const int64_t nblk = (e + kR0E - 1) / kR0E;
+    std::vector<int32_t> br(nblk + 1, 0);
+    int32_t i = 0;
+    for (int64_t b = 0; b <= nblk; ++b) {
+      const int64_t k = b < nblk ? b * kR0E : e - 1;
+      while (i + 1 < n && rowptr[i + 1] <= k) ++i;  // last row with rowptr[i] <= k
+      br[b] = i;
+    }
+    if ((rc = dmalloc(&h->blk_row, br.size()))) return cleanup(rc);
+    if (hipMemcpy(h->blk_row, br.data(), sizeof(int32_t) * br.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
+  }
   if ((rc = build_tiles(h))) return cleanup(rc);
-  if ((rc = ensure_a2(h))) return cleanup(rc);
   if ((rc = dmalloc(&h->pctl, 3)) || (rc = dmalloc(&h->code[0], 4 * (size_t)na)) ||
       (rc = dmalloc(&h->code[1], 4 * (size_t)na)))
     return cleanup(rc);
@@ -3593,22 +1846,30 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   FU_TRY_END
 }
 
+// The flow reconstruction needs every i -> j to have its j -> i: a caller's rev is checked to
+// be that pairing; without one, fu::build_rev checks symmetry (the index itself is not kept).
 int fu_create(int32_t n, int64_t e, const int64_t *rowptr, const int32_t *col,
               const int32_t *rev, const double *value, int32_t device, fu_handle **out) {
   FU_TRY_BEGIN
-  if (!rowptr || n <= 0) return fail(FU_ERR_ARG, "fu_create: bad arguments");
-  std::vector<int32_t> own_rev;
-  if (!rev && e > 0) {
+  if (!rowptr || n <= 0 || e < 0 || (e > 0 && !col)) return fail(FU_ERR_ARG, "fu_create: bad arguments");
+  if (rowptr[0] != 0 || rowptr[n] != e) return fail(FU_ERR_ARG, "fu_create: rowptr[0] must be 0 and rowptr[n] == e");
+  if (e > 0 && !rev) {
     fu_graph g;
     g.n = n;
     g.rowptr.assign(rowptr, rowptr + n + 1);
-    if (!col) return fail(FU_ERR_ARG, "fu_create: col is NULL");
     g.col.assign(col, col + e);
     if (int rc = fu::build_rev(g)) return rc;
-    own_rev.swap(g.rev);
-    rev = own_rev.data();
+  } else if (e > 0) {
+    for (int32_t i = 0; i < n; ++i)
+      for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+        const int32_t j = col[k];
+        const int64_t r = rev[k];
+        if (j < 0 || j >= n || r < rowptr[j] || r >= rowptr[j + 1] || col[r] != i)
+          return fail(FU_ERR_GRAPH, "fu_create: rev is not the reverse-edge pairing (the graph must be symmetric) at edge " +
+                                        std::to_string(k));
+      }
   }
-  return fu__create_common(n, e, rowptr, col, rev, value, device, 0, 0, out);
+  return fu__create_common(n, e, rowptr, col, value, device, 0, out);
   FU_TRY_END
 }
 
@@ -3617,7 +1878,7 @@ int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
   if (!g) return fail(FU_ERR_ARG, "fu_create_from_graph: NULL graph");
   const int64_t E = g->rowptr[g->n];
   if ((int64_t)g->rev.size() != E) return fail(FU_ERR_GRAPH, "fu_create_from_graph: graph is not symmetric");
-  return fu__create_common(g->n, E, g->rowptr.data(), g->col.data(), g->rev.data(), value, device, 0, 0, out);
+  return fu__create_common(g->n, E, g->rowptr.data(), g->col.data(), value, device, 0, out);
 }
 
 int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t device,
@@ -3644,49 +1905,21 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value < 0 || value > 10) return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0..10");
-    if (h->dist && value != 0 && value != 2 && value != 4)  // 5, 6: single GPU only
-      return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 2 (pull) and 4 (recon)");
-    if (!h->rev && h->E > 0 && value >= 1 && value <= 3)
-      return fail(FU_ERR_ARG, "fu_set_option: kernels 1-3 need the reverse-edge index (estimates-only halo)");
+    if (value != 0 && value != 4 && value != 8)
+      return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon) or 8 (stage)");
+    if (h->dist && value == 8) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernel 4 (recon)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
+    if (value == 8) {
+      if (int rc = ensure_stage(h)) return rc;
+    }
     h->kernel = value == 0 ? 4 : (int)value;
     h->autotune = value == 0;
     h->tuned = false;
-    h->nt = 0;
-    if (h->kernel == 3) return ensure_inbox(h);
-    if (h->kernel == 4 || h->kernel == 7) return ensure_a2(h);
-    if (h->kernel == 9) {
-      if (int rc = ensure_a2(h)) return rc;
-      if (int rc = ensure_light(h)) {
-        h->kernel = 4;
-        return rc;
-      }
-    }
-    if (h->kernel == 8 || h->kernel == 10) {
-      if (int rc = ensure_a2(h)) return rc;
-      if (int rc = ensure_stage(h)) {
-        h->kernel = 4;
-        return rc;
-      }
-    }
-    if (h->kernel == 5 || h->kernel == 6) {
-      if (int rc = ensure_a2(h)) return rc;
-      if (int rc = ensure_split(h)) {
-        h->kernel = 4;
-        return rc;
-      }
-    }
     return FU_OK;
   }
   if (!std::strcmp(key, "stage_layout")) {  // kernel 8: -1 = by packing width, 0..3 forced
     if (value < -1 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: stage_layout must be -1..3");
     h->st_force = (int)value;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "pipe_bpc")) {  // kernels 9/10: persistent blocks per CU
-    if (value < 1 || value > 64) return fail(FU_ERR_ARG, "fu_set_option: pipe_bpc must be in [1, 64]");
-    h->pipe_bpc = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "diag")) {  // timing-only ablations (wrong results): tools builds only
@@ -3712,15 +1945,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->pack_every = (int)value;
     return FU_OK;
   }
-  if (!std::strcmp(key, "bins")) {
-    h->bins = value != 0;
-    return build_tiles(h);
-  }
-  if (!std::strcmp(key, "wave_edges")) {  // kernel 7 wave tile: 256 (x32 nodes) or 512 (x64)
-    if (value != 256 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: wave_edges must be 256 or 512");
-    h->wgeo = value == 512;
-    return FU_OK;
-  }
   if (!std::strcmp(key, "tile_edges")) {
     if (value != 2048 && value != 1024 && value != 512) return fail(FU_ERR_ARG, "fu_set_option: tile_edges must be 2048, 1024 or 512");
     h->tile_edges = (int)value;
@@ -3733,16 +1957,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->geo = h->tile_edges == 2048 ? 0 : h->tile_edges == 512 ? 3 : h->tile_nodes == 256 ? 2 : 1;
     return FU_OK;
   }
-  if (!std::strcmp(key, "stage_compact")) {  // kernel 8: u16 sidx with per-tile runs (1) or u32 (0)
-    h->st_compact = value != 0;
-    return FU_OK;
-  }
   if (!std::strcmp(key, "fork_heavy")) {  // kernel 4: heavy tiles on a side stream (1) or in order (0)
     h->fork_heavy = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_scan")) {  // mega hubs: parallel exact sums (1) or one chain (0)
-    h->hub_scan = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "wave_heavy")) {  // kernel 4: heavy rows one per wave (1) or per block (0)
@@ -3756,7 +1972,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "hub_threshold")) {
     if (value < 1) return fail(FU_ERR_ARG, "fu_set_option: hub_threshold must be >= 1");
-    h->hub_threshold = (int)std::min<int64_t>(value, kTileEdges);
+    if (h->st_tiles) return fail(FU_ERR_STATE, "fu_set_option: hub_threshold must be set before kernel 8 is prepared");
+    h->hub_threshold = (int)std::min<int64_t>(value, 2048);
     return build_tiles(h);
   }
   return fail(FU_ERR_ARG, std::string("fu_set_option: unknown key '") + key + "'");
@@ -3767,12 +1984,11 @@ int fu_reset(fu_handle *h) {
   if (int rc = set_device(h)) return rc;
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
-  h->cur = 0;
   h->pw_pending = false;  // the stream is idle: no plan copy in flight
   *h->h_pw = 0;           // round 0 clears the packing plan
   h->seen_width = 0;
   if (h->autotune && h->tuned && h->tune_cache[0] >= 0) {  // unpacked again: its winner
-    use_cand(h, tune_cands(h)[h->tune_cache[0]]);
+    use_cand(h, kCands[h->tune_cache[0]]);
     h->tuned_width = 0;
   }
   return FU_OK;
@@ -3803,57 +2019,35 @@ int fu__err_slots(fu_handle *h, int count) {
   return FU_OK;
 }
 
-// Kernels 4, 5 and 6 share the state layout (F[r & 1], A[r % 3]) and are all bitwise
-// exact, so switching between them (or between kernel 4's tile geometries) mid-run changes
-// nothing but speed. "auto" times each candidate on real rounds (1 warm + 4 timed each)
-// once round 0 is done and keeps the fastest. The rounds count toward the caller's total,
-// and the results are unchanged. The pass re-runs when the packing plan changes width (the
-// packed gather shifts the balance between the candidates), at most kMaxTunes times.
+// Kernels 4 (every geometry) and 8 share the state layout (F[r & 1], A[r % 3]) and are
+// bitwise identical, so switching between them mid-run changes nothing but speed. "auto"
+// times each candidate on real rounds (1 warm + 8 timed each) and keeps the fastest. The
+// rounds count toward the caller's total and the results are unchanged. The pass re-runs
+// when the packing plan changes width (the packed gather shifts the balance between the
+// candidates), at most kMaxTunes times; fu_tune runs one pass on demand.
 constexpr int kMaxTunes = 4;
+constexpr int kTimed = 8;
 
-// width: the packing width the pass runs under (kernel 6 writes unpacked tables, so it is
-// only a candidate while the table is unpacked)
 static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
-  const std::vector<TuneCand> cands = tune_cands(h);
-  constexpr int kTimed = 8;
-  auto active = [&](size_t c) {
-    // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
-    // candidate is dropped and none stops early on rank-local timings
-    return (h->dist || h->tune_out[c] < 2) && !(cands[c].kernel == 6 && width != 0) && !(h->dist && cands[c].kernel != 4);
-  };
+  // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
+  // candidate is dropped and none stops early on rank-local timings
+  auto active = [&](int c) { return (h->dist || h->tune_out[c] < 2) && !(h->dist && kCands[c].kernel != 4); };
   int32_t need = 0;
-  for (size_t c = 0; c < cands.size(); ++c) need += active(c) ? 1 + kTimed : 0;
+  for (int c = 0; c < kNCands; ++c) need += active(c) ? 1 + kTimed : 0;
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
   int bi = -1;
-  for (size_t c = 0; c < cands.size(); ++c) {
-    // a candidate more than 1.3x slower than the winner in two passes sits out the later
-    // ones (its last ns per round stays reported)
-    if (!h->dist && h->tune_out[c] >= 2) continue;
+  for (int c = 0; c < kNCands; ++c) {
+    if (!h->dist && h->tune_out[c] >= 2) continue;  // its last ns per round stays reported
     h->tune_ms[c] = 0.f;
     if (!active(c)) continue;
-    if (cands[c].kernel == 9) {
-      if (ensure_light(h) != FU_OK) {
-        set_error("");
-        continue;
-      }
-    } else if (cands[c].kernel == 8 || cands[c].kernel == 10) {
-      if (ensure_stage(h) != FU_OK) {  // too many nodes for a slice layout
-        set_error("");
-        continue;
-      }
-    } else if (cands[c].kernel >= 5) {
-      if (ensure_split(h) != FU_OK) {  // rows not sorted: column split not applicable
-        set_error("");
-        continue;
-      }
+    if (kCands[c].kernel == 8 && ensure_stage(h) != FU_OK) {  // no slice layout fits this graph
+      set_error("");
+      continue;
     }
-    h->kernel = cands[c].kernel;
-    h->nt = cands[c].nt;
-    if (h->kernel == 7) h->wgeo = cands[c].geo;
-    else h->geo = cands[c].geo;
+    use_cand(h, kCands[c]);
     // the warm round is timed too: a candidate more than twice the best per-round time so far
-    // stops there (on R-MAT-24 the staged kernels take 3x kernel 4: 8 rounds of 30 ms each)
+    // stops there (on R-MAT-24 the staged kernel would take 3x kernel 4 for 8 rounds)
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
@@ -3878,13 +2072,13 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     *budget -= 1 + kTimed;
     if (ms < best) {
       best = ms;
-      bi = (int)c;
+      bi = c;
     }
   }
   if (bi < 0) return fail(FU_ERR_STATE, "autotune: no candidate ran");
-  for (size_t c = 0; c < cands.size(); ++c)
+  for (int c = 0; c < kNCands; ++c)
     if (h->tune_ms[c] > 1.3f * h->tune_ms[bi]) h->tune_out[c]++;
-  use_cand(h, cands[bi]);
+  use_cand(h, kCands[bi]);
   h->tune_cache[width_class(width)] = bi;
   h->tuned = true;
   h->n_tunes++;
@@ -3900,7 +2094,7 @@ static void poll_pack_width(fu_handle *h) {
   if (!h->autotune || !h->tuned || *h->h_pw == h->tuned_width) return;
   const int cached = h->tune_cache[width_class(*h->h_pw)];
   if (cached >= 0) {  // this width was tuned before (e.g. before fu_reset): reuse its winner
-    use_cand(h, tune_cands(h)[cached]);
+    use_cand(h, kCands[cached]);
     h->tuned_width = *h->h_pw;
   } else if (h->n_tunes < kMaxTunes) {
     h->tuned = false;
@@ -3912,7 +2106,7 @@ static int run_rounds(fu_handle *h, int32_t rounds, int32_t err_every, int nerr)
   for (int32_t r = 0; r < rounds; ++r) {
     poll_pack_width(h);
     // tune between rounds when no error slot is pending in the rounds it would consume
-    if (h->autotune && !h->tuned && h->kernel >= 4 && h->rounds >= 1 && nerr == 0) {
+    if (h->autotune && !h->tuned && h->rounds >= 1 && nerr == 0) {
       int32_t budget = rounds - r;
       const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
       if (int rc = autotune_kernel(h, &budget, w)) return rc;
@@ -4035,23 +2229,13 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   if (!h || (!f_out && h->E)) return fail(FU_ERR_ARG, "fu_get_flows: NULL argument");
   if (h->E == 0) return FU_OK;
   if (int rc = set_device(h)) return rc;
-  const double *src = cur_f(h);
-  if (h->kernel == 3 && h->rounds > 0) {
-    if (!h->ftmp) {
-      if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
-    }
-    hipLaunchKernelGGL(k_push_flows, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E,
-                       h->rev, h->inbox[h->cur], h->ftmp);
-    HIP_TRY(hipGetLastError());
-    src = h->ftmp;
-  } else if (h->kernel >= 4) {  // split words (st_f) -> doubles
-    if (!h->ftmp) {
-      if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
-    }
-    hipLaunchKernelGGL(k_unsplit, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E, src, h->ftmp);
-    HIP_TRY(hipGetLastError());
-    src = h->ftmp;
+  if (!h->ftmp) {
+    if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
   }
+  // split words -> doubles
+  hipLaunchKernelGGL(k_unsplit, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E, cur_f(h), h->ftmp);
+  HIP_TRY(hipGetLastError());
+  const double *src = h->ftmp;
   if (!h->h_new_of_old.empty()) {  // rows back to the caller's order (blocks, same order inside)
     std::vector<double> f2(h->E);
     HIP_TRY(hipMemcpyAsync(f2.data(), src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
@@ -4070,6 +2254,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
 
 int fu_get_info(fu_handle *h, int64_t info[32]) {
   if (!h || !info) return fail(FU_ERR_ARG, "fu_get_info: NULL argument");
+  for (int k = 0; k < 32; ++k) info[k] = 0;
   info[0] = h->kernel;
   info[1] = h->nt;
   info[2] = h->autotune ? (h->tuned ? 2 : 1) : 0;
@@ -4078,22 +2263,11 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   info[5] = kGeoNodes[h->geo];
   info[6] = h->n_tunes;
   info[7] = h->tuned_width;
-  for (int k = 0; k < 12; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
-  {  // autotune winner per packing width 0, 8, 16, 32 (kernel * 10 + geometry; -1 = none)
-    const std::vector<TuneCand> cands = tune_cands(h);
-    for (int k = 0; k < 4; ++k)
-      info[23 + k] = h->tune_cache[k] < 0 ? -1 : cands[h->tune_cache[k]].kernel * 10 + cands[h->tune_cache[k]].geo;
-  }
+  for (int k = 0; k < kNCands; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
   info[20] = h->n_hub;
-  info[21] = h->n_piece;
-  info[22] = 0;
-  if (h->hub_redo) {
-    if (int rc = set_device(h)) return rc;
-    unsigned long long redo = 0;
-    HIP_TRY(hipMemcpyAsync(&redo, h->hub_redo, sizeof(redo), hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
-    info[22] = (int64_t)redo;
-  }
+  for (int k = 0; k < 4; ++k)  // autotune winner per packing width 0, 8, 16, 32 (kernel * 10 + geometry; -1 = none)
+    info[23 + k] = h->tune_cache[k] < 0 ? -1 : kCands[h->tune_cache[k]].kernel * 10 + kCands[h->tune_cache[k]].geo;
+  for (int li = 0; li < 4; ++li) info[27 + li] = h->st[li].P;  // kernel 8 slices per layout (0 = not built)
   return FU_OK;
 }
 
@@ -4124,31 +2298,24 @@ int fu_destroy(fu_handle *h) {
   if (!h) return FU_OK;
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
+  if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->dist) fu__dist_free(h);
-  void *ptrs[] = {h->rowptr, h->col, h->rev, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2],
-                  h->inbox[0], h->inbox[1], h->target, h->err, h->ftmp, h->tiles, h->tiles_geo[0],
-                  h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3], h->wtiles[0], h->wtiles[1],
-                  h->wheavy[0], h->wheavy[1],
-                  h->colpm, h->rowptr0, h->G, h->tiles_s, h->tiles_g, h->perm,
-                  h->code[0], h->code[1], h->pctl, h->psample, h->st_tiles, h->st_gbase, h->st_heavy,
-                  h->stG, h->st[0].aoff, h->st[0].aitem, h->st[0].colS, h->st[0].sidx, h->st[1].aoff,
-                  h->st[1].aitem, h->st[1].colS, h->st[1].sidx, h->st[2].aoff, h->st[2].aitem,
-                  h->st[2].colS, h->st[2].sidx, h->st[3].aoff, h->st[3].aitem, h->st[3].colS,
-                  h->st[3].sidx, h->st[0].gbase, h->st[1].gbase, h->st[2].gbase, h->st[3].gbase,
-                  h->hub_rows, h->hub_off, h->hubxy, h->hrows, h->hub_piece, h->hub_p0, h->psum,
-                  h->hsum, h->hub_redo, h->st[0].sidx16, h->st[1].sidx16, h->st[2].sidx16,
-                  h->st[3].sidx16, h->st[0].dtab, h->st[1].dtab, h->st[2].dtab, h->st[3].dtab};
+  std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
+                              h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
+                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->code[0], h->code[1], h->pctl,
+                              h->psample, h->st_tiles, h->st_heavy, h->stG};
+  for (const auto &L : h->st) {
+    ptrs.push_back(L.brange);
+    ptrs.push_back(L.colS);
+    ptrs.push_back(L.sidx16);
+    ptrs.push_back(L.dtab);
+  }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  if (h->ev0) hipEventDestroy(h->ev0);
-  if (h->ev1) hipEventDestroy(h->ev1);
-  if (h->ev2) hipEventDestroy(h->ev2);
-  if (h->ev3) hipEventDestroy(h->ev3);
-  if (h->ev_pw) hipEventDestroy(h->ev_pw);
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join})
+    if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);
-  if (h->ev_fork) hipEventDestroy(h->ev_fork);
-  if (h->ev_join) hipEventDestroy(h->ev_join);
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
@@ -4460,12 +2627,8 @@ extern "C" {
 void *fu__handle_dist(fu_handle *h) { return h->dist; }
 void fu__handle_set_dist(fu_handle *h, void *d) { h->dist = d; }
 hipStream_t fu__handle_stream(fu_handle *h) { return h->stream; }
-double *fu__handle_f(fu_handle *h, int which) { return h->f[which]; }
-double *fu__handle_a(fu_handle *h, int which) { return h->a[which]; }
-int fu__handle_cur(fu_handle *h) { return h->cur; }
 unsigned long long *fu__handle_err(fu_handle *h) { return h->err; }
 int fu__handle_device(fu_handle *h) { return h->device; }
 double *fu__handle_cur_a(fu_handle *h) { return cur_a(h); }
-double *fu__handle_cur_f(fu_handle *h) { return cur_f(h); }
-int fu__handle_kernel(fu_handle *h) { return h->kernel; }
+
 }

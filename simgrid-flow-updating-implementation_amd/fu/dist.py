@@ -198,26 +198,34 @@ def unique_id() -> bytes:
 class DistCollectAll:
     """One rank of a partitioned collect-all run (RCCL halo exchange every round)."""
 
-    def __init__(self, plan: Plan, values_local, uid: bytes, device: int = 0,
+    def __init__(self, plan: Plan, values_local, uid: bytes | None, device: int = 0,
                  kernel: str = "auto"):
+        """uid = the RCCL unique id shared by all ranks; None = the local test transport
+        (all ranks in this process; rounds driven by run_local)."""
         from .engine import KERNELS
 
         self.plan = plan
         self.values = np.ascontiguousarray(values_local, dtype=np.float64)
         if len(self.values) != plan.n_local:
             raise ValueError("values_local must have n_local entries")
-        keep = [plan.rowptr, plan.col, plan.rev, plan.send_f_off, plan.send_f_idx,
-                plan.recv_f_off, plan.send_a_off, plan.send_a_idx, plan.recv_a_off]
-        self._keep = [None if x is None else np.ascontiguousarray(x) for x in keep]
-        (rp, c, r, sfo, sfi, rfo, sao, sai, rao) = self._keep
-        idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        # estimates-only halo: the round kernels rebuild the neighbours' flows, so the plan's
+        # ghost-flow part (rev, send_f_*, recv_f_off) is not sent to the device
+        zf = np.zeros(plan.nranks + 1, dtype=np.int64)
+        keep = [plan.rowptr, plan.col, zf, plan.send_a_off, plan.send_a_idx, plan.recv_a_off]
+        self._keep = [np.ascontiguousarray(x) for x in keep]
+        (rp, c, zf, sao, sai, rao) = self._keep
         out = L.vp()
-        L.call("fu_dist_create", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c),
-               None if r is None else L.ptr(r),
-               L.ptr(self.values), plan.n_ghost_a, plan.n_ghost_f, plan.nranks, plan.rank,
-               L.ptr(sfo), L.ptr(sfi) if len(sfi) else None, L.ptr(rfo), L.ptr(sao),
-               L.ptr(sai) if len(sai) else None, L.ptr(rao), idbuf, int(device),
-               ctypes.byref(out))
+        if uid is None:  # local test transport (exchange_local), no communicator
+            L.call("fu_dist_create_local", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c),
+                   L.ptr(self.values), plan.n_ghost_a, plan.nranks, plan.rank, L.ptr(sao),
+                   L.ptr(sai) if len(sai) else None, L.ptr(rao), int(device), ctypes.byref(out))
+        else:
+            idbuf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+            L.call("fu_dist_create", plan.n_local, plan.e_local, L.ptr(rp), L.ptr(c), None,
+                   L.ptr(self.values), plan.n_ghost_a, 0, plan.nranks, plan.rank,
+                   L.ptr(zf), None, L.ptr(zf), L.ptr(sao),
+                   L.ptr(sai) if len(sai) else None, L.ptr(rao), idbuf, int(device),
+                   ctypes.byref(out))
         self._h = out
         self.n = plan.n_local
         self.E = plan.e_local
@@ -282,3 +290,13 @@ class DistCollectAll:
 
     def __del__(self):
         self.close()
+
+
+def run_local(engines, rounds: int):
+    """Local test transport: `rounds` rounds of every rank (DistCollectAll(..., uid=None)),
+    one round at a time, each followed by fu_dist_exchange_local."""
+    arr = (ctypes.c_void_p * len(engines))(*[e._h.value for e in engines])
+    for _ in range(rounds):
+        for e in engines:
+            L.call("fu_run_collectall", e._h, 1, 0, None)
+        L.call("fu_dist_exchange_local", arr, len(engines))

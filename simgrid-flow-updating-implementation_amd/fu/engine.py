@@ -16,8 +16,7 @@ import numpy as np
 from . import _lib as L
 from .graph import Graph
 
-KERNELS = {"auto": 0, "thread": 1, "tile": 2, "push": 3, "recon": 4, "split": 5, "split2": 6, "wave": 7, "stage": 8, "pipe": 9,
-           "pipe_stage": 10}
+KERNELS = {"auto": 0, "recon": 4, "stage": 8}
 LAYOUTS = {"given": 0, "degree": 1}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
@@ -26,24 +25,27 @@ def handle_info(h) -> dict:
     """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
     a = np.zeros(32, dtype=np.int64)
     L.call("fu_get_info", h, L.ptr(a))
-    names = {1: "thread", 2: "tile", 3: "push", 4: "recon", 5: "split", 6: "split2", 7: "wave", 8: "stage", 9: "pipe",
-             10: "pipe_stage"}
+    names = {4: "recon", 8: "stage"}
     return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
             "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
             "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
-            "tuned_pack_width": int(a[7]),
-            "mega_hubs": int(a[20]), "hub_pieces": int(a[21]), "hub_pieces_redone": int(a[22]),
+            "tuned_pack_width": int(a[7]), "mega_hubs": int(a[20]),
+            "stage_slices": [int(x) for x in a[27:31]],
             "tune_winner_by_width": {w: _cand_name(int(a[23 + k])) for k, w in
                                      enumerate((0, 8, 16, 32)) if a[23 + k] >= 0},
             "tune_us_per_round": {k: a[8 + i] / 1e3 for i, k in
-                                  enumerate(("recon", "recon_512", "split2", "stage",
-                                             "pipe_stage", "recon_1024"))}}
+                                  enumerate(TUNE_CANDIDATES)}}
+
+
+# fu_engine.hip kCands order
+TUNE_CANDIDATES = ("recon", "recon_512", "stage", "recon_1024")
 
 
 def _cand_name(code: int) -> str:
     kernel, geo = divmod(code, 10)
-    names = {4: "recon", 6: "split2", 8: "stage", 10: "pipe_stage"}
-    return names.get(kernel, str(kernel)) + ({3: "_512", 1: "_1024"}.get(geo, "") if kernel == 4 else "")
+    if kernel == 8:
+        return "stage"
+    return "recon" + {3: "_512", 1: "_1024", 2: "_1024x256"}.get(geo, "")
 
 
 class CollectAll:

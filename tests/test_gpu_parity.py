@@ -15,20 +15,14 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = ["thread", "tile", "push", "recon", "split", "split2", "wave", "stage", "pipe", "pipe_stage"]
-
-
-def _rows_sorted(rowptr, col):
-    return all(np.all(np.diff(col[rowptr[i]:rowptr[i + 1]]) > 0) for i in range(len(rowptr) - 1))
+# kernel 4 (recon: LDS tiles with flow reconstruction) and kernel 8 (stage: LDS-staged
+# slices + recon tiles); "auto" switches between them and kernel 4's tile geometries mid-run
+KERNELS = ["recon", "stage"]
 
 
 def _check_fixture(meta, kernel, hub_threshold=None):
     d = load_npz(meta["file"])
     rounds = [int(r) for r in d["rounds"]]
-    if kernel in ("split", "split2") and not _rows_sorted(d["rowptr"], d["col"]):
-        with pytest.raises(fu.FuError, match="sorted"):
-            fu.CollectAll(rowptr=d["rowptr"], col=d["col"], values=d["values"], kernel=kernel)
-        return
     eng = fu.CollectAll(rowptr=d["rowptr"], col=d["col"], values=d["values"], kernel=kernel,
                         hub_threshold=hub_threshold)
     done = 0
@@ -46,8 +40,7 @@ def test_ca_sync_fixture_bitwise(name, meta, kernel):
     _check_fixture(meta, kernel)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave", "stage", "pipe",
-                                    "pipe_stage"])
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("name", ["rmat9_ef8", "star_257", "star_1500", "er300_m450"])
 def test_ca_sync_fixture_heavy_path(name, kernel):
     """hub_threshold=3 sends most nodes down the heavy (block-per-node) path."""
@@ -55,7 +48,7 @@ def test_ca_sync_fixture_heavy_path(name, kernel):
     _check_fixture(meta, kernel, hub_threshold=3)
 
 
-@pytest.mark.parametrize("kernel", KERNELS)
+@pytest.mark.parametrize("kernel", KERNELS + ["auto"])
 def test_er_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.erdos_renyi(200_000, 800_000, seed=5)
     v = fu.uniform_values(g.n, seed=1)
@@ -66,8 +59,7 @@ def test_er_vs_c_oracle_bitwise(kernel):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["tile", "push", "recon", "split", "split2", "wave", "stage", "pipe",
-                                    "pipe_stage"])
+@pytest.mark.parametrize("kernel", KERNELS)
 def test_rmat_hubs_vs_c_oracle_bitwise(kernel):
     g = fu.Graph.rmat(15, 16, seed=2)
     assert g.max_deg > 2048  # exercises chunked heavy tiles
@@ -123,17 +115,19 @@ def test_isolated_and_empty():
 def test_option_errors():
     g = fu.Graph.random_regular(64, 4, seed=1)
     eng = fu.CollectAll(g, np.ones(g.n))
-    with pytest.raises(fu.FuError):
-        eng.set_option("kernel", 11)
-    with pytest.raises(fu.FuError):
-        eng.set_option("nope", 1)
+    for k in (1, 2, 3, 5, 6, 7, 9, 10, 11):  # removed variants / out of range
+        with pytest.raises(fu.FuError, match="kernel must be"):
+            eng.set_option("kernel", k)
+    for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag"):
+        with pytest.raises(fu.FuError):
+            eng.set_option(key, 1)
     with pytest.raises(fu.FuError):
         eng.run(5, err_every=1)  # no targets
     eng.run(2)
     with pytest.raises(fu.FuError):
-        eng.set_option("kernel", 1)  # after rounds ran
+        eng.set_option("kernel", 8)  # after rounds ran
     eng.reset()
-    eng.set_option("kernel", 1)
+    eng.set_option("kernel", 8)
     eng.run(1)
 
 
@@ -220,17 +214,16 @@ def test_full_size_er1m_convergence_and_prefix_parity():
     assert np.all(np.diff(tr[5:]) <= 0) or tr[-1] < 1e-12  # settles monotonically
 
 
-@pytest.mark.parametrize("kernel", ["recon", "tile"])
-def test_dist_single_rank_rccl_matches_engine(kernel):
+def test_dist_single_rank_rccl_matches_engine():
     """fu_dist_create + RCCL communicator at world size 1 (the only size one GPU box can
-    run): no ghosts, the per-round halo hook runs with empty send lists. The multi-rank
-    plan is covered on the CPU (tests/test_dist_gloo.py)."""
+    run): no ghosts, the per-round halo hook runs with empty send lists. Ghost slots are
+    exercised by the local-transport tests below."""
     from fu.dist import DistCollectAll, partition, unique_id
 
     g = fu.Graph.random_geometric(50_000, avg_deg=8, seed=3)
     v = fu.uniform_values(g.n, seed=1)
     plan = partition(g.rowptr, g.col, g.rev, 1, 0)
-    d = DistCollectAll(plan, v, unique_id(), kernel=kernel)
+    d = DistCollectAll(plan, v, unique_id(), kernel="recon")
     d.run(30)
     eng = fu.CollectAll(g, v)
     eng.run(30)
@@ -240,7 +233,57 @@ def test_dist_single_rank_rccl_matches_engine(kernel):
     d.set_targets(tgt)
     tr = d.run(10, err_every=5)
     assert len(tr) == 2 and np.isfinite(tr).all()
+    with pytest.raises(fu.FuError, match="multi-GPU supports kernel 4"):
+        DistCollectAll(plan, v, unique_id(), kernel="stage")
     d.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["rgg", "er"])
+def test_dist_ghost_slots_local_transport_bitwise(world, kind):
+    """Every rank of a partitioned graph as its own handle on GPU 0, the halo moved by the
+    test transport (device copies in RCCL's slot order): the round kernels read ghost slots
+    (col >= n_local), k_pack packs non-empty send lists. Gathered estimates and flows equal
+    the C oracle bitwise. ER cuts most edges (every rank talks to every rank)."""
+    from fu.dist import DistCollectAll, partition, run_local
+
+    if kind == "rgg":
+        g = fu.Graph.random_geometric(200_000, avg_deg=8, seed=21)
+    else:
+        g = fu.Graph.erdos_renyi(60_000, 240_000, seed=21)
+    v = fu.uniform_values(g.n, seed=21)
+    plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
+    assert all(p.n_ghost_a > 0 and len(p.send_a_idx) > 0 for p in plans)
+    engs = [DistCollectAll(p, v[p.lo:p.hi], None) for p in plans]
+    rounds = 25
+    run_local(engs, rounds)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
+    for p, e in zip(plans, engs):
+        assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), p.rank
+        assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), p.rank
+    for e in engs:
+        e.close()
+
+
+def test_dist_rgg_slabs_local_transport_bitwise():
+    """The native slab generator's halo plans (fu_part_gen_rgg, 3 parts) on the local
+    transport equal the single-GPU engine on the global graph."""
+    from fu.dist import DistCollectAll, RggPart, run_local
+
+    n, world = 300_000, 3
+    parts = [RggPart(n, avg_deg=8.0, seed=7, nparts=world, part=r) for r in range(world)]
+    engs = [DistCollectAll(p.to_plan(), p.values(seed=3), None) for p in parts]
+    run_local(engs, 20)
+    g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=7)
+    v = fu.uniform_values(g.n, seed=3)
+    eng = fu.CollectAll(g, v)
+    eng.run(20)
+    a, f = eng.estimates(), eng.flows()
+    for p, e in zip(parts, engs):
+        assert np.array_equal(e.estimates(), a[p.lo:p.hi])
+        assert np.array_equal(e.flows(), f[g.rowptr[p.lo]:g.rowptr[p.hi]])
+    for e in engs:
+        e.close()
 
 
 @pytest.mark.parametrize("persistent", [False, True])
@@ -262,16 +305,14 @@ def test_replay_with_faults_vs_c_oracle(persistent):
 
 
 def test_dist_rgg_slab_estimates_only_halo_matches_engine():
-    """The native slab generator + estimates-only halo (rev = NULL) at world size 1 equals
-    the single-GPU engine on the global graph, bitwise; kernels that need rev are refused."""
+    """The native slab generator + estimates-only halo at world size 1 (RCCL) equals the
+    single-GPU engine on the global graph, bitwise."""
     from fu.dist import DistCollectAll, RggPart, unique_id
 
     n = 200_000
     part = RggPart(n, avg_deg=8.0, seed=5, nparts=1, part=0)
     v = part.values(seed=2)
     d = DistCollectAll(part.to_plan(), v, unique_id())
-    with pytest.raises(fu.FuError, match="reverse-edge"):
-        d2 = DistCollectAll(part.to_plan(), v, unique_id(), kernel="tile")
     d.run(40)
     g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=5)
     eng = fu.CollectAll(g, v)
@@ -281,7 +322,7 @@ def test_dist_rgg_slab_estimates_only_halo_matches_engine():
 
 
 def test_autotune_switches_kernels_bitwise():
-    """kernel="auto" times kernel 4 (three tile geometries, +nt), 6 and 5 on real rounds and
+    """kernel="auto" times kernel 4 (three tile geometries) and kernel 8 on real rounds and
     keeps the fastest; the switch happens mid-run and must not change a single bit."""
     g = fu.Graph.erdos_renyi(300_000, 1_200_000, seed=8)
     v = fu.uniform_values(g.n, seed=8)
@@ -337,10 +378,8 @@ def _er_with_outlier_pairs(n, m, pairs, seed):
     return fu.Graph.from_edges(n + 2 * pairs, s, d), v
 
 
-@pytest.mark.parametrize("kind,kernel", [("er", "recon"), ("rmat", "recon"), ("rmat_bins", "recon"),
-                                         ("er", "wave"), ("rmat", "wave"), ("er", "stage"),
-                                         ("rmat", "stage"), ("er", "pipe"), ("rmat", "pipe"),
-                                         ("er", "pipe_stage"), ("rmat", "pipe_stage")])
+@pytest.mark.parametrize("kind,kernel", [("er", "recon"), ("rmat", "recon"), ("er", "stage"),
+                                         ("rmat", "stage")])
 def test_packed_gather_long_run_bitwise(kind, kernel):
     """The packed estimate table (8/16/32-bit lossless codes + escapes) switches on as the
     estimates converge; 300 rounds must still equal the C oracle bit for bit, and equal the
@@ -353,8 +392,6 @@ def test_packed_gather_long_run_bitwise(kind, kernel):
     rounds = 300
     eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=16)
     eng.set_option("pack_every", 4)
-    if kind == "rmat_bins":
-        eng.set_option("bins", 1)
     seen = set()
     for _ in range(rounds // 25):
         eng.run(25)
@@ -371,13 +408,12 @@ def test_packed_gather_long_run_bitwise(kind, kernel):
 
 
 def test_packed_gather_with_kernel_switches():
-    """Kernel 6 rounds mark their estimate table unpacked (width 0), so a kernel-4 round after
-    them gathers the doubles. recon, split2 and auto (which switches kernels mid-run) give
-    the same bits over a run long enough for packing to engage."""
+    """recon, stage and auto (which switches kernels and geometries mid-run, re-tuning at each
+    packing width) give the same bits over a run long enough for packing to engage."""
     g = fu.Graph.erdos_renyi(50_000, 200_000, seed=9)
     v = fu.uniform_values(g.n, seed=9)
     ref = None
-    for kernel in ("recon", "split2", "wave", "stage", "pipe", "pipe_stage", "auto"):
+    for kernel in ("recon", "stage", "auto"):
         eng = fu.CollectAll(g, v, kernel=kernel)
         eng.set_option("pack_every", 2)
         eng.run(260)
@@ -387,15 +423,14 @@ def test_packed_gather_with_kernel_switches():
         assert np.array_equal(got[0], ref[0]) and np.array_equal(got[1], ref[1]), kernel
 
 
-@pytest.mark.parametrize("kernel,opts", [("recon", {"tile_edges": 1024}),
+@pytest.mark.parametrize("kernel,opts", [("recon", {"tile_edges": 2048}),
+                                         ("recon", {"tile_edges": 1024}),
                                          ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
-                                         ("recon", {"tile_edges": 512}),
-                                         ("wave", {"wave_edges": 256}),
-                                         ("wave", {"wave_edges": 512})])
+                                         ("recon", {"tile_edges": 512})])
 @pytest.mark.parametrize("kind", ["er", "rmat"])
 def test_tile_geometries_bitwise(kernel, opts, kind):
-    """Every kernel 4 / kernel 7 tile geometry the autotuner may pick, incl. the heavy-row
-    launch of kernel 7 (hub_threshold 16 on R-MAT), against the C oracle."""
+    """Every kernel 4 tile geometry the autotuner may pick, with heavy rows (hub_threshold 16
+    on R-MAT), against the C oracle."""
     if kind == "er":
         g = fu.Graph.erdos_renyi(200_000, 800_000, seed=6)
     else:
@@ -410,16 +445,15 @@ def test_tile_geometries_bitwise(kernel, opts, kind):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("kernel", ["stage", "pipe_stage"])
 @pytest.mark.parametrize("layout", [0, 1, 2, 3])
-def test_stage_forced_layouts_bitwise(layout, kernel):
+def test_stage_forced_layouts_bitwise(layout):
     """Kernel 8 with each slice layout forced (1/2/4/8-byte elements) over a run in which the
     table goes from doubles to 32/16/8-bit codes: a table wider than the layout is gathered
     from global memory by the stage launch, a narrower one sits in LDS; escapes (far-off
     2-node components) read the double through the edge's column. Heavy rows (R-MAT part)
     run as kernel 4 heavy tiles."""
     g, v = _er_with_outlier_pairs(60_000, 240_000, 32, seed=11)
-    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=16)
+    eng = fu.CollectAll(g, v, kernel="stage", hub_threshold=16)
     eng.set_option("stage_layout", layout)
     eng.set_option("pack_every", 4)
     seen = set()
@@ -430,21 +464,6 @@ def test_stage_forced_layouts_bitwise(layout, kernel):
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     assert seen & {8, 16, 32}, seen
-
-
-@pytest.mark.parametrize("bpc", [1, 3, 8])
-@pytest.mark.parametrize("kernel", ["pipe", "pipe_stage"])
-def test_pipe_grid_sizes_bitwise(kernel, bpc):
-    """Kernels 9/10 with few persistent blocks (long tile lists per block, up to the 64-tile
-    chunk) and many, on R-MAT (hub blocks at the front of the grid) against the C oracle."""
-    g = fu.Graph.rmat(15, 16, seed=7)
-    v = fu.uniform_values(g.n, seed=7)
-    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=32)
-    eng.set_option("pipe_bpc", bpc)
-    eng.run(20)
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
-    assert np.array_equal(eng.estimates(), a_ref)
-    assert np.array_equal(eng.flows(), f_ref)
 
 
 @pytest.mark.parametrize("tile", [2048, 1024, 512])
@@ -499,3 +518,105 @@ def test_heavy_rows_wave_and_block_paths_bitwise(tile, wave_heavy):
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 80, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+def test_round0_flows_sparse_rows_and_hubs():
+    """Round 0's per-block row search: long runs of isolated nodes between edges (a block's
+    rows span more than its LDS window) and a hub whose edges fill whole blocks."""
+    n = 300_000
+    rng = np.random.default_rng(3)
+    hub = 5
+    leaves = rng.choice(np.arange(10, n), size=5000, replace=False)
+    s = np.concatenate([np.full(len(leaves), hub), rng.integers(0, n, 3000)])
+    d = np.concatenate([leaves, rng.integers(0, n, 3000)])
+    g = fu.Graph.from_edges(n, s, d)
+    v = fu.uniform_values(g.n, seed=4)
+    for kernel in KERNELS:
+        eng = fu.CollectAll(g, v, kernel=kernel)
+        for r in (1, 2, 3):
+            eng.run(1)
+            a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, r)
+            assert np.array_equal(eng.estimates(), a_ref), (kernel, r)
+            assert np.array_equal(eng.flows(), f_ref), (kernel, r)
+
+
+def test_stage_layout_slices_and_unbuildable_graphs():
+    """Kernel 8's layouts: ER-1M builds all four (1-byte codes: 16 slices of 64K nodes, the
+    u16 offset limit; doubles: 62 slices of 16K), each tile within the 64 runs the u16
+    index addresses."""
+    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
+    eng = fu.CollectAll(g, fu.uniform_values(g.n, seed=0), kernel="stage")
+    assert eng.info()["stage_slices"] == [16, 16, 31, 62]
+    eng.close()
+
+
+def _check_flow_bookkeeping(g, v, a, f):
+    """Each node's estimate after its average equals its value minus its outgoing flows
+    (CA:107 with CA:117: Σ_j f_new = Σ fr + d·a - Σ er = v - a), so Σ a + Σ f = Σ v: the
+    mass in flight is the flow sum. Both hold to rounding."""
+    idx = np.minimum(g.rowptr[:-1], g.E - 1)  # reduceat needs indices < len; empty rows -> 0
+    empty = np.diff(g.rowptr) == 0
+    out = np.add.reduceat(f, idx)
+    out[empty] = 0.0
+    absout = np.add.reduceat(np.abs(f), idx)
+    absout[empty] = 0.0
+    scale = np.abs(v) + absout + 1.0
+    assert np.max(np.abs(a - (v - out)) / scale) < 1e-12
+    tot = np.sum(np.abs(v)) + np.sum(np.abs(f))
+    assert abs(np.sum(a) + np.sum(f) - np.sum(v)) / tot < 1e-12
+
+
+@pytest.mark.timeout(900)
+def test_rmat24_degree_layout_bitwise():
+    """BASELINE config 4 at full size: R-MAT scale 24 (edge factor 16; E = 5.2e8, max degree
+    406,598: mega hubs, heavy rows) with the degree layout and the autotuned kernel on one
+    MI355X. 10 rounds bitwise against the C oracle (16 threads), and the flow bookkeeping."""
+    g = fu.Graph.rmat(24, 16, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    eng = fu.CollectAll(g, v, layout="degree")
+    eng.run(10)
+    a, f = eng.estimates(), eng.flows()
+    eng.close()
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 10, nthreads=16)
+    assert np.array_equal(a, a_ref)
+    assert np.array_equal(f, f_ref)
+    del a_ref, f_ref
+    _check_flow_bookkeeping(g, v, a, f)
+
+
+def test_rgg_2pow23_partition_unit_bitwise():
+    """BASELINE config 5's weak-scaling unit: RggPart(2^23) at world size 1 (native slab
+    generator, RCCL communicator), 5 rounds bitwise against the C oracle on the same graph."""
+    from fu.dist import DistCollectAll, RggPart, unique_id
+
+    n = 1 << 23
+    part = RggPart(n, avg_deg=8.0, seed=1, nparts=1, part=0)
+    v = part.values(seed=0)
+    d = DistCollectAll(part.to_plan(), v, unique_id())
+    d.run(5)
+    g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 5, nthreads=16)
+    assert np.array_equal(d.estimates(), a_ref)
+    assert np.array_equal(d.flows(), f_ref)
+    d.close()
+
+
+@pytest.mark.timeout(900)
+def test_rgg64m_single_gpu_properties():
+    """BASELINE config 5's graph at full size on one GPU (2^26 nodes, E = 5.4e8): 10 rounds,
+    finite estimates, the flow bookkeeping (Σ a + Σ f = Σ v: mass conserved counting the flows
+    in flight), and the mean of the values recovered to 1e-9 by the math.fsum means."""
+    import math
+
+    n = 1 << 26
+    g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    eng = fu.CollectAll(g, v)
+    eng.run(10)
+    a, f = eng.estimates(), eng.flows()
+    eng.close()
+    assert np.isfinite(a).all() and np.isfinite(f).all()
+    _check_flow_bookkeeping(g, v, a, f)
+    mean_v = math.fsum(v.tolist()) / n
+    mass = (math.fsum(a.tolist()) + float(np.sum(f))) / n
+    assert abs(mass - mean_v) < 1e-9 * mean_v

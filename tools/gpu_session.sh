@@ -19,7 +19,7 @@ step() {  # name limit cmd...
 }
 for s in $STEPS; do
   case $s in
-    pytest) step pytest 1100 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} ;;
+    pytest) step pytest 1100 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   export TMPDIR=/tmp

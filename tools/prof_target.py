@@ -33,9 +33,12 @@ if a.tile:
 for kv in a.opt:
     k, _, val = kv.partition("=")
     eng.set_option(k, int(val))
+if a.kernel == "auto":
+    eng.tune()  # as bench.py: one untimed autotune pass
 eng.run(a.warm)
 eng.reset()
-eng.set_option("diag", a.diag)
+if a.diag:
+    eng.set_option("diag", a.diag)  # needs FU_LIBRARY=.../libfu_diag.so
 eng.run(a.rounds)
 eng.synchronize()
 print("n", g.n, "E", g.E, "alg_bytes", 24 * g.E + 28 * g.n, "info", eng.info(), "pack", eng.pack_widths())

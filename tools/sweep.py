@@ -14,95 +14,31 @@ sys.path.insert(0, os.path.join(ROOT, "simgrid-flow-updating-implementation_amd"
 import fu  # noqa: E402
 
 VARIANTS = {
-    "thread": ("thread", {}),
-    "tile": ("tile", {}),
-    "push": ("push", {}),
-    "recon": ("recon", {}),
-    "recon_nt": ("recon", {"nt": 1}),
-    "recon_nopack": ("recon", {"pack": 0}),
-    "recon_nt_nopack": ("recon", {"nt": 1, "pack": 0}),
-    "split": ("split", {}),
-    "split2": ("split2", {}),
-    "wave256": ("wave", {"wave_edges": 256}),
-    "wave512": ("wave", {"wave_edges": 512}),
-    "recon_nobins": ("recon", {"bins": 0}),
+    "recon": ("recon", {"tile_edges": 2048}),
     "recon_1024": ("recon", {"tile_edges": 1024}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
-    "recon_1024_nt": ("recon", {"tile_edges": 1024, "nt": 1}),
     "recon_512": ("recon", {"tile_edges": 512}),
-    "diag1_gather_free": ("recon", {"diag": 1}),
-    "diag2_flow_free": ("recon", {"diag": 2}),
-    "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
-    "diag1_512": ("recon", {"tile_edges": 512, "diag": 1}),
-    "diag2_512": ("recon", {"tile_edges": 512, "diag": 2}),
-    "diag12_512": ("recon", {"tile_edges": 512, "diag": 12}),
-    "diag3_half_table": ("recon", {"diag": 3}),
-    "diag4_quarter_table": ("recon", {"diag": 4}),
-    "diag5_no_hub_chain": ("recon", {"diag": 5}),
-    "recon_hub256": ("recon", {"hub_threshold": 256}),
-    "recon_hub2048": ("recon", {"hub_threshold": 2048}),
+    "recon_nt": ("recon", {"nt": 1}),
+    "recon_nopack": ("recon", {"pack": 0}),
+    "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
+    "recon_nofork": ("recon", {"fork_heavy": 0}),
+    "recon_blockheavy": ("recon", {"wave_heavy": 0}),
+    "recon_deg": ("recon", {"layout": "degree"}),
+    "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
-    "diag1_stage": ("stage", {"diag": 1}),
-    "diag2_stage": ("stage", {"diag": 2}),
+    "stage_pe64": ("stage", {"pack_every": 64}),
+    # timing-only ablations (WRONG results): need the -DFU_DIAG library (make DIAG=1,
+    # FU_LIBRARY=.../libfu_diag.so)
+    "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
+    "diag2_1024": ("recon", {"tile_edges": 1024, "diag": 2}),
+    "diag12_1024": ("recon", {"tile_edges": 1024, "diag": 12}),
+    "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
+    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
     "diag1_stage_nopack": ("stage", {"pack": 0, "diag": 1}),
     "diag2_stage_nopack": ("stage", {"pack": 0, "diag": 2}),
-    "diag3_stage": ("stage", {"diag": 3}),
-    "pipe": ("pipe", {}),
-    "recon_512_blockheavy": ("recon", {"tile_edges": 512, "wave_heavy": 0}),
-    "recon_blockheavy": ("recon", {"wave_heavy": 0}),
-    "diag4_stage": ("stage", {"diag": 4}),
     "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
-    "pipe_nopack": ("pipe", {"pack": 0}),
-    "stage_pe64": ("stage", {"pack_every": 64}),
-    "recon_nofork": ("recon", {"fork_heavy": 0}),
-    "recon_deg_mega1024": ("recon", {"mega_hub": 1024, "layout": "degree"}),
-    "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
-    "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
-    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
-    "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
-    "stage_u32": ("stage", {"stage_compact": 0}),
-    "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
-    "pipe_stage_b2": ("pipe_stage", {"pipe_bpc": 2}),
-    "pipe_stage_b3": ("pipe_stage", {"pipe_bpc": 3}),
-    "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
-    "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
-    "pipe_stage": ("pipe_stage", {}),
-    "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
-    "pipe_b2": ("pipe", {"pipe_bpc": 2}),
-    "pipe_b4": ("pipe", {"pipe_bpc": 4}),
-    "pipe_b8": ("pipe", {"pipe_bpc": 8}),
-    "pipe_stage_b4": ("pipe_stage", {"pipe_bpc": 4}),
-    "pipe_stage_b8": ("pipe_stage", {"pipe_bpc": 8}),
-    "diag3_stage_nopack": ("stage", {"pack": 0, "diag": 3}),
-    "diag1_512_nopack": ("recon", {"tile_edges": 512, "pack": 0, "diag": 1}),
-    "recon_512_nopack": ("recon", {"tile_edges": 512, "pack": 0}),
-    "recon_deg": ("recon", {"layout": "degree"}),
-    "recon_512_deg": ("recon", {"tile_edges": 512, "layout": "degree"}),
-    "stage_deg": ("stage", {"layout": "degree"}),
-    "auto_deg": ("auto", {"layout": "degree"}),
-    "auto": ("auto", {}),
-    "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
-    "recon_noscan": ("recon", {"hub_scan": 0}),
-    "pipe_stage_nopack": ("pipe_stage", {"pack": 0}),
-    "pipe_nopack": ("pipe", {"pack": 0}),
-    "stage_pe64": ("stage", {"pack_every": 64}),
-    "recon_nofork": ("recon", {"fork_heavy": 0}),
-    "recon_deg_mega1024": ("recon", {"mega_hub": 1024, "layout": "degree"}),
-    "recon_deg_mega512": ("recon", {"mega_hub": 512, "layout": "degree"}),
-    "recon_deg_mega256": ("recon", {"mega_hub": 256, "layout": "degree"}),
-    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
-    "recon_deg_nt": ("recon", {"nt": 1, "layout": "degree"}),
-    "stage_u32": ("stage", {"stage_compact": 0}),
-    "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
-    "pipe_stage_b2": ("pipe_stage", {"pipe_bpc": 2}),
-    "pipe_stage_b3": ("pipe_stage", {"pipe_bpc": 3}),
-    "recon_deg_1024": ("recon", {"tile_edges": 1024, "layout": "degree"}),
-    "recon_deg_512": ("recon", {"tile_edges": 512, "layout": "degree"}),
-    "recon_mega4096": ("recon", {"mega_hub": 4096}),
-    "recon_mega2048": ("recon", {"mega_hub": 2048}),
-    "recon_mega1024": ("recon", {"mega_hub": 1024}),
-    "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
+    "diag4_stage": ("stage", {"diag": 4}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -140,7 +76,7 @@ for spec in specs:
         out[k] = {"us_per_round_med": med, "us_min": min(ts),
                   "alg_GBs": alg / (med * 1e-6) / 1e9, "edge_updates_per_s": g.E / (med * 1e-6),
                   "pack": engs[k].pack_widths(),
-                  "hub": [engs[k].info()[x] for x in ("mega_hubs", "hub_pieces", "hub_pieces_redone")]}
+                  "info": {k2: engs[k].info()[k2] for k2 in ("kernel", "tile", "mega_hubs")}}
     print(json.dumps(out), flush=True)
     for e in engs.values():
         e.close()
