@@ -40,6 +40,12 @@ struct DistState {
   int *send_a_idx = nullptr;
   double *sbuf_a = nullptr;
   int64_t n_send_a = 0;
+  // every RCCL call goes on comm_stream (one stream per communicator): the halo of round r
+  // runs there beside round r's interior tiles, behind ev_bnd (boundary tiles done); the
+  // next round waits for ev_halo
+  hipStream_t comm_stream = nullptr;
+  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
+  bool halo_pending = false;
 };
 
 __global__ void k_pack(long long cnt, const int *__restrict__ idx, const double *__restrict__ src,
@@ -57,6 +63,7 @@ extern "C" hipStream_t fu__handle_stream(fu_handle *h);
 extern "C" unsigned long long *fu__handle_err(fu_handle *h);
 extern "C" int fu__handle_device(fu_handle *h);
 extern "C" double *fu__handle_cur_a(fu_handle *h);
+extern "C" double *fu__handle_halo_a(fu_handle *h);
 
 #define NCCL_TRY(expr)                                                                     \
   do {                                                                                     \
@@ -76,22 +83,46 @@ int fu_dist_unique_id(uint8_t *id_out) {
   return FU_OK;
 }
 
-// phase 0: before a round (nothing); phase 1: after a round -> halo exchange of the new
-// state; phase 100 + k: all-reduce max of k error slots.
+#define HIPD_TRY(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess) return fu::fail(FU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// phase 0: before a round (or a host sync / reset): the main stream waits for the last halo.
+// phase 2: mid-round, once the boundary tiles (and heavy rows) of round r are queued: pack
+//   a_r[send_a_idx] and exchange with every neighbouring part on comm_stream, concurrently with
+//   round r's interior tiles (they never read ghost slots; the receives write only ghost
+//   slots [n_local, na) of the buffer, the interior tiles only own slots). Local transport:
+//   pack only, on the main stream (fu_dist_exchange_local moves the bytes).
+// phase 100 + k: all-reduce max of k error slots (on comm_stream, joined back).
 int fu__dist_round_hook(fu_handle *h, int phase) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   hipStream_t s = fu__handle_stream(h);
-  if (phase == 0) return FU_OK;
+  if (phase == 0) {
+    if (d->halo_pending) HIPD_TRY(hipStreamWaitEvent(s, d->ev_halo, 0));
+    d->halo_pending = false;
+    return FU_OK;
+  }
   if (phase >= 100) {
     if (!d->comm) return FU_OK;  // local transport: the caller combines the per-rank maxima
     const int k = phase - 100;
     unsigned long long *err = fu__handle_err(h);
-    NCCL_TRY(ncclAllReduce(err, err, (size_t)k, ncclUint64, ncclMax, d->comm, s));
+    HIPD_TRY(hipEventRecord(d->ev_bnd, s));
+    HIPD_TRY(hipStreamWaitEvent(d->comm_stream, d->ev_bnd, 0));
+    NCCL_TRY(ncclAllReduce(err, err, (size_t)k, ncclUint64, ncclMax, d->comm, d->comm_stream));
+    HIPD_TRY(hipEventRecord(d->ev_halo, d->comm_stream));
+    HIPD_TRY(hipStreamWaitEvent(s, d->ev_halo, 0));
     return FU_OK;
   }
-  double *a = fu__handle_cur_a(h);
+  double *a = fu__handle_halo_a(h);
+  hipStream_t cs = d->comm ? d->comm_stream : s;
+  if (d->comm) {
+    HIPD_TRY(hipEventRecord(d->ev_bnd, s));
+    HIPD_TRY(hipStreamWaitEvent(cs, d->ev_bnd, 0));
+  }
   if (d->n_send_a > 0) {
-    hipLaunchKernelGGL(k_pack, dim3((unsigned)((d->n_send_a + 255) / 256)), dim3(256), 0, s,
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)((d->n_send_a + 255) / 256)), dim3(256), 0, cs,
                        (long long)d->n_send_a, d->send_a_idx, a, d->sbuf_a);
   }
   hipError_t he = hipGetLastError();
@@ -102,17 +133,23 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
     if (p == d->rank) continue;
     const int64_t sa = d->send_a_off[p + 1] - d->send_a_off[p];
     const int64_t ra = d->recv_a_off[p + 1] - d->recv_a_off[p];
-    if (sa) NCCL_TRY(ncclSend(d->sbuf_a + d->send_a_off[p], (size_t)sa, ncclDouble, p, d->comm, s));
-    if (ra) NCCL_TRY(ncclRecv(a + d->n_local + d->recv_a_off[p], (size_t)ra, ncclDouble, p, d->comm, s));
+    if (sa) NCCL_TRY(ncclSend(d->sbuf_a + d->send_a_off[p], (size_t)sa, ncclDouble, p, d->comm, cs));
+    if (ra) NCCL_TRY(ncclRecv(a + d->n_local + d->recv_a_off[p], (size_t)ra, ncclDouble, p, d->comm, cs));
   }
   NCCL_TRY(ncclGroupEnd());
+  HIPD_TRY(hipEventRecord(d->ev_halo, cs));
+  d->halo_pending = true;
   return FU_OK;
 }
 
 void fu__dist_free(fu_handle *h) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   if (!d) return;
+  if (d->comm_stream) hipStreamSynchronize(d->comm_stream);
   if (d->comm) ncclCommDestroy(d->comm);
+  if (d->ev_bnd) hipEventDestroy(d->ev_bnd);
+  if (d->ev_halo) hipEventDestroy(d->ev_halo);
+  if (d->comm_stream) hipStreamDestroy(d->comm_stream);
   void *ptrs[] = {d->send_a_idx, d->sbuf_a};
   for (void *p : ptrs)
     if (p) hipFree(p);
@@ -164,6 +201,10 @@ static int dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, 
     *out = h;
     return FU_OK;
   }
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_bnd, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(FU_ERR_HIP, "fu_dist_create: communication stream"));
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   ncclResult_t r = ncclCommInitRank(&d->comm, nranks, id, rank);

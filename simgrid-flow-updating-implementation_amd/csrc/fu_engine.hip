@@ -65,9 +65,14 @@ __device__ inline void block_max_to(unsigned long long x, unsigned long long *ds
 // ------------------------------------------------------------------------------------
 // Round 0: the timeout fire on zero state (CA:33-34, CA:87-91 -> CA:105-128)
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_round0(int n, const int *__restrict__ rowptr,
-                                                   const double *__restrict__ v, double *__restrict__ a) {
+// a_0 (the timeout fire on zero state) into A[0]; a_{-1} = 0.0 into A[2] (na slots, ghosts
+// included); the three packing slots cleared (no codes yet)
+__global__ __launch_bounds__(kBlock) void k_round0(int n, int na, const int *__restrict__ rowptr,
+                                                   const double *__restrict__ v, double *__restrict__ a,
+                                                   double *__restrict__ a_m1, unsigned long long *__restrict__ pctl) {
   const int i = blockIdx.x * kBlock + threadIdx.x;
+  if (i < 6) pctl[i] = 0ull;  // 3 x 16-byte PackCtl
+  if (i < na) a_m1[i] = 0.0;
   if (i >= n) return;
   a[i] = ((v[i] - 0.0) + 0.0) / (double)(rowptr[i + 1] - rowptr[i] + 1);
 }
@@ -258,19 +263,33 @@ __global__ __launch_bounds__(kBlock) void k_round0_flows(long long E, const int 
   if (lds)
     for (int q = t; q <= span; q += kBlock) s_rp[q] = rowptr[r0 + q];
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < kR0E / kBlock; ++u) {
-    const long long k = e0 + t + u * kBlock;
-    if (k < E) {
-      int lo = 0, hi = span - 1;
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if ((lds ? s_rp[mid] : rowptr[r0 + mid]) <= k) lo = mid; else hi = mid - 1;
-      }
-      st_f_full(F0, (int)k, (0.0 + a[r0 + lo]) - 0.0);
-      st_f_full(F1, (int)k, -0.0);
-    }
+  // thread t: edges k0 .. k0 + 3, 4-aligned, so each split-word store is one 16-byte lane store
+  const long long k0 = e0 + 4 * t;
+  if (k0 >= E) return;
+  auto rp = [&](int q) { return lds ? s_rp[q] : rowptr[r0 + q]; };
+  int lo = 0, hi = span - 1;  // row of k0 relative to r0
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (rp(mid) <= k0) lo = mid; else hi = mid - 1;
   }
+  unsigned hw[4], lw[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long k = k0 + u;
+    while (lo + 1 < span && rp(lo + 1) <= k) ++lo;  // next rows (empty ones skipped)
+    const double fv = k < E ? (0.0 + a[r0 + lo]) - 0.0 : 0.0;
+    hw[u] = (unsigned)__double2hiint(fv);
+    lw[u] = (unsigned)__double2loint(fv);
+  }
+  // split words: block k / 32 holds 32 high words, then 32 low words; E is padded to whole
+  // 32-edge blocks in F, so the tail lanes write padding
+  const long long j = ((k0 & ~31LL) << 1) | (k0 & 31);
+  unsigned *w0 = reinterpret_cast<unsigned *>(F0), *w1 = reinterpret_cast<unsigned *>(F1);
+  *reinterpret_cast<uint4 *>(w0 + j) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+  *reinterpret_cast<uint4 *>(w0 + j + 32) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  const unsigned mh = (unsigned)__double2hiint(-0.0), ml = (unsigned)__double2loint(-0.0);
+  *reinterpret_cast<uint4 *>(w1 + j) = make_uint4(mh, mh, mh, mh);
+  *reinterpret_cast<uint4 *>(w1 + j + 32) = make_uint4(ml, ml, ml, ml);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1221,6 +1240,8 @@ struct fu_handle {
   int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
   int ntiles_geo[4] = {0, 0, 0, 0};
   int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
+  int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
+  double *halo_a = nullptr;          // multi-GPU: the estimate buffer the round being launched writes
   std::vector<int32_t> h_hrows;
   int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first (per geometry)
   int n_hub = 0;
@@ -1273,7 +1294,7 @@ constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 // Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
 // block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
 // {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy) {
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -1315,6 +1336,18 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     all.insert(all.end(), heavy.begin(), heavy.end());
   }
   *nheavy = (int)all.size();
+  // multi-GPU (ghost estimate slots exist): light tiles that read a ghost go first, so the
+  // halo exchange can start once they are done, beside the interior tiles
+  *nbound = 0;
+  if (h->na > h->n) {
+    auto has_ghost = [&](const int4 &tl) {
+      for (int32_t e = tl.z; e < tl.w; ++e)
+        if (h->h_col[e] >= h->n) return true;
+      return false;
+    };
+    auto mid = std::stable_partition(light.begin(), light.end(), has_ghost);
+    *nbound = (int)(mid - light.begin());
+  }
   all.insert(all.end(), light.begin(), light.end());
   if (*dst) hipFree(*dst);
   *dst = nullptr;
@@ -1356,7 +1389,8 @@ int build_hubs(fu_handle *h) {
 int build_tiles(fu_handle *h) {
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g]))
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g],
+                                  &h->nbound_geo[g]))
       return rc;
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
@@ -1572,15 +1606,19 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   if (r == 0) {
     // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91); f_{-1} = -0.0 and
     // a_{-1} = 0.0 so that round 1 reproduces round 0's (0.0 + a) - 0.0
-    hipLaunchKernelGGL(k_round0, dim3(grid_for(h->n)), dim3(kBlock), 0, h->stream, h->n, h->rowptr, h->v, h->a[0]);
+    static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
+    hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
+                       h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
     if (h->E)
       hipLaunchKernelGGL(k_round0_flows, dim3((unsigned)((h->E + kR0E - 1) / kR0E)), dim3(kBlock), 0, h->stream,
                          (long long)h->E, h->rowptr, h->blk_row, h->a[0], h->f[0], h->f[1]);
-    HIP_TRY(hipMemsetAsync(h->a[2], 0, sizeof(double) * h->na, h->stream));  // a_{-1} = 0.0
-    HIP_TRY(hipMemsetAsync(h->pctl, 0, sizeof(PackCtl) * 3, h->stream));      // no codes yet
     if (check)
       hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
                          h->a[0], h->target, err_slot);
+    if (h->dist) {  // a_0 of the boundary nodes to the peers
+      h->halo_a = h->a[0];
+      if (int rc = fu__dist_round_hook(h, 2)) return rc;
+    }
   } else if (h->kernel == 8) {
     double *F = h->f[r & 1];
     const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -1630,7 +1668,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     // light-path register budget)
     const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
     const int hub_sep = h->n_hub ? 1 : 0;  // k_hub_flows writes the hubs' flows after the chains
-    const bool fork = nh > 0 && h->fork_heavy;
+    const int nb = h->nbound_geo[h->geo];  // boundary light tiles (multi-GPU), then the interior
+    // multi-GPU: heavy tiles stay on the main stream, ahead of the boundary tiles and the halo
+    const bool fork = nh > 0 && h->fork_heavy && !h->dist;
     hipStream_t hs = fork ? h->stream2 : h->stream;
     if (fork) {
       HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
@@ -1647,11 +1687,20 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                          hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
                          h->hrows, hub_sep);                                                              \
-    if (nl)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl), dim3(kBlock), 0, h->stream,        \
+    if (nb)                                                                                               \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nb), dim3(kBlock), 0, h->stream,        \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
                          err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
                          nullptr, nullptr, 0);                                                            \
+    if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
+      h->halo_a = an;                                                                                     \
+      if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
+    }                                                                                                     \
+    if (nl - nb)                                                                                          \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl - nb), dim3(kBlock), 0, h->stream,   \
+                         h->tiles_geo[h->geo] + nh + nb, h->rowptr, h->col, h->v, F, ap, ap2, an,          \
+                         h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1),  \
+                         nullptr, nullptr, nullptr, 0);                                                   \
   } while (0)
 #define FU_RECON(C, N, D)                                                                                 \
   do {                                                                                                    \
@@ -1700,9 +1749,6 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       HIP_TRY(hipEventRecord(h->ev_pw, h->stream));
       h->pw_pending = true;
     }
-  }
-  if (h->dist) {
-    if (int rc = fu__dist_round_hook(h, 1)) return rc;
   }
   return FU_OK;
 }
@@ -1982,6 +2028,9 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
 int fu_reset(fu_handle *h) {
   if (!h) return fail(FU_ERR_ARG, "fu_reset: NULL handle");
   if (int rc = set_device(h)) return rc;
+  if (h->dist) {
+    if (int rc = fu__dist_round_hook(h, 0)) return rc;
+  }
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
   h->pw_pending = false;  // the stream is idle: no plan copy in flight
@@ -2290,6 +2339,9 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done) {
 int fu_synchronize(fu_handle *h) {
   if (!h) return fail(FU_ERR_ARG, "fu_synchronize: NULL handle");
   if (int rc = set_device(h)) return rc;
+  if (h->dist) {
+    if (int rc = fu__dist_round_hook(h, 0)) return rc;  // the stream waits for the last halo
+  }
   HIP_TRY(hipStreamSynchronize(h->stream));
   return FU_OK;
 }
@@ -2630,5 +2682,6 @@ hipStream_t fu__handle_stream(fu_handle *h) { return h->stream; }
 unsigned long long *fu__handle_err(fu_handle *h) { return h->err; }
 int fu__handle_device(fu_handle *h) { return h->device; }
 double *fu__handle_cur_a(fu_handle *h) { return cur_a(h); }
+double *fu__handle_halo_a(fu_handle *h) { return h->halo_a; }
 
 }

@@ -30,7 +30,10 @@ for s in $STEPS; do
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;
     rmat)   step bench_rmat 500 python bench.py --workload rmat --n 22 --no-conv --cpu-seconds 0 --steps 100 ;;
     ubench) step ubench 200 tools/bin/ubench_gather ;;
-    rggdist) step bench_rggdist 500 python bench.py --workload rgg-dist --n 8388608 --steps 300 ;;
+    rggdist) step bench_rggdist 500 python bench.py --workload rgg-dist --steps 100 --warmup 5 ;;
+    pairwise) step bench_pairwise 400 python bench.py --workload pairwise --steps 400 --warmup 50 ;;
+    profpw) export TMPDIR=/tmp
+            step profpw 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profpw" -o run -- python3 "$ROOTDIR/bench.py" --workload pairwise --steps 400 --warmup 50 --cpu-seconds 0 ;;
     pmc)    step pmc 900 bash tools/pmc.sh ;;
     *) echo "unknown step $s" ;;
   esac
