@@ -365,7 +365,10 @@ __device__ inline T ld_stream(const T *p) {
 //   5 = hub chains skipped (prices the exact sequential hub sums);
 //   6 = the flow pass of multi-chunk heavy rows skips its estimate gathers;
 //   12 = 1 and 2 together (prices col + the per-node arrays alone).
-template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0>
+// PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
+// order) by the two staging passes; the tile reads it coalesced instead of col + gather.
+template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
+          bool PRE = false>
 __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
@@ -374,7 +377,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     unsigned long long *__restrict__ err,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
-    const int *__restrict__ hrows, int hub_sep) {
+    const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -411,11 +414,14 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
           const int k = c0 + lane + 64 * u;
-          cc[u] = k < d ? col[b + k] : 0;
+          if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
+          else cc[u] = k < d ? col[b + k] : 0;
           fo[u] = k < d ? ld_f(F, b + k) : 0.0;
         }
+        if constexpr (!PRE) {
 #pragma unroll
-        for (int u = 0; u < PL; ++u) er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+          for (int u = 0; u < PL; ++u) er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+        }
         wave_sync();  // the previous chunk's chain is done with the buffer
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
@@ -444,12 +450,15 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int k = k0 + lane + 64 * u;
-          cc[u] = k < d ? col[b + k] : 0;
+          if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
+          else cc[u] = k < d ? col[b + k] : 0;
           fo[u] = k < d ? ld_f(F, b + k) : 0.0;
         }
+        if constexpr (!PRE) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          er[u] = k0 + lane + 64 * u < d ? (DIAG == 6 ? 0.0 : ld_est(pp, code_prev, a_prev, cc[u])) : 0.0;
+          for (int u = 0; u < 4; ++u)
+            er[u] = k0 + lane + 64 * u < d ? (DIAG == 6 ? 0.0 : ld_est(pp, code_prev, a_prev, cc[u])) : 0.0;
+        }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int k = k0 + lane + 64 * u;
@@ -528,7 +537,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const int c0 = b + c * CH, cn = min(CH, e - c0);
       double *xs = s_x + (c & 1) * CH, *es = s_er + (c & 1) * CH;
       for (int q = tid; q < cn; q += nthr) {
-        const double er = ld_est(pp, code_prev, a_prev, col[c0 + q]);
+        const double er = PRE ? Gb[c0 + q] : ld_est(pp, code_prev, a_prev, col[c0 + q]);
         xs[q] = recon_fr(ld_f(F, c0 + q), er, own2);
         es[q] = er;
       }
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     __syncthreads();
     const double a = s_a[0];
     for (int k = b + t; k < e; k += kBlock) {
-      const double er = ld_est(pp, code_prev, a_prev, col[k]);
+      const double er = PRE ? Gb[k] : ld_est(pp, code_prev, a_prev, col[k]);
       const double fo = ld_f(F, k);
       st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
     }
@@ -576,8 +585,12 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const int q = t + k * kBlock;
     c[k] = 0;
     x[k] = 0.0;
+    g[k] = 0.0;
     if (q < ne) {
-      if (NT) {
+      if (PRE) {
+        g[k] = Gb[e0 + q];
+        x[k] = ld_f(F, e0 + q);
+      } else if (NT) {
         c[k] = ld_stream(col + e0 + q);
         x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_f(F, e0 + q);
       } else {
@@ -591,7 +604,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
   const double vv = t < nn ? v[nb + t] : 0.0;
   const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
-  if (DIAG != 0 || pp.width == 0) {
+  if (PRE) {
+  } else if (DIAG != 0 || pp.width == 0) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
@@ -689,6 +703,7 @@ struct StageArgs {
   const unsigned short *sidx16[4];     // per light-tile edge, slice order: position | run << 10
   const int *dtab[4];                  // per light tile: kStageRuns x (G index - m) of each run
   int sel[4];                          // layout used for tables of width 8, 16, 32, 0
+  int f64;                             // kernel 9: always stage the doubles (layout 3)
 };
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
@@ -805,8 +820,9 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         void *__restrict__ G) {
   __shared__ __align__(16) unsigned char s_tab[kStageLds];
   const PackCtl pp = ctl[rslot ^ 1];
-  const int wb = pp.width ? pp.width / 8 : 8;  // bytes per element of the table gathered
-  const int li = sa.sel[width_index(pp.width)];
+  // bytes per element of the table gathered (kernel 9 stages the doubles, always written)
+  const int wb = (pp.width && !sa.f64) ? pp.width / 8 : 8;
+  const int li = sa.f64 ? 3 : sa.sel[width_index(pp.width)];
   if ((int)blockIdx.x >= sa.NB[li]) return;
   const int4 rg = sa.brange[li][blockIdx.x];
   if (rg.x >= rg.y) return;  // no slice here (grid rounded to whole XCD rows) or empty region
@@ -814,7 +830,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
   const int SN = sa.SN[li];
   const int nb = rg.z * SN;
   const int cnt = min(SN, n - nb);
-  const void *src = pp.width ? code_prev : static_cast<const void *>(a_prev);
+  const void *src = (pp.width && !sa.f64) ? code_prev : static_cast<const void *>(a_prev);
   const unsigned short *colS = sa.colS[li];
 #define FU_BODY(T)                                                                                    \
   do {                                                                                                \
@@ -830,6 +846,111 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
   else if (wb == 4) FU_BODY(unsigned);
   else FU_BODY(unsigned long long);
 #undef FU_BODY
+}
+
+// ------------------------------------------------------------------------------------
+// Kernel 9, "pregather": propagation blocking for power-law graphs, where tiles touch far
+// more slices than kernel 8's u16 index can address and most edges sit in heavy rows. Two
+// passes turn every random gather a_{r-1}[col e] into streams:
+//   * k_stage (doubles, 128 KB slices): G_A in slice-major order, within slice s the edges
+//     whose neighbour lies in s, in edge order (so each bucket of kTrBE consecutive edges
+//     has one contiguous run per slice);
+//   * k_transpose: one block per bucket reads its runs (the run starts of every slice are
+//     precomputed per bucket), scatters the values into LDS by their position in the bucket
+//     and writes Gb[e] for the bucket's edges, coalesced.
+// The round kernels (kernel 4's tiles, heavy rows and mega hubs, PRE = true) then read Gb[e]
+// beside the flows. Bytes per edge: stage 2 + 8, transpose 8 + 2 + 8, round 8 (instead of
+// col 4 + one random 8-byte gather).
+// ------------------------------------------------------------------------------------
+constexpr int kTrBE = 16384;   // edges per bucket (its values fill 128 KB of LDS)
+constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
+constexpr int kTrThreads = 1024;
+
+__global__ __launch_bounds__(kTrThreads) void k_transpose(int P, long long E, const int *__restrict__ offT,
+                                                        const double *__restrict__ GA,
+                                                        const unsigned short *__restrict__ pos16,
+                                                        double *__restrict__ GB) {
+  __shared__ double s_v[kTrBE];
+  __shared__ int s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
+  __shared__ int s_o[kTrMaxP];      // G_A index of each run
+  __shared__ int s_c[kTrBE / 64 + 1];
+  __shared__ int s_w[kTrThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const long long e0 = (long long)blockIdx.x * kTrBE;
+  const int ne = (int)min((long long)kTrBE, E - e0);
+  // runs: thread t owns slices 2t, 2t + 1
+  int o[2], len[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int sl = 2 * t + j;
+    o[j] = sl < P ? offT[(long long)blockIdx.x * P + sl] : 0;
+    len[j] = sl < P ? offT[(long long)(blockIdx.x + 1) * P + sl] - o[j] : 0;
+  }
+  // exclusive scan of len0 + len1 over the block: wave shuffles, then the 16 wave totals
+  int x = len[0] + len[1];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(x, off, 64);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_w[w] = x;
+  __syncthreads();
+  int base = 0;
+  for (int k = 0; k < w; ++k) base += s_w[k];
+  const int excl = base + x - (len[0] + len[1]);
+  if (2 * t < P) {
+    s_m[2 * t] = excl;
+    s_o[2 * t] = o[0];
+  }
+  if (2 * t + 1 < P) {
+    s_m[2 * t + 1] = excl + len[0];
+    s_o[2 * t + 1] = o[1];
+  }
+  if (t == 0) s_m[P] = ne;
+  __syncthreads();
+  // coarse table: the run holding element 64 k (s_c), so each element's search spans only
+  // the runs of its 64-element stretch
+  if (t < kTrBE / 64) {
+    const int m = t * 64;
+    int lo = 1, hi = P;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_m[mid] > m) hi = mid; else lo = mid + 1;
+    }
+    s_c[t] = lo;
+  }
+  if (t == 0) s_c[kTrBE / 64] = P;
+  __syncthreads();
+  // element m (the bucket's G_A runs in slice order) -> G_A index; all searches first, then
+  // every load of the thread in flight at once, then the LDS scatter by bucket position
+  constexpr int kPerT = kTrBE / kTrThreads;
+  int g[kPerT];
+#pragma unroll
+  for (int k = 0; k < kPerT; ++k) {
+    const int m = t + k * kTrThreads;
+    g[k] = -1;
+    if (m < ne) {
+      int lo = s_c[m >> 6], hi = s_c[(m >> 6) + 1];  // first boundary s_m[s] > m lies in [lo, hi]
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_m[mid] > m) hi = mid; else lo = mid + 1;
+      }
+      const int run = lo - 1;  // s_m[run] <= m < s_m[run + 1]: a non-empty run
+      g[k] = s_o[run] + (m - s_m[run]);
+    }
+  }
+  double val[kPerT];
+  unsigned short pos[kPerT];
+#pragma unroll
+  for (int k = 0; k < kPerT; ++k) {
+    val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
+    pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
+  }
+#pragma unroll
+  for (int k = 0; k < kPerT; ++k)
+    if (g[k] >= 0) s_v[pos[k]] = val[k];
+  __syncthreads();
+  for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
 }
 
 // DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
@@ -962,7 +1083,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
                                                       const double *__restrict__ a_prev2,
                                                       const void *__restrict__ code_prev,
                                                       const PackCtl *__restrict__ ctl, int rslot,
-                                                      double2 *__restrict__ hubxy) {
+                                                      double2 *__restrict__ hubxy, const double *__restrict__ Gb) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
@@ -973,7 +1094,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
   const int4 hb = hubs[lo];
   const int k = hb.y + (int)(q - hb.w);
   const PackCtl pp = ctl[rslot ^ 1];
-  const double er = ld_est(pp, code_prev, a_prev, col[k]);
+  const double er = Gb ? Gb[k] : ld_est(pp, code_prev, a_prev, col[k]);
   hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
 }
 
@@ -1279,6 +1400,18 @@ struct fu_handle {
   int seen_width = 0;                     // packing width the host last saw
   int st_force = -1;                      // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
   std::vector<int4> h_light;              // host copy (layout construction)
+  // kernel 9 (pregather): slice-major G_A, per-bucket run starts, edge-order Gb
+  struct TransLayout {
+    int P = 0, Q = 0, NB = 0, B = 0;      // slices, blocks per slice, stage blocks, buckets
+    int4 *brange = nullptr;               // stage blocks: {begin, end} in G_A, slice, 0
+    unsigned short *colS = nullptr;       // per G_A element: column offset in its slice
+    unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
+    int *offT = nullptr;                  // (B + 1) x P: G_A index where bucket b's run of slice s starts
+    double *GA = nullptr, *GB = nullptr;
+  };
+  TransLayout tr;
+  bool tr_ready = false;
+  std::string tr_why;
   int n_cu = 256;
   void *dist = nullptr;  // multi-GPU (fu_dist.hip)
 };
@@ -1594,6 +1727,74 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
   return sa;
 }
 
+// Kernel 9 preparation (see k_transpose): slices of 16K nodes, buckets of kTrBE edges. G_A:
+// slice-major, within a slice in edge order, each slice's region starting at a multiple of
+// 16 (the stage launch stores 16 bytes per lane); offT[b * P + s] = where bucket b's run of
+// slice s starts (offT[B * P + s]: the end of slice s's elements); stage blocks cut each
+// slice's region into Q pieces.
+int ensure_transpose(fu_handle *h) {
+  if (h->tr_ready) return FU_OK;
+  if (!h->tr_why.empty()) return fail(FU_ERR_GRAPH, h->tr_why);
+  const int64_t n = h->n, E = h->E;
+  const int64_t SN = kStageLds / 8;
+  const int64_t P = (n + SN - 1) / SN;
+  if (E == 0 || P > kTrMaxP) {
+    h->tr_why = E == 0 ? "kernel 9 (pregather): no edges" : "kernel 9 (pregather): more than 2^25 nodes";
+    return fail(FU_ERR_GRAPH, h->tr_why);
+  }
+  const int64_t B = (E + kTrBE - 1) / kTrBE;
+  std::vector<int64_t> cnt(P, 0);
+  for (int64_t e = 0; e < E; ++e) cnt[h->h_col[e] / SN]++;
+  std::vector<int64_t> reg(P + 1, 0);
+  for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
+  const int64_t total = reg[P];
+  if (total >= (int64_t)INT32_MAX) {
+    h->tr_why = "kernel 9 (pregather): more than 2^31 staged elements";
+    return fail(FU_ERR_GRAPH, h->tr_why);
+  }
+  std::vector<uint16_t> colS(total, 0), pos(total, 0);
+  std::vector<int32_t> offT((size_t)(B + 1) * P);
+  std::vector<int64_t> cur(reg.begin(), reg.end() - 1);
+  for (int64_t b = 0; b < B; ++b) {
+    for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
+    const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
+    for (int64_t e = b * kTrBE; e < e1; ++e) {
+      const int32_t c = h->h_col[e];
+      const int64_t g = cur[c / SN]++;
+      colS[g] = (uint16_t)(c % SN);
+      pos[g] = (uint16_t)(e - b * kTrBE);
+    }
+  }
+  for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)B * P + s2] = (int32_t)cur[s2];
+  // stage pieces by element count, not per slice: under the degree layout the hottest slice
+  // holds ~40% of all elements (R-MAT-24), so a slice gets as many blocks as its share
+  // (each re-reads the 128 KB slice, mostly from L2)
+  const int64_t piece = std::max<int64_t>(16384, (total / (4 * (int64_t)h->n_cu) + 15) / 16 * 16);
+  std::vector<int4> br;
+  for (int64_t s2 = 0; s2 < P; ++s2)
+    for (int64_t p0 = reg[s2]; p0 < reg[s2 + 1] || p0 == reg[s2]; p0 += piece)
+      br.push_back(make_int4((int)p0, (int)std::min(reg[s2 + 1], p0 + piece), (int)s2, 0));
+  const int64_t Q = (int64_t)br.size() / P;
+  auto &T = h->tr;
+  auto up = [&](auto **dst, const auto *src, size_t count) -> int {
+    if (int rc = dmalloc(dst, std::max<size_t>(1, count))) return rc;
+    if (count) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * count, hipMemcpyHostToDevice));
+    return FU_OK;
+  };
+  if (int rc = up(&T.brange, br.data(), br.size())) return rc;
+  if (int rc = up(&T.colS, colS.data(), colS.size())) return rc;
+  if (int rc = up(&T.pos16, pos.data(), pos.size())) return rc;
+  if (int rc = up(&T.offT, offT.data(), offT.size())) return rc;
+  if (int rc = dmalloc(&T.GA, (size_t)total)) return rc;
+  if (int rc = dmalloc(&T.GB, (size_t)E)) return rc;
+  T.P = (int)P;
+  T.Q = (int)Q;
+  T.NB = (int)br.size();
+  T.B = (int)B;
+  h->tr_ready = true;
+  return FU_OK;
+}
+
 inline unsigned grid_for(long long work) { return (unsigned)((work + kBlock - 1) / kBlock); }
 
 // One round: state of round r-1 -> round r. err_slot: nullptr = no check.
@@ -1638,11 +1839,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                            h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0);
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr);
       else
         hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                            h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0);
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr);
     }
 #define FU_STAGED(C, D)                                                                                  \
   hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
@@ -1663,6 +1864,64 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     double *F = h->f[r & 1];
     const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
     double *an = h->a[r % 3];
+    const bool pre = h->kernel == 9;  // kernel 9: stage + transpose, then kernel 4 reading Gb
+    const double *Gb = pre ? h->tr.GB : nullptr;
+    if (pre) {
+      // the mega hubs' long exact chains do not wait for the two passes: their (fr, er) are
+      // gathered directly and their chains run on the side stream from the round's start
+      const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
+      const int4 *tl = h->tiles_geo[1];
+      if (nmega) {
+        HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+        HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+        hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
+                           h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl,
+                           (int)(r & 1), h->hubxy, nullptr);
+        if (check)
+          hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2>), dim3(nmega), dim3(kBlock), 0, h->stream2,
+                             tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->code[(r - 1) & 1],
+                             h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, h->hrows, 1, nullptr);
+        else
+          hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 2>), dim3(nmega), dim3(kBlock), 0, h->stream2,
+                             tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->code[(r - 1) & 1],
+                             h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, h->hrows, 1, nullptr);
+        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
+                           h->hub_rows, (long long)h->hub_total, h->hubxy, an, F);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+      }
+      StageArgs sa{};
+      for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
+      sa.P[3] = h->tr.P;
+      sa.Q[3] = h->tr.Q;
+      sa.SN[3] = kStageLds / 8;
+      sa.NB[3] = h->tr.NB;
+      sa.brange[3] = h->tr.brange;
+      sa.colS[3] = h->tr.colS;
+      sa.f64 = 1;
+      hipLaunchKernelGGL(k_stage, dim3(h->tr.NB), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
+                         h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA);
+      hipLaunchKernelGGL(k_transpose, dim3(h->tr.B), dim3(kTrThreads), 0, h->stream, h->tr.P, (long long)h->E,
+                         h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+#define FU_PRE(C)                                                                                         \
+  do {                                                                                                    \
+    if (nh > nmega)                                                                                       \
+      hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 2, true>), dim3(nh - nmega), dim3(kBlock), 0, \
+                         h->stream, tl + nmega, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,  \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
+                         h->hrows, 1, Gb);                                                                \
+    if (nl)                                                                                               \
+      hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, h->stream, \
+                         tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
+                         nullptr, 0, Gb);                                                                 \
+  } while (0)
+      if (check) FU_PRE(true);
+      else FU_PRE(false);
+#undef FU_PRE
+      HIP_TRY(hipGetLastError());
+      if (nmega) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+    } else {
     // heavy tiles (hubs, heavy rows) lead the tile list: they run as their own launch on the
     // side stream, concurrently with the light tiles' launch (which then keeps kernel 4's
     // light-path register budget)
@@ -1679,35 +1938,35 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (h->n_hub)
       hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
-                         h->hubxy);
-#define FU_RECON_G(C, N, D, TE, TN)                                                                       \
+                         h->hubxy, Gb);
+#define FU_RECON_G(C, N, D, TE, TN, PR)                                                                   \
   do {                                                                                                    \
     if (nh)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh), dim3(kBlock), 0, \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nh), dim3(kBlock), 0, \
                          hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
-                         h->hrows, hub_sep);                                                              \
+                         h->hrows, hub_sep, Gb);                                                          \
     if (nb)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nb), dim3(kBlock), 0, h->stream,        \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, PR>), dim3(nb), dim3(kBlock), 0, h->stream,    \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
                          err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
-                         nullptr, nullptr, 0);                                                            \
+                         nullptr, nullptr, 0, Gb);                                                        \
     if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
       h->halo_a = an;                                                                                     \
       if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
     }                                                                                                     \
     if (nl - nb)                                                                                          \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl - nb), dim3(kBlock), 0, h->stream,   \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, PR>), dim3(nl - nb), dim3(kBlock), 0, h->stream, \
                          h->tiles_geo[h->geo] + nh + nb, h->rowptr, h->col, h->v, F, ap, ap2, an,          \
                          h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1),  \
-                         nullptr, nullptr, nullptr, 0);                                                   \
+                         nullptr, nullptr, nullptr, 0, Gb);                                               \
   } while (0)
 #define FU_RECON(C, N, D)                                                                                 \
   do {                                                                                                    \
-    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                                      \
-    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                                 \
-    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                                 \
-    else FU_RECON_G(C, N, D, 512, 64);                                                                    \
+    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256, false);                                          \
+    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256, false);                                          \
+    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128, false);                                          \
+    else FU_RECON_G(C, N, D, 512, 64, false);                                                             \
   } while (0)
 #ifdef FU_DIAG
     if (h->diag == 1) FU_RECON(false, false, 1);
@@ -1734,6 +1993,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
       HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     }
+    }  // kernel 4
   }
   HIP_TRY(hipGetLastError());
   h->rounds++;
@@ -1757,13 +2017,14 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 struct TuneCand {
   int kernel, geo;
 };
-constexpr TuneCand kCands[] = {{4, 0}, {4, 3}, {8, 1}, {4, 1}};
+constexpr TuneCand kCands[] = {{4, 0}, {4, 3}, {8, 1}, {4, 1}, {9, 1}};
 constexpr int kNCands = (int)(sizeof(kCands) / sizeof(kCands[0]));
 static int width_class(int w) { return w == 8 ? 1 : w == 16 ? 2 : w == 32 ? 3 : 0; }
 static void use_cand(fu_handle *h, const TuneCand &c) {
   h->kernel = c.kernel;
   h->geo = c.geo;
 }
+int ensure_transpose(fu_handle *h);
 
 int set_device(fu_handle *h) {
   HIP_TRY(hipSetDevice(h->device));
@@ -1951,12 +2212,16 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
-    if (value != 0 && value != 4 && value != 8)
-      return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon) or 8 (stage)");
-    if (h->dist && value == 8) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernel 4 (recon)");
+    if (value != 0 && value != 4 && value != 8 && value != 9)
+      return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon), 8 (stage) or 9 (pregather)");
+    if (h->dist && value >= 8) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernel 4 (recon)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     if (value == 8) {
       if (int rc = ensure_stage(h)) return rc;
+    }
+    if (value == 9) {
+      if (int rc = ensure_transpose(h)) return rc;
+      h->geo = 1;
     }
     h->kernel = value == 0 ? 4 : (int)value;
     h->autotune = value == 0;
@@ -2081,16 +2346,22 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
   // candidate is dropped and none stops early on rank-local timings
   auto active = [&](int c) { return (h->dist || h->tune_out[c] < 2) && !(h->dist && kCands[c].kernel != 4); };
+  // kernel 9 stages the doubles whatever the packing: a candidate of the unpacked table only
+  auto active9 = [&](int c) { return active(c) && !(kCands[c].kernel == 9 && width != 0); };
   int32_t need = 0;
-  for (int c = 0; c < kNCands; ++c) need += active(c) ? 1 + kTimed : 0;
+  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 1 + kTimed : 0;
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
   float best = 1e30f;
   int bi = -1;
   for (int c = 0; c < kNCands; ++c) {
     if (!h->dist && h->tune_out[c] >= 2) continue;  // its last ns per round stays reported
     h->tune_ms[c] = 0.f;
-    if (!active(c)) continue;
+    if (!active9(c)) continue;
     if (kCands[c].kernel == 8 && ensure_stage(h) != FU_OK) {  // no slice layout fits this graph
+      set_error("");
+      continue;
+    }
+    if (kCands[c].kernel == 9 && ensure_transpose(h) != FU_OK) {  // too many nodes for the slices
       set_error("");
       continue;
     }
@@ -2356,6 +2627,9 @@ int fu_destroy(fu_handle *h) {
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
                               h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG};
+  for (void *p : {(void *)h->tr.brange, (void *)h->tr.colS, (void *)h->tr.pos16, (void *)h->tr.offT,
+                  (void *)h->tr.GA, (void *)h->tr.GB})
+    ptrs.push_back(p);
   for (const auto &L : h->st) {
     ptrs.push_back(L.brange);
     ptrs.push_back(L.colS);

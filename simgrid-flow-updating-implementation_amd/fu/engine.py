@@ -16,7 +16,7 @@ import numpy as np
 from . import _lib as L
 from .graph import Graph
 
-KERNELS = {"auto": 0, "recon": 4, "stage": 8}
+KERNELS = {"auto": 0, "recon": 4, "stage": 8, "pregather": 9}
 LAYOUTS = {"given": 0, "degree": 1}
 MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
@@ -25,7 +25,7 @@ def handle_info(h) -> dict:
     """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
     a = np.zeros(32, dtype=np.int64)
     L.call("fu_get_info", h, L.ptr(a))
-    names = {4: "recon", 8: "stage"}
+    names = {4: "recon", 8: "stage", 9: "pregather"}
     return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
             "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
             "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
@@ -38,13 +38,15 @@ def handle_info(h) -> dict:
 
 
 # fu_engine.hip kCands order
-TUNE_CANDIDATES = ("recon", "recon_512", "stage", "recon_1024")
+TUNE_CANDIDATES = ("recon", "recon_512", "stage", "recon_1024", "pregather")
 
 
 def _cand_name(code: int) -> str:
     kernel, geo = divmod(code, 10)
     if kernel == 8:
         return "stage"
+    if kernel == 9:
+        return "pregather"
     return "recon" + {3: "_512", 1: "_1024", 2: "_1024x256"}.get(geo, "")
 
 

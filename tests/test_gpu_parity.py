@@ -15,9 +15,10 @@ from conftest import (ca_sync_fixtures, fixture_decl_csr, load_json, load_npz, t
 
 pytestmark = pytest.mark.gpu
 
-# kernel 4 (recon: LDS tiles with flow reconstruction) and kernel 8 (stage: LDS-staged
-# slices + recon tiles); "auto" switches between them and kernel 4's tile geometries mid-run
-KERNELS = ["recon", "stage"]
+# kernel 4 (recon: LDS tiles with flow reconstruction), kernel 8 (stage: LDS-staged slices +
+# recon tiles) and kernel 9 (pregather: slice staging + per-bucket transpose, then recon
+# tiles reading the pre-gathered estimates); "auto" switches between them mid-run
+KERNELS = ["recon", "stage", "pregather"]
 
 
 def _check_fixture(meta, kernel, hub_threshold=None):
@@ -115,7 +116,7 @@ def test_isolated_and_empty():
 def test_option_errors():
     g = fu.Graph.random_regular(64, 4, seed=1)
     eng = fu.CollectAll(g, np.ones(g.n))
-    for k in (1, 2, 3, 5, 6, 7, 9, 10, 11):  # removed variants / out of range
+    for k in (1, 2, 3, 5, 6, 7, 10, 11):  # removed variants / out of range
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag"):
@@ -129,6 +130,9 @@ def test_option_errors():
     eng.reset()
     eng.set_option("kernel", 8)
     eng.run(1)
+    eng.reset()
+    eng.set_option("kernel", 9)
+    eng.run(2)
 
 
 @pytest.mark.parametrize("persistent", [False, True])
@@ -379,7 +383,7 @@ def _er_with_outlier_pairs(n, m, pairs, seed):
 
 
 @pytest.mark.parametrize("kind,kernel", [("er", "recon"), ("rmat", "recon"), ("er", "stage"),
-                                         ("rmat", "stage")])
+                                         ("rmat", "stage"), ("er", "pregather"), ("rmat", "pregather")])
 def test_packed_gather_long_run_bitwise(kind, kernel):
     """The packed estimate table (8/16/32-bit lossless codes + escapes) switches on as the
     estimates converge; 300 rounds must still equal the C oracle bit for bit, and equal the
@@ -413,7 +417,7 @@ def test_packed_gather_with_kernel_switches():
     g = fu.Graph.erdos_renyi(50_000, 200_000, seed=9)
     v = fu.uniform_values(g.n, seed=9)
     ref = None
-    for kernel in ("recon", "stage", "auto"):
+    for kernel in ("recon", "stage", "pregather", "auto"):
         eng = fu.CollectAll(g, v, kernel=kernel)
         eng.set_option("pack_every", 2)
         eng.run(260)
@@ -464,6 +468,22 @@ def test_stage_forced_layouts_bitwise(layout):
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     assert seen & {8, 16, 32}, seen
+
+
+@pytest.mark.parametrize("mega", [64, 300, 8192])
+def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
+    """Kernel 9 on R-MAT with heavy rows (hub_threshold 16) and mega hubs above `mega`
+    (k_hub_stage reading the pre-gathered estimates), packed rounds included; several
+    buckets and slices (n > 16K nodes, E > 16K edges)."""
+    g = fu.Graph.rmat(15, 16, seed=15)
+    v = fu.uniform_values(g.n, seed=15)
+    eng = fu.CollectAll(g, v, kernel="pregather", hub_threshold=16)
+    eng.set_option("mega_hub", mega)
+    eng.set_option("pack_every", 4)
+    eng.run(60)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 60, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
 
 
 @pytest.mark.parametrize("tile", [2048, 1024, 512])

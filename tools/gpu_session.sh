@@ -19,7 +19,7 @@ step() {  # name limit cmd...
 }
 for s in $STEPS; do
   case $s in
-    pytest) step pytest 1100 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ;;
+    pytest) step pytest 1100 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} ;;
     smoke)  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)  step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)   export TMPDIR=/tmp
@@ -28,9 +28,9 @@ for s in $STEPS; do
     sweepdiag) step sweepdiag 900 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/libfu_diag.so python tools/sweep.py ${SWEEP_ARGS:-} ;;
     replay) step replay 400 python tools/bench_replay.py ;;
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;
-    rmat)   step bench_rmat 500 python bench.py --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ;;
+    rmat)   step bench_rmat 500 python bench.py --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ${RMAT_ARGS:-} ;;
     profrmat) export TMPDIR=/tmp
-            step profrmat 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profrmat" -o run -- python3 "$ROOTDIR/bench.py" --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ;;
+            step profrmat 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profrmat" -o run -- python3 "$ROOTDIR/bench.py" --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ${RMAT_ARGS:-} ;;
     ubench) step ubench 200 tools/bin/ubench_gather ;;
     rggdist) step bench_rggdist 500 python bench.py --workload rgg-dist --steps 100 --warmup 5 ;;
     pairwise) step bench_pairwise 400 python bench.py --workload pairwise --steps 400 --warmup 50 ;;
