@@ -733,23 +733,33 @@ __device__ __forceinline__ unsigned col_at(const ColVec<EPL> &c, int j) {
   return (j & 1) ? w >> 16 : w & 0xFFFFu;
 }
 
-// One batch: kStageU steps of EPL elements per lane, all column loads first (caller), then
-// the LDS (or global) lookups and one 16-byte store per step.
+// Per lane per step: EPL = 16 / sizeof(T) elements, one lane-contiguous 16-byte G store.
+// Steps per batch: enough that every lane keeps 64 B of column loads in flight whatever the
+// element width (4 steps of 4-byte loads for doubles left 16 KB in flight per CU, ~2 TB/s at
+// HBM latency).
+template <typename T>
+struct StageU {
+  static constexpr int EPL = 16 / (int)sizeof(T);
+  static constexpr int U = EPL >= 8 ? kStageU : kStageU * 8 / EPL;
+};
+
+// One batch: U steps of EPL elements per lane, all column loads first (caller), then the
+// LDS (or global) lookups and one 16-byte store per step.
 template <typename T, bool LDS>
-__device__ __forceinline__ void stage_load(ColVec<16 / sizeof(T)> (&c)[kStageU], int g, int g1,
+__device__ __forceinline__ void stage_load(ColVec<StageU<T>::EPL> (&c)[StageU<T>::U], int g, int g1,
                                            const unsigned short *__restrict__ colS) {
-  constexpr int EPL = 16 / sizeof(T), STEP = kStageThreads * EPL;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, STEP = kStageThreads * EPL;
 #pragma unroll
-  for (int u = 0; u < kStageU; ++u)
+  for (int u = 0; u < U; ++u)
     if (g + u * STEP < g1) ld_cols<EPL>(c[u], colS + g + u * STEP);
 }
 template <typename T, bool LDS>
-__device__ __forceinline__ void stage_put(const ColVec<16 / sizeof(T)> (&c)[kStageU], int g, int g1,
+__device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[StageU<T>::U], int g, int g1,
                                           const unsigned char *s_tab, const T *__restrict__ tab, int nb,
                                           T *__restrict__ G) {
-  constexpr int EPL = 16 / sizeof(T), STEP = kStageThreads * EPL;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, STEP = kStageThreads * EPL;
 #pragma unroll
-  for (int u = 0; u < kStageU; ++u) {
+  for (int u = 0; u < U; ++u) {
     const int gg = g + u * STEP;
     if (gg < g1) {
       T val[EPL];
@@ -774,7 +784,7 @@ template <typename T, bool LDS>
 __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt, int g0, int g1,
                                            const unsigned short *__restrict__ colS,
                                            const T *__restrict__ tab, T *__restrict__ G) {
-  constexpr int EPL = 16 / (int)sizeof(T), BSTEP = kStageU * kStageThreads * EPL;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, BSTEP = U * kStageThreads * EPL;
   constexpr int kW = kStageLds / 16 / kStageThreads;
   const int t = threadIdx.x;
   uint4 buf[kW];
@@ -788,7 +798,7 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
       buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  ColVec<EPL> ca[kStageU], cb[kStageU];
+  ColVec<EPL> ca[U], cb[U];
   int g = g0 + t * EPL;
   stage_load<T, LDS>(ca, g, g1, colS);
   if constexpr (LDS) {  // slice stores after the first batch's loads are in flight
@@ -906,8 +916,13 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int P, long long E, co
     s_m[2 * t + 1] = excl + len[0];
     s_o[2 * t + 1] = o[1];
   }
-  if (t == 0) s_m[P] = ne;
+  if (t == 0) {  // staged elements of the bucket (< ne when mega-hub edges are left out)
+    int tot = 0;
+    for (int k = 0; k < kTrThreads / 64; ++k) tot += s_w[k];
+    s_m[P] = tot;
+  }
   __syncthreads();
+  const int nst = s_m[P];
   // coarse table: the run holding element 64 k (s_c), so each element's search spans only
   // the runs of its 64-element stretch
   if (t < kTrBE / 64) {
@@ -929,7 +944,7 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int P, long long E, co
   for (int k = 0; k < kPerT; ++k) {
     const int m = t + k * kTrThreads;
     g[k] = -1;
-    if (m < ne) {
+    if (m < nst) {
       int lo = s_c[m >> 6], hi = s_c[(m >> 6) + 1];  // first boundary s_m[s] > m lies in [lo, hi]
       while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -1342,6 +1357,7 @@ struct fu_handle {
   int hub_threshold = 64;
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
+  int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
@@ -1519,7 +1535,10 @@ int build_hubs(fu_handle *h) {
   return FU_OK;
 }
 
+void free_transpose(fu_handle *h);
+
 int build_tiles(fu_handle *h) {
+  free_transpose(h);  // its hub exclusion follows the tiles
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
     if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g],
@@ -1732,6 +1751,14 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
 // 16 (the stage launch stores 16 bytes per lane); offT[b * P + s] = where bucket b's run of
 // slice s starts (offT[B * P + s]: the end of slice s's elements); stage blocks cut each
 // slice's region into Q pieces.
+void free_transpose(fu_handle *h) {
+  auto &T = h->tr;
+  for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA, (void *)T.GB})
+    if (p) hipFree(p);
+  T = fu_handle::TransLayout{};
+  h->tr_ready = false;
+}
+
 int ensure_transpose(fu_handle *h) {
   if (h->tr_ready) return FU_OK;
   if (!h->tr_why.empty()) return fail(FU_ERR_GRAPH, h->tr_why);
@@ -1743,8 +1770,14 @@ int ensure_transpose(fu_handle *h) {
     return fail(FU_ERR_GRAPH, h->tr_why);
   }
   const int64_t B = (E + kTrBE - 1) / kTrBE;
+  // mega-hub rows gather directly on the side stream: their edges stay out of G_A
+  std::vector<unsigned char> skip(E, 0);
+  for (int32_t i = 0; i < h->n; ++i)
+    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub)
+      std::fill(skip.begin() + h->h_rowptr[i], skip.begin() + h->h_rowptr[i + 1], (unsigned char)1);
   std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < E; ++e) cnt[h->h_col[e] / SN]++;
+  for (int64_t e = 0; e < E; ++e)
+    if (!skip[e]) cnt[h->h_col[e] / SN]++;
   std::vector<int64_t> reg(P + 1, 0);
   for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
   const int64_t total = reg[P];
@@ -1759,6 +1792,7 @@ int ensure_transpose(fu_handle *h) {
     for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
     const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
     for (int64_t e = b * kTrBE; e < e1; ++e) {
+      if (skip[e]) continue;
       const int32_t c = h->h_col[e];
       const int64_t g = cur[c / SN]++;
       colS[g] = (uint16_t)(c % SN);
@@ -1865,7 +1899,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
     double *an = h->a[r % 3];
     const bool pre = h->kernel == 9;  // kernel 9: stage + transpose, then kernel 4 reading Gb
+    if (pre) {
+      if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
+    }
     const double *Gb = pre ? h->tr.GB : nullptr;
+    if (pre && !Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
     if (pre) {
       // the mega hubs' long exact chains do not wait for the two passes: their (fr, er) are
       // gathered directly and their chains run on the side stream from the round's start
@@ -1931,6 +1969,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     // multi-GPU: heavy tiles stay on the main stream, ahead of the boundary tiles and the halo
     const bool fork = nh > 0 && h->fork_heavy && !h->dist;
     hipStream_t hs = fork ? h->stream2 : h->stream;
+    // with mega hubs, only their tiles go to the side stream (k_hub_stage -> chains ->
+    // k_hub_flows), so the other heavy tiles need not wait for k_hub_stage
+    const int nmh = fork && h->n_hub && h->split_hubs ? h->n_hub : nh;
     if (fork) {
       HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
       HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
@@ -1941,11 +1982,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                          h->hubxy, Gb);
 #define FU_RECON_G(C, N, D, TE, TN, PR)                                                                   \
   do {                                                                                                    \
-    if (nh)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nh), dim3(kBlock), 0, \
+    if (nmh)  /* mega hubs (or every heavy tile) on the side stream */                                   \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nmh), dim3(kBlock), 0, \
                          hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
                          h->hrows, hub_sep, Gb);                                                          \
+    if (nh - nmh)  /* the other heavy tiles ahead of the light ones on the main stream */                \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nh - nmh),  \
+                         dim3(kBlock), 0, h->stream, h->tiles_geo[h->geo] + nmh, h->rowptr, h->col, h->v, F, ap, \
+                         ap2, an, h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl,          \
+                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, Gb);                         \
     if (nb)                                                                                               \
       hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, PR>), dim3(nb), dim3(kBlock), 0, h->stream,    \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
@@ -2270,6 +2316,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "fork_heavy")) {  // kernel 4: heavy tiles on a side stream (1) or in order (0)
     h->fork_heavy = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "split_hubs")) {  // kernel 4: mega-hub tiles alone on the side stream (1)
+    h->split_hubs = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "wave_heavy")) {  // kernel 4: heavy rows one per wave (1) or per block (0)
@@ -2627,9 +2677,7 @@ int fu_destroy(fu_handle *h) {
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
                               h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG};
-  for (void *p : {(void *)h->tr.brange, (void *)h->tr.colS, (void *)h->tr.pos16, (void *)h->tr.offT,
-                  (void *)h->tr.GA, (void *)h->tr.GB})
-    ptrs.push_back(p);
+  free_transpose(h);
   for (const auto &L : h->st) {
     ptrs.push_back(L.brange);
     ptrs.push_back(L.colS);

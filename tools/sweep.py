@@ -25,6 +25,9 @@ VARIANTS = {
     "recon_blockheavy": ("recon", {"wave_heavy": 0}),
     "recon_deg": ("recon", {"layout": "degree"}),
     "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
+    "deg_np": ("recon", {"layout": "degree", "pack": 0}),
+    "deg_np_pre": ("pregather", {"layout": "degree", "pack": 0}),
+    "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
