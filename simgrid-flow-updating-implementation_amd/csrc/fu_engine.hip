@@ -358,13 +358,23 @@ __device__ inline T ld_stream(const T *p) {
   return __builtin_nontemporal_load(p);
 }
 
+// Heavy rows (one per wave) up to 64 x max(kHeavyRL, chunk / 64) edges keep their operands
+// in registers (measured on R-MAT-24: 8 or 16 per lane cost more in occupancy than the
+// second pass they save).
+#ifndef FU_HEAVY_RL
+#define FU_HEAVY_RL 4
+#endif
+constexpr int kHeavyRL = FU_HEAVY_RL;
+
 // DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
 //   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
 //   2 = no flow load/store (prices the flow stream);
 //   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
 //   5 = hub chains skipped (prices the exact sequential hub sums);
 //   6 = the flow pass of multi-chunk heavy rows skips its estimate gathers;
-//   12 = 1 and 2 together (prices col + the per-node arrays alone).
+//   12 = 1 and 2 together (prices col + the per-node arrays alone);
+//   kernel 9 only: 20 = staging passes alone, 21 = round tiles alone, 22 = no hub path,
+//   23 = no k_stage, 24 = no k_transpose.
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
@@ -408,7 +418,50 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const double own2 = a_prev2[i];
       double *xs = s_x + w * CH, *es = s_er + w * CH;
       double S = 0.0, T = 0.0;
-      double fo[PL], er[PL];  // the last chunk's operands (a one-chunk row writes its flows from them)
+      constexpr int RL = kHeavyRL > PL ? kHeavyRL : PL;  // whole chunks (TE 2048: PL = 8)
+      if (d <= 64 * RL) {
+        // the whole row in registers (RL elements per lane, all loads in flight at
+        // once): the chain runs chunk by chunk through the wave's LDS quarter and the flows
+        // are written from the same registers, with no second pass over the row
+        double fo[RL], er[RL];
+        int cc[RL];
+#pragma unroll
+        for (int u = 0; u < RL; ++u) {
+          const int k = lane + 64 * u;
+          if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
+          else cc[u] = k < d ? col[b + k] : 0;
+          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+        }
+        if constexpr (!PRE) {
+#pragma unroll
+          for (int u = 0; u < RL; ++u) er[u] = lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+        }
+#pragma unroll
+        for (int c = 0; c < RL / PL; ++c) {
+          if (c * CH < d) {
+            wave_sync();  // the previous chunk's chain is done with the buffer
+#pragma unroll
+            for (int j = 0; j < PL; ++j) {
+              xs[lane + 64 * j] = recon_fr(fo[c * PL + j], er[c * PL + j], own2);
+              es[lane + 64 * j] = er[c * PL + j];
+            }
+            wave_sync();
+            if (DIAG != 5) chain_sum(xs, es, min(CH, d - c * CH), S, T);
+          }
+        }
+        const double a = ((v[i] - S) + T) / (double)(d + 1);
+        if (lane == 0) {
+          st_wt(a_new + i, a);
+          if (pc.width) put_code(pc, code_new, i, a);
+          if (CHECK) eb = err_bits(a, target[i]);
+        }
+#pragma unroll
+        for (int u = 0; u < RL; ++u) {  // flows (CA:117-118)
+          const int k = lane + 64 * u;
+          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
+        }
+      } else {
+      double fo[PL], er[PL];
       for (int c0 = 0; c0 < d; c0 += CH) {
         int cc[PL];
 #pragma unroll
@@ -437,13 +490,6 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         if (pc.width) put_code(pc, code_new, i, a);
         if (CHECK) eb = err_bits(a, target[i]);
       }
-      if (d <= CH) {  // flows (CA:117-118) from the registers that staged the row
-#pragma unroll
-        for (int u = 0; u < PL; ++u) {
-          const int k = lane + 64 * u;
-          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
-        }
-      } else
       for (int k0 = 0; k0 < d; k0 += 4 * 64) {  // flows (CA:117-118), 4 loads in flight per lane
         int cc[4];
         double fo[4], er[4];
@@ -465,6 +511,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
         }
       }
+      }  // rows longer than 64 x kHeavyRL
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -477,11 +524,40 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     // streams the pairs through two LDS halves (the loads of chunk c + 1 in flight while
     // chunk c is summed), with no block barrier and no gather on the chain's path.
     const int i = tl.x, b = tl.z, e = tl.w;
-    const double2 *xy = hubxy + hub_off[blockIdx.x];
+    const double2 *xy = PRE ? nullptr : hubxy + hub_off[blockIdx.x];
     const int d = e - b;
     double S = 0.0, T = 0.0;
     constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
-    if (t < 64) {
+    if (PRE && t < 64) {
+      // kernel 9: the row's estimates are pre-gathered (Gb), so the chain wave streams Gb
+      // and the old flows itself, coalesced, and rebuilds fr as k_hub_stage would
+      const double own2 = a_prev2[i];
+      double nf[PL], ng[PL];
+#pragma unroll
+      for (int u = 0; u < PL; ++u) {
+        const int k = t + 64 * u;
+        nf[u] = k < d ? ld_f(F, b + k) : 0.0;
+        ng[u] = k < d ? Gb[b + k] : 0.0;
+      }
+      for (int c0 = 0; c0 < d; c0 += CH) {
+        double *xs = s_x + ((c0 / CH) & 1) * CH, *es = s_er + ((c0 / CH) & 1) * CH;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          xs[t + 64 * u] = recon_fr(nf[u], ng[u], own2);
+          es[t + 64 * u] = ng[u];
+        }
+        const int c1 = c0 + CH;
+#pragma unroll
+        for (int u = 0; u < PL; ++u) {
+          const int k = c1 + t + 64 * u;
+          nf[u] = k < d ? ld_f(F, b + k) : 0.0;
+          ng[u] = k < d ? Gb[b + k] : 0.0;
+        }
+        wave_sync();
+        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+        wave_sync();
+      }
+    } else if (!PRE && t < 64) {
       double2 nx[PL];
 #pragma unroll
       for (int u = 0; u < PL; ++u) nx[u] = t + 64 * u < d ? xy[t + 64 * u] : make_double2(0.0, 0.0);
@@ -510,7 +586,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
-    if (!hub_sep) {  // else k_hub_flows writes the row's flows with many blocks
+    if (!PRE && !hub_sep) {  // else k_hub_flows writes the row's flows with many blocks
       __syncthreads();
       const double a = s_a[0];
       for (int k = t; k < d; k += kBlock) {
@@ -876,7 +952,7 @@ constexpr int kTrBE = 16384;   // edges per bucket (its values fill 128 KB of LD
 constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
 constexpr int kTrThreads = 1024;
 
-__global__ __launch_bounds__(kTrThreads) void k_transpose(int P, long long E, const int *__restrict__ offT,
+__global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int P, long long E, const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
                                                         double *__restrict__ GB) {
@@ -886,15 +962,15 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int P, long long E, co
   __shared__ int s_c[kTrBE / 64 + 1];
   __shared__ int s_w[kTrThreads / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const long long e0 = (long long)blockIdx.x * kTrBE;
+  const long long e0 = (long long)(b0 + blockIdx.x) * kTrBE;
   const int ne = (int)min((long long)kTrBE, E - e0);
   // runs: thread t owns slices 2t, 2t + 1
   int o[2], len[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int sl = 2 * t + j;
-    o[j] = sl < P ? offT[(long long)blockIdx.x * P + sl] : 0;
-    len[j] = sl < P ? offT[(long long)(blockIdx.x + 1) * P + sl] - o[j] : 0;
+    o[j] = sl < P ? offT[(long long)(b0 + blockIdx.x) * P + sl] : 0;
+    len[j] = sl < P ? offT[(long long)(b0 + blockIdx.x + 1) * P + sl] - o[j] : 0;
   }
   // exclusive scan of len0 + len1 over the block: wave shuffles, then the 16 wave totals
   int x = len[0] + len[1];
@@ -1119,7 +1195,9 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
 // the round's critical path).
 __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__restrict__ hubs, long long total,
                                                       const double2 *__restrict__ hubxy,
-                                                      const double *__restrict__ a_new, double *__restrict__ F) {
+                                                      const double *__restrict__ a_new, double *__restrict__ F,
+                                                      const double *__restrict__ Gb,
+                                                      const double *__restrict__ a_prev2) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
@@ -1130,6 +1208,11 @@ __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__re
   const int4 hb = hubs[lo];
   const int k = hb.y + (int)(q - hb.w);
   const double a = a_new[hb.x];
+  if (Gb) {  // kernel 9: (fr, er) rebuilt from the pre-gathered estimate and the old flow
+    const double er = Gb[k], fo = ld_f(F, k);
+    st_f(F, k, (recon_fr(fo, er, a_prev2[hb.x]) + a) - er, fo);
+    return;
+  }
   const double2 p2 = hubxy[q];
   st_f(F, k, (p2.x + a) - p2.y, ld_f(F, k));
 }
@@ -1419,6 +1502,7 @@ struct fu_handle {
   // kernel 9 (pregather): slice-major G_A, per-bucket run starts, edge-order Gb
   struct TransLayout {
     int P = 0, Q = 0, NB = 0, B = 0;      // slices, blocks per slice, stage blocks, buckets
+    int Bh = 0;                           // buckets [0, Bh) hold the mega-hub rows' edges
     int4 *brange = nullptr;               // stage blocks: {begin, end} in G_A, slice, 0
     unsigned short *colS = nullptr;       // per G_A element: column offset in its slice
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
@@ -1770,14 +1854,12 @@ int ensure_transpose(fu_handle *h) {
     return fail(FU_ERR_GRAPH, h->tr_why);
   }
   const int64_t B = (E + kTrBE - 1) / kTrBE;
-  // mega-hub rows gather directly on the side stream: their edges stay out of G_A
-  std::vector<unsigned char> skip(E, 0);
+  // buckets [0, Bh) hold every mega-hub edge: transposed first, so the hub chains can start
+  int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
-    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub)
-      std::fill(skip.begin() + h->h_rowptr[i], skip.begin() + h->h_rowptr[i + 1], (unsigned char)1);
+    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
   std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < E; ++e)
-    if (!skip[e]) cnt[h->h_col[e] / SN]++;
+  for (int64_t e = 0; e < E; ++e) cnt[h->h_col[e] / SN]++;
   std::vector<int64_t> reg(P + 1, 0);
   for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
   const int64_t total = reg[P];
@@ -1792,7 +1874,6 @@ int ensure_transpose(fu_handle *h) {
     for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
     const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
     for (int64_t e = b * kTrBE; e < e1; ++e) {
-      if (skip[e]) continue;
       const int32_t c = h->h_col[e];
       const int64_t g = cur[c / SN]++;
       colS[g] = (uint16_t)(c % SN);
@@ -1825,6 +1906,7 @@ int ensure_transpose(fu_handle *h) {
   T.Q = (int)Q;
   T.NB = (int)br.size();
   T.B = (int)B;
+  T.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
   h->tr_ready = true;
   return FU_OK;
 }
@@ -1905,29 +1987,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     const double *Gb = pre ? h->tr.GB : nullptr;
     if (pre && !Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
     if (pre) {
-      // the mega hubs' long exact chains do not wait for the two passes: their (fr, er) are
-      // gathered directly and their chains run on the side stream from the round's start
+      // the mega hubs' chains read the pre-gathered estimates too: the buckets holding them
+      // are transposed first, then the chains (and k_hub_flows) run on the side stream
+      // beside the remaining buckets and the other tiles
       const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
       const int4 *tl = h->tiles_geo[1];
-      if (nmega) {
-        HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-        hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl,
-                           (int)(r & 1), h->hubxy, nullptr);
-        if (check)
-          hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2>), dim3(nmega), dim3(kBlock), 0, h->stream2,
-                             tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->code[(r - 1) & 1],
-                             h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, h->hrows, 1, nullptr);
-        else
-          hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 2>), dim3(nmega), dim3(kBlock), 0, h->stream2,
-                             tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, h->code[(r - 1) & 1],
-                             h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off, h->hrows, 1, nullptr);
-        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, h->hubxy, an, F);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
-      }
+#ifdef FU_DIAG
+      const bool hubs = nmega && h->diag != 22;  // 22: timing without the hub path
+#else
+      const bool hubs = nmega;
+#endif
       StageArgs sa{};
       for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
       sa.P[3] = h->tr.P;
@@ -1937,14 +2006,47 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       sa.brange[3] = h->tr.brange;
       sa.colS[3] = h->tr.colS;
       sa.f64 = 1;
+#ifdef FU_DIAG
+      if (h->diag != 21 && h->diag != 23)
+#endif
       hipLaunchKernelGGL(k_stage, dim3(h->tr.NB), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
                          h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA);
-      hipLaunchKernelGGL(k_transpose, dim3(h->tr.B), dim3(kTrThreads), 0, h->stream, h->tr.P, (long long)h->E,
-                         h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
-#define FU_PRE(C)                                                                                         \
+      const int bh = hubs ? h->tr.Bh : 0;
+#ifdef FU_DIAG
+      if (h->diag != 21 && h->diag != 24)
+#endif
+      {
+        if (bh)
+          hipLaunchKernelGGL(k_transpose, dim3(bh), dim3(kTrThreads), 0, h->stream, 0, h->tr.P, (long long)h->E,
+                             h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+        if (hubs) {
+          HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+          HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+        }
+        if (h->tr.B > bh)
+          hipLaunchKernelGGL(k_transpose, dim3(h->tr.B - bh), dim3(kTrThreads), 0, h->stream, bh, h->tr.P,
+                             (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+      }
+      if (hubs) {
+        if (check)
+          hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
+                             h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
+                             1, Gb);
+        else
+          hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
+                             h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
+                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
+                             1, Gb);
+        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
+                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+      }
+#define FU_PRE(C, D)                                                                                      \
   do {                                                                                                    \
     if (nh > nmega)                                                                                       \
-      hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 2, true>), dim3(nh - nmega), dim3(kBlock), 0, \
+      hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 2, true>), dim3(nh - nmega), dim3(kBlock), 0, \
                          h->stream, tl + nmega, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,  \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
                          h->hrows, 1, Gb);                                                                \
@@ -1954,11 +2056,17 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
                          nullptr, 0, Gb);                                                                 \
   } while (0)
-      if (check) FU_PRE(true);
-      else FU_PRE(false);
+#ifdef FU_DIAG
+      if (h->diag == 20) {  // timing: the staging passes alone
+      } else if (h->diag == 5) FU_PRE(false, 5);
+      else if (h->diag == 6) FU_PRE(false, 6);
+      else
+#endif
+      if (check) FU_PRE(true, 0);
+      else FU_PRE(false, 0);
 #undef FU_PRE
       HIP_TRY(hipGetLastError());
-      if (nmega) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+      if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     } else {
     // heavy tiles (hubs, heavy rows) lead the tile list: they run as their own launch on the
     // side stream, concurrently with the light tiles' launch (which then keeps kernel 4's
@@ -2033,7 +2141,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #undef FU_RECON_G
     if (hub_sep)
       hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, h->hubxy, an, F);
+                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr);
     if (fork) {
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(h->ev_join, h->stream2));

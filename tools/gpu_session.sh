@@ -25,6 +25,9 @@ for s in $STEPS; do
     prof)   export TMPDIR=/tmp
             step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOTDIR/bench.py" --cpu-seconds 0 ${BENCH_ARGS:-} ;;
     sweep)  step sweep 900 python tools/sweep.py ${SWEEP_ARGS:-} ;;
+    sweeplibs) for lib in ${SWEEP_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...)
+                 step "sweep_$lib" 600 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so python tools/sweep.py ${SWEEP_ARGS:-}
+               done ;;
     sweepdiag) step sweepdiag 900 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/libfu_diag.so python tools/sweep.py ${SWEEP_ARGS:-} ;;
     replay) step replay 400 python tools/bench_replay.py ;;
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;

@@ -27,6 +27,13 @@ VARIANTS = {
     "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
     "deg_np": ("recon", {"layout": "degree", "pack": 0}),
     "deg_np_pre": ("pregather", {"layout": "degree", "pack": 0}),
+    "pre_d20": ("pregather", {"layout": "degree", "pack": 0, "diag": 20}),
+    "pre_d21": ("pregather", {"layout": "degree", "pack": 0, "diag": 21}),
+    "pre_d22": ("pregather", {"layout": "degree", "pack": 0, "diag": 22}),
+    "pre_d23": ("pregather", {"layout": "degree", "pack": 0, "diag": 23}),
+    "pre_d24": ("pregather", {"layout": "degree", "pack": 0, "diag": 24}),
+    "pre_d5": ("pregather", {"layout": "degree", "pack": 0, "diag": 5}),
+    "pre_d6": ("pregather", {"layout": "degree", "pack": 0, "diag": 6}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
