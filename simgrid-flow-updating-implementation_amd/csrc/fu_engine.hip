@@ -322,7 +322,10 @@ __device__ inline void wave_sync() {
 // one fp64 add per element advances both sums: a wave64 v_add_f64 occupies the SIMD for the
 // same cycles whatever the EXEC mask, and two separate chains cost two. The LDS reads of
 // the next B elements are issued before the dependent adds of the current B (B = 16: the adds
-// of one batch cover the LDS latency of the next).
+// of one batch cover the LDS latency of the next), into two register batches used in turn
+// (no register copies: those cost two more VALU instructions per element). The caller
+// keeps xs and es in different LDS banks (es = xs + 8 TE + 8 bytes in the tiles), so the
+// two addresses of one read do not conflict.
 #ifndef FU_CHAIN_B
 #define FU_CHAIN_B 16  // measured: 8 -> 8.75, 16 -> 7.2, 32 -> 6.4 ns per element (32 costs registers)
 #endif
@@ -333,20 +336,32 @@ __device__ __forceinline__ void chain_sum(const double *xs, const double *es, in
   double acc = odd ? T : S;
   int q = 0;
   if (cn >= B) {
-    double a[B];
+    double a[B], c[B];
 #pragma unroll
     for (int k = 0; k < B; ++k) a[k] = src[k];
-    for (q = B; q + B <= cn; q += B) {
-      double a2[B];
+    q = B;
+    for (;;) {
+      if (q + B > cn) {
 #pragma unroll
-      for (int k = 0; k < B; ++k) a2[k] = src[q + k];
+        for (int k = 0; k < B; ++k) acc = acc + a[k];
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) c[k] = src[q + k];
 #pragma unroll
       for (int k = 0; k < B; ++k) acc = acc + a[k];
+      q += B;
+      if (q + B > cn) {
 #pragma unroll
-      for (int k = 0; k < B; ++k) a[k] = a2[k];
+        for (int k = 0; k < B; ++k) acc = acc + c[k];
+        break;
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) a[k] = src[q + k];
+#pragma unroll
+      for (int k = 0; k < B; ++k) acc = acc + c[k];
+      q += B;
     }
-#pragma unroll
-    for (int k = 0; k < B; ++k) acc = acc + a[k];
   }
   for (; q < cn; ++q) acc = acc + src[q];
   S = __shfl(acc, 0);
@@ -393,7 +408,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
   __shared__ double s_x[TE];   // f_{r-2} on load, fr after phase B
-  __shared__ double s_er[TE];  // a_{r-1}[col e]
+  __shared__ double s_er_buf[TE + 2];  // a_{r-1}[col e], one double off s_x's banks
+  double *const s_er = s_er_buf + 1;
   __shared__ unsigned char s_own[TE];
   __shared__ int s_rp[TN + 1];
   __shared__ double s_a[TN];
