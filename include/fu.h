@@ -103,23 +103,24 @@ int fu_create_from_graph(const fu_graph *g, const double *value, int32_t device,
  * targets, estimates and flows stay in the caller's numbering: the handle maps them. */
 int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t device,
                             int32_t layout, fu_handle **out);
-/* Options: "kernel" (0 = auto = 4, 1 = thread-per-node, 2 = LDS tile (pull), 3 = push/inbox,
- *          4 = LDS tile with flow reconstruction, 5 = 4 with a column-split gather launch,
- *          6 = 4 with the low half of each row staged by a gather launch
- *          (rows must be sorted by neighbour id), 7 = 4 with one tile per wave,
- *          8 = LDS-staged slices: a stage launch turns the estimate gather into streams,
- *          9 = persistent software-pipelined tiles, 10 = 9 reading 8's staged estimates),
- * "hub_threshold" (degree above which a node gets a block; default 64),
- * "nt" (1 = non-temporal loads/stores for the streamed arrays of kernel 4; default 0),
- * "pack" (kernel 4: gather lossless 8/16/32-bit codes of the estimates once they have
- *          converged into a narrow cluster; default 1), "pack_every" (rounds between
- *          encoding plans; default 16), "bins" (degree bins for kernel 4's heavy rows),
- * "mega_hub" (kernel 4: degree above which a row's (fr, er) pairs are staged by many blocks;
- *          default 8192), "hub_scan" (mega hubs: 1 = parallel exact left-to-right sums,
- *          speculated per binade and verified; 0 = one wave's sequential chain, default),
- * "wave_heavy" (kernel 4: rows above hub_threshold one per wave (1, default) or per block),
- * "pipe_bpc" (kernels 9/10: persistent blocks per CU; default 4), "stage_layout" (kernels
- *          8/10, tests: -1 = by packing width, 0..3 = slice layout of 1/2/4/8-byte elements). */
+/* Options (fu_set_option; FU_ERR_ARG for an unknown key or value):
+ * "kernel"        0 = auto (fu_tune / autotuned between rounds), 4 = recon (LDS tiles, flow
+ *                 reconstruction, direct estimate gathers), 8 = stage (estimates staged slice
+ *                 by slice through LDS; single GPU, needs a slice layout), 9 = pregather
+ *                 (stage + per-bucket transpose into edge order; single GPU, <= 2^25 nodes).
+ *                 Partitioned (fu_dist_*) handles run kernel 4. All kernels are bitwise equal.
+ * "tile_edges"    kernel 4 tile edges: 2048, 1024 (default) or 512; "tile_nodes" 0/128/256.
+ * "hub_threshold" rows of higher degree run as heavy rows, one wave each (default 128).
+ * "mega_hub"      rows of higher degree run as mega hubs: one chain-only block each, their
+ *                 (fr, er) staged by many blocks (default 8192).
+ * "wave_heavy"    heavy rows one per wave (1, default) or one per block (0).
+ * "fork_heavy"    kernel 4: heavy tiles on a side stream beside the light tiles (default 1).
+ * "split_hubs"    kernel 4: only the mega-hub tiles on the side stream (default 1).
+ * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).
+ * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster
+ *                 (default 1); "pack_every" rounds between encoding plans (default 16).
+ * "stage_layout"  kernel 8, tests: -1 = by packing width, 0..3 = the 1/2/4/8-byte layout.
+ * Timing-only ablations ("diag") exist only in a -DFU_DIAG build (tools/). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);

@@ -1453,7 +1453,7 @@ struct fu_handle {
   int64_t rounds = 0;
   int kernel = 4;        // 4 = recon (LDS tiles), 8 = stage (LDS-staged slices + recon tiles)
   int geo = 1;           // kernel 4 tile geometry (kGeoEdges x kGeoNodes)
-  int hub_threshold = 64;
+  int hub_threshold = 128;  // rows above it run as heavy rows (R-MAT-24: 128 beat 64, 256, 512)
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
@@ -1563,12 +1563,16 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     int64_t eb = h->h_rowptr[b];
     while (i < n && i - b < tn) {
       int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
-      if (di > h->hub_threshold || di > te) break;
+      if (di > h->hub_threshold || di > te || di > h->mega_hub) break;  // (mega_hub may be < hub_threshold)
       if (h->h_rowptr[i + 1] - eb > te) break;
       ++i;
     }
     light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
   }
+  // every mega hub must lead the list: its tile index is its hub_off / hubxy slot
+  int64_t n_mega = 0;
+  for (int32_t r = 0; r < n; ++r) n_mega += h->h_rowptr[r + 1] - h->h_rowptr[r] > h->mega_hub;
+  if ((int64_t)hubs.size() != n_mega) return fail(FU_ERR_STATE, "build_tiles: a mega hub fell into a light tile");
   // mega hubs, then heavy tiles first so their long sequential chains start early
   std::vector<int4> all(hubs);
   if (h->wave_heavy && !heavy.empty()) {

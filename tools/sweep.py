@@ -34,6 +34,11 @@ VARIANTS = {
     "pre_d24": ("pregather", {"layout": "degree", "pack": 0, "diag": 24}),
     "pre_d5": ("pregather", {"layout": "degree", "pack": 0, "diag": 5}),
     "pre_d6": ("pregather", {"layout": "degree", "pack": 0, "diag": 6}),
+    "pre_ht128": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
+    "pre_ht256": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
+    "pre_ht512": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 512}),
+    "deg_np_ht128": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
+    "deg_np_ht256": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
