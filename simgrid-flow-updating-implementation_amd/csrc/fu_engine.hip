@@ -964,29 +964,40 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
 // beside the flows. Bytes per edge: stage 2 + 8, transpose 8 + 2 + 8, round 8 (instead of
 // col 4 + one random 8-byte gather).
 // ------------------------------------------------------------------------------------
-constexpr int kTrBE = 16384;   // edges per bucket (its values fill 128 KB of LDS)
+#ifndef FU_TR_BE
+#define FU_TR_BE 8192
+#endif
+constexpr int kTrBE = FU_TR_BE;  // edges per bucket (8K: 76 KB of LDS, two blocks per CU; R-MAT-24 7.78 -> 7.59 ms vs 16K)
+static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 positions, coarse table");
 constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
 constexpr int kTrThreads = 1024;
 
-__global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int P, long long E, const int *__restrict__ offT,
+__global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P, long long E,
+                                                        const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
                                                         double *__restrict__ GB) {
   __shared__ double s_v[kTrBE];
-  __shared__ int s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
+  __shared__ unsigned short s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
   __shared__ int s_o[kTrMaxP];      // G_A index of each run
   __shared__ int s_c[kTrBE / 64 + 1];
   __shared__ int s_w[kTrThreads / 64];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const long long e0 = (long long)(b0 + blockIdx.x) * kTrBE;
+  // XCD-contiguous buckets (block b runs on XCD b % 8): a G_A line that ends one bucket's
+  // run and starts the next bucket's is fetched into one L2, not two
+  const int per = (nbk + 7) >> 3;
+  const int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  if (bk >= nbk) return;
+  const int bb = b0 + bk;
+  const long long e0 = (long long)bb * kTrBE;
   const int ne = (int)min((long long)kTrBE, E - e0);
   // runs: thread t owns slices 2t, 2t + 1
   int o[2], len[2];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int sl = 2 * t + j;
-    o[j] = sl < P ? offT[(long long)(b0 + blockIdx.x) * P + sl] : 0;
-    len[j] = sl < P ? offT[(long long)(b0 + blockIdx.x + 1) * P + sl] - o[j] : 0;
+    o[j] = sl < P ? offT[(long long)bb * P + sl] : 0;
+    len[j] = sl < P ? offT[(long long)(bb + 1) * P + sl] - o[j] : 0;
   }
   // exclusive scan of len0 + len1 over the block: wave shuffles, then the 16 wave totals
   int x = len[0] + len[1];
@@ -2037,15 +2048,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #endif
       {
         if (bh)
-          hipLaunchKernelGGL(k_transpose, dim3(bh), dim3(kTrThreads), 0, h->stream, 0, h->tr.P, (long long)h->E,
+          hipLaunchKernelGGL(k_transpose, dim3(8 * ((bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
+                             (long long)h->E,
                              h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
         if (hubs) {
           HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
           HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
         }
         if (h->tr.B > bh)
-          hipLaunchKernelGGL(k_transpose, dim3(h->tr.B - bh), dim3(kTrThreads), 0, h->stream, bh, h->tr.P,
-                             (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+          hipLaunchKernelGGL(k_transpose, dim3(8 * ((h->tr.B - bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, bh,
+                             h->tr.B - bh, h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
       }
       if (hubs) {
         if (check)
