@@ -477,20 +477,28 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
         }
       } else {
-      double fo[PL], er[PL];
-      for (int c0 = 0; c0 < d; c0 += CH) {
-        int cc[PL];
+      // longer rows: chunk by chunk, the next chunk's loads in flight during this chunk's
+      // chain; the flows in a second pass
+      double fo[PL], er[PL], nf[PL], ng[PL];
+      int nc[PL];
+      auto fetch = [&](int c0) {
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
           const int k = c0 + lane + 64 * u;
-          if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
-          else cc[u] = k < d ? col[b + k] : 0;
-          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+          if constexpr (PRE) ng[u] = k < d ? Gb[b + k] : 0.0;
+          else nc[u] = k < d ? col[b + k] : 0;
+          nf[u] = k < d ? ld_f(F, b + k) : 0.0;
         }
-        if constexpr (!PRE) {
+      };
+      fetch(0);
+      for (int c0 = 0; c0 < d; c0 += CH) {
 #pragma unroll
-          for (int u = 0; u < PL; ++u) er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
+        for (int u = 0; u < PL; ++u) {
+          fo[u] = nf[u];
+          if constexpr (PRE) er[u] = ng[u];
+          else er[u] = c0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, nc[u]) : 0.0;
         }
+        if (c0 + CH < d) fetch(c0 + CH);
         wave_sync();  // the previous chunk's chain is done with the buffer
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
@@ -506,11 +514,11 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         if (pc.width) put_code(pc, code_new, i, a);
         if (CHECK) eb = err_bits(a, target[i]);
       }
-      for (int k0 = 0; k0 < d; k0 += 4 * 64) {  // flows (CA:117-118), 4 loads in flight per lane
-        int cc[4];
-        double fo[4], er[4];
+      for (int k0 = 0; k0 < d; k0 += 8 * 64) {  // flows (CA:117-118), 8 loads in flight per lane
+        int cc[8];
+        double fo[8], er[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const int k = k0 + lane + 64 * u;
           if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
           else cc[u] = k < d ? col[b + k] : 0;
@@ -518,11 +526,11 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
         }
         if constexpr (!PRE) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
+          for (int u = 0; u < 8; ++u)
             er[u] = k0 + lane + 64 * u < d ? (DIAG == 6 ? 0.0 : ld_est(pp, code_prev, a_prev, cc[u])) : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < 8; ++u) {
           const int k = k0 + lane + 64 * u;
           if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
         }
