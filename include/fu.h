@@ -151,14 +151,14 @@ int fu_get_flows(fu_handle *h, double *f_out);
 int fu_get_round(fu_handle *h, int64_t *rounds_done);
 /* info[0] = kernel in use, [1] = nt, [2] = autotune (0 off, 1 pending, 2 done),
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
- * passes, [7] = packing width of the last pass, [8..13] = the last pass's ns per round for
- * its candidates (4, 4 at 512x64, 6, 8, 10, 4 at 1024x128; 0 = not run), [20] = mega hubs, [21] = their
- * pieces, [22] = pieces the exact-sum serial pass redid element by element (cumulative;
- * synchronises), [23..26] = the autotune winner per packing width 0, 8, 16, 32 (kernel * 10 +
- * kernel-4 geometry index, -1 = not tuned yet). With kernel
- * "auto" (the default) a fu_run_collectall(_timed) with >= 45 rounds left after round 0
- * times the candidates on real rounds (they share state and are bitwise identical) and keeps
- * the fastest; the pass re-runs (at most 4 times) when the packing plan changes width. */
+ * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
+ * its candidates (kernel 4 at 2048x256, kernel 4 at 512x64, kernel 8, kernel 4 at
+ * 1024x128, kernel 9; 0 = not run), [20] = mega hubs, [23..26] = the autotune winner per
+ * packing width 0, 8, 16, 32 (kernel * 10 + kernel-4 geometry index, -1 = not tuned yet),
+ * [27..30] = kernel 8 slices per layout (element bytes 1, 2, 4, 8; 0 = not built).
+ * With kernel "auto" (the default) fu_tune, or a run with enough rounds left, times the
+ * candidates on real rounds (they share state and are bitwise identical) and keeps the
+ * fastest; the pass re-runs when the packing plan changes width. */
 int fu_get_info(fu_handle *h, int64_t info[32]);  /* ABI 2: 32 entries */
 /* Packed estimate table widths (0 = doubles): [0]/[1] = the code tables of the last
  * even/odd round, [2] = the current encoding plan (synchronises). */

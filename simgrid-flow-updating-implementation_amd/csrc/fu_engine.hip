@@ -2781,7 +2781,7 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   info[5] = kGeoNodes[h->geo];
   info[6] = h->n_tunes;
   info[7] = h->tuned_width;
-  for (int k = 0; k < kNCands; ++k) info[8 + k] = (int64_t)(h->tune_ms[k] * 1e3f);  // ns per round
+  for (int k = 0; k < kNCands; ++k) info[8 + k] = (int64_t)((double)h->tune_ms[k] * 1e6);  // ns per round
   info[20] = h->n_hub;
   for (int k = 0; k < 4; ++k)  // autotune winner per packing width 0, 8, 16, 32 (kernel * 10 + geometry; -1 = none)
     info[23 + k] = h->tune_cache[k] < 0 ? -1 : kCands[h->tune_cache[k]].kernel * 10 + kCands[h->tune_cache[k]].geo;
