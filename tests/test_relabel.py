@@ -61,7 +61,7 @@ def test_relabelled_rounds_are_bitwise_the_same():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kernel", ["auto", "recon", "stage"])
+@pytest.mark.parametrize("kernel", ["auto", "recon", "stage", "pregather"])
 def test_gpu_degree_layout_matches_oracle(kernel):
     g = fu.Graph.rmat(14, 16, seed=3)
     v = fu.uniform_values(g.n, seed=3)
