@@ -1543,15 +1543,8 @@ struct fu_handle {
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
     int *offT = nullptr;                  // (B + 1) x P: G_A index where bucket b's run of slice s starts
     double *GA = nullptr, *GB = nullptr;
-    // pipelined round: chunk j transposes buckets [ck_b[j], ck_b[j + 1]) and then (stream3)
-    // runs tiles [ck_t[j], ck_t[j + 1]) of geometry 1, which read no later bucket
-    std::vector<int> ck_b, ck_t;
-    std::vector<hipEvent_t> ck_ev;
   };
   TransLayout tr;
-  hipStream_t stream3 = nullptr;          // kernel 9: the round's tiles, chunk by chunk
-  hipEvent_t ev_r3 = nullptr;
-  int64_t pg_chunk = 16 << 20;            // kernel 9: edges per pipelined chunk (0 = one chunk)
   bool tr_ready = false;
   std::string tr_why;
   int n_cu = 256;
@@ -1885,8 +1878,6 @@ void free_transpose(fu_handle *h) {
   auto &T = h->tr;
   for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA, (void *)T.GB})
     if (p) hipFree(p);
-  for (hipEvent_t e : T.ck_ev)
-    if (e) hipEventDestroy(e);
   T = fu_handle::TransLayout{};
   h->tr_ready = false;
 }
@@ -1955,41 +1946,6 @@ int ensure_transpose(fu_handle *h) {
   T.NB = (int)br.size();
   T.B = (int)B;
   T.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
-  // chunks: tile t (after the mega hubs) needs the buckets up to its last edge; chunk j is
-  // the run of tiles whose running need fits the first j + 1 chunks of buckets
-  {
-    const int nt = h->ntiles_geo[1], t0 = h->n_hub;
-    std::vector<int4> tl(nt);
-    if (nt) HIP_TRY(hipMemcpy(tl.data(), h->tiles_geo[1], sizeof(int4) * nt, hipMemcpyDeviceToHost));
-    const int64_t cb = h->pg_chunk > 0 ? std::max<int64_t>(1, h->pg_chunk / kTrBE) : B;
-    const int K = (int)std::max<int64_t>(1, (B - T.Bh + cb - 1) / cb);
-    T.ck_b.assign(K + 1, 0);
-    for (int j = 0; j <= K; ++j) T.ck_b[j] = (int)std::min<int64_t>(B, T.Bh + (int64_t)j * cb);
-    T.ck_b[K] = (int)B;
-    T.ck_t.assign(K + 1, nt);
-    T.ck_t[0] = t0;
-    int64_t need = 0;
-    int j = 0;
-    for (int t = t0; t < nt; ++t) {
-      const int4 q = tl[t];
-      int64_t last = q.w;  // light and block-heavy tiles: {.., .., first edge, end edge}
-      if (q.y == -4) {
-        last = 0;
-        for (int k = 0; k < q.z; ++k) last = std::max<int64_t>(last, h->h_rowptr[h->h_hrows[q.x + k] + 1]);
-      }
-      need = std::max(need, (last + kTrBE - 1) / kTrBE);
-      while (j < K && T.ck_b[j + 1] < need) T.ck_t[++j] = t;
-    }
-    while (j < K) T.ck_t[++j] = nt;
-    T.ck_ev.assign(K, nullptr);
-    for (auto &e : T.ck_ev)
-      if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return fail(FU_ERR_HIP, "hipEventCreate failed");
-    if (!h->stream3) {
-      if (hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess ||
-          hipEventCreateWithFlags(&h->ev_r3, hipEventDisableTiming) != hipSuccess)
-        return fail(FU_ERR_HIP, "hipStreamCreate failed");
-    }
-  }
   h->tr_ready = true;
   return FU_OK;
 }
@@ -2073,7 +2029,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       // the mega hubs' chains read the pre-gathered estimates too: the buckets holding them
       // are transposed first, then the chains (and k_hub_flows) run on the side stream
       // beside the remaining buckets and the other tiles
-      const int nmega = h->n_hub;
+      const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
       const int4 *tl = h->tiles_geo[1];
 #ifdef FU_DIAG
       const bool hubs = nmega && h->diag != 22;  // 22: timing without the hub path
@@ -2094,21 +2050,24 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #endif
       hipLaunchKernelGGL(k_stage, dim3(h->tr.NB), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
                          h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA);
-      const auto &TL = h->tr;
+      const int bh = hubs ? h->tr.Bh : 0;
 #ifdef FU_DIAG
-      const bool do_tr = h->diag != 21 && h->diag != 24, do_tiles = h->diag != 20;
-#else
-      const bool do_tr = true, do_tiles = true;
+      if (h->diag != 21 && h->diag != 24)
 #endif
-      auto transpose = [&](int b0, int b1) {
-        if (do_tr && b1 > b0)
-          hipLaunchKernelGGL(k_transpose, dim3(8 * ((b1 - b0 + 7) / 8)), dim3(kTrThreads), 0, h->stream, b0, b1 - b0,
-                             TL.P, (long long)h->E, TL.offT, TL.GA, TL.pos16, TL.GB);
-      };
-      transpose(0, TL.Bh);  // the buckets holding the mega hubs' edges first
+      {
+        if (bh)
+          hipLaunchKernelGGL(k_transpose, dim3(8 * ((bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
+                             (long long)h->E,
+                             h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+        if (hubs) {
+          HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+          HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+        }
+        if (h->tr.B > bh)
+          hipLaunchKernelGGL(k_transpose, dim3(8 * ((h->tr.B - bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, bh,
+                             h->tr.B - bh, h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+      }
       if (hubs) {
-        HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
         if (check)
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
                              h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
@@ -2124,32 +2083,28 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
       }
-      // the other buckets chunk by chunk on the main stream; each chunk's tiles (which read
-      // no later bucket) on stream3 as soon as it is transposed, beside the next chunks, so
-      // G_B is read back while the lines are still on the die
-#define FU_PRE(C, D, t0, t1)                                                                              \
-  hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 0, true>), dim3((t1) - (t0)), dim3(kBlock), 0,   \
-                     h->stream3, tl + (t0), h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,     \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,       \
-                     h->hrows, 1, Gb)
-      const int K = (int)TL.ck_ev.size();
-      for (int j = 0; j < K; ++j) {
-        transpose(TL.ck_b[j], TL.ck_b[j + 1]);
-        const int t0 = TL.ck_t[j], t1 = TL.ck_t[j + 1];
-        if (t1 <= t0 || !do_tiles) continue;
-        HIP_TRY(hipEventRecord(TL.ck_ev[j], h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->stream3, TL.ck_ev[j], 0));
+#define FU_PRE(C, D)                                                                                      \
+  do {                                                                                                    \
+    if (nh > nmega)                                                                                       \
+      hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 2, true>), dim3(nh - nmega), dim3(kBlock), 0, \
+                         h->stream, tl + nmega, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,  \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
+                         h->hrows, 1, Gb);                                                                \
+    if (nl)                                                                                               \
+      hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, h->stream, \
+                         tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
+                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
+                         nullptr, 0, Gb);                                                                 \
+  } while (0)
 #ifdef FU_DIAG
-        if (h->diag == 5) FU_PRE(false, 5, t0, t1);
-        else if (h->diag == 6) FU_PRE(false, 6, t0, t1);
-        else
+      if (h->diag == 20) {  // timing: the staging passes alone
+      } else if (h->diag == 5) FU_PRE(false, 5);
+      else if (h->diag == 6) FU_PRE(false, 6);
+      else
 #endif
-        if (check) FU_PRE(true, 0, t0, t1);
-        else FU_PRE(false, 0, t0, t1);
-      }
+      if (check) FU_PRE(true, 0);
+      else FU_PRE(false, 0);
 #undef FU_PRE
-      HIP_TRY(hipEventRecord(h->ev_r3, h->stream3));
-      HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_r3, 0));
       HIP_TRY(hipGetLastError());
       if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     } else {
@@ -2511,12 +2466,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->fork_heavy = value != 0;
     return FU_OK;
   }
-  if (!std::strcmp(key, "pg_chunk")) {  // kernel 9: edges per pipelined chunk (0 = one chunk)
-    if (value < 0) return fail(FU_ERR_ARG, "fu_set_option: pg_chunk must be >= 0");
-    h->pg_chunk = value;
-    free_transpose(h);
-    return FU_OK;
-  }
   if (!std::strcmp(key, "split_hubs")) {  // kernel 4: mega-hub tiles alone on the side stream (1)
     h->split_hubs = value != 0;
     return FU_OK;
@@ -2871,7 +2820,6 @@ int fu_destroy(fu_handle *h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
-  if (h->stream3) hipStreamSynchronize(h->stream3);
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
@@ -2893,8 +2841,6 @@ int fu_destroy(fu_handle *h) {
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
-  if (h->ev_r3) hipEventDestroy(h->ev_r3);
-  if (h->stream3) hipStreamDestroy(h->stream3);
   delete h;
   return FU_OK;
 }

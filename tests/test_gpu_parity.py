@@ -486,18 +486,15 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("chunk", [0, 16384, 100000])
 @pytest.mark.parametrize("mega", [100, 1000])
-def test_pregather_degree_layout_hub_buckets_first(mega, chunk):
+def test_pregather_degree_layout_hub_buckets_first(mega):
     """Kernel 9 under the degree layout: the mega hubs are the first rows, so their buckets
     are transposed first and their chains (reading the pre-gathered estimates and the old
-    flows) and k_hub_flows overlap the other buckets' transpose and the other tiles; the
-    tiles run chunk by chunk behind the transpose (pg_chunk edges per chunk, 0 = one)."""
+    flows) and k_hub_flows overlap the other buckets' transpose and the other tiles."""
     g = fu.Graph.rmat(15, 16, seed=21)
     v = fu.uniform_values(g.n, seed=21)
     eng = fu.CollectAll(g, v, kernel="pregather", layout="degree")
     eng.set_option("mega_hub", mega)
-    eng.set_option("pg_chunk", chunk)
     assert eng.info()["mega_hubs"] > 0
     eng.run(40)
     a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 40, nthreads=16)

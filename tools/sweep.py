@@ -39,10 +39,6 @@ VARIANTS = {
     "pre_ht512": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 512}),
     "deg_np_ht128": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
     "deg_np_ht256": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
-    "pre_ck0": ("pregather", {"layout": "degree", "pack": 0, "pg_chunk": 0}),
-    "pre_ck8m": ("pregather", {"layout": "degree", "pack": 0, "pg_chunk": 8 << 20}),
-    "pre_ck32m": ("pregather", {"layout": "degree", "pack": 0, "pg_chunk": 32 << 20}),
-    "pre_ck64m": ("pregather", {"layout": "degree", "pack": 0, "pg_chunk": 64 << 20}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
