@@ -233,7 +233,9 @@ int fu_replay_run(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t 
 int fu_replay_run_timed(fu_replay *r, int32_t tick_end, float *ms);
 int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est);
 /* "persistent" = 1: one launch for all ticks in dataflow order (per-node event streams,
- * unique message slots tagged by a sentinel); 0 = one launch per tick (default). Same bits. */
+ * unique message slots tagged by a sentinel); 0 = one launch per tick (default). Same bits.
+ * "persistent_reg" = 1 (default): in persistent mode, when every node's thread can be
+ * resident and the degree is <= 16, each thread keeps its node's state in registers. */
 int fu_replay_set_option(fu_replay *r, const char *key, int64_t value);
 int fu_replay_destroy(fu_replay *r);
 

@@ -1428,6 +1428,125 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 }
 
 
+// k_replay_persist with one node per thread and the node's state (its row of flows and
+// estimate caches, cursor, snapshot cursor, last average) kept in registers for the whole
+// run (degree <= MAXD): an event costs its own loads (event, tick, and for a receive the
+// payload) instead of also re-reading the node's state from memory on every pass. Same
+// event semantics and order as k_replay_persist; a blocked receive leaves the event loop
+// and is retried on the next pass (no lane spins on another lane of its wave).
+template <int MAXD>
+__global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
+    int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_ev,
+    const int *__restrict__ node_tick, const int *__restrict__ out_uid,
+    const long long *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ flow,
+    double *__restrict__ est, double *__restrict__ last, unsigned long long *__restrict__ pay,
+    long long *__restrict__ cursor, int *__restrict__ scur, int n_snap,
+    const int *__restrict__ snap_ticks, double *__restrict__ snaps, int *__restrict__ status,
+    long long max_iters) {
+  const int node = blockIdx.x * kBlock + threadIdx.x;
+  if (node >= n) return;
+  long long p = cursor[node];
+  const long long pe = node_off[node + 1];
+  int sc = scur[node];
+  const long long rb = rowptr[node];
+  const int deg = (int)(rowptr[node + 1] - rb);
+  double fl[MAXD], es[MAXD];
+#pragma unroll
+  for (int j = 0; j < MAXD; ++j) {
+    fl[j] = j < deg ? flow[rb + j] : 0.0;
+    es[j] = j < deg ? est[rb + j] : 0.0;
+  }
+  const double val = v[node];
+  double lst = last[node];
+  long long it = 0;
+  bool done = false;
+  while (!done) {
+    bool progressed = false;
+    while (p < pe) {
+      const int tk = node_tick[p];
+      if (tk >= tick_end) break;
+      while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
+      const int4 ev = node_ev[p];
+      if (ev.x == FU_EV_RECV) {
+        const unsigned long long fx = ld_tag(pay + 2 * (long long)ev.z);
+        const unsigned long long fy = ld_tag(pay + 2 * (long long)ev.z + 1);
+        if (fx == kMsgSentinel || fy == kMsgSentinel) break;  // not sent yet: retry next pass
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j)
+          if (j == ev.y) {
+            es[j] = __longlong_as_double((long long)fy);
+            fl[j] = -__longlong_as_double((long long)fx);
+          }
+      } else if (ev.x == FU_EV_FIRE_CA) {
+        const int k = ev.y;
+        double S = 0.0, T = 0.0;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j)
+          if (j < k) S = S + fl[j];
+        const double estimate = val - S;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j)
+          if (j < k) T = T + es[j];
+        const double avg = (estimate + T) / (double)(k + 1);
+        lst = avg;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j)
+          if (j < k) {
+            const double nf = (fl[j] + avg) - es[j];
+            fl[j] = nf;
+            es[j] = avg;
+            const long long m = out_uid[ev.z + j];
+            st_tag(pay + 2 * m, nf);
+            st_tag(pay + 2 * m + 1, avg);
+          }
+      } else {
+        const int sl = ev.y, k = ev.z;
+        double S = 0.0, fs = 0.0, esl = 0.0;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j) {
+          if (j < k) S = S + fl[j];
+          if (j == sl) {
+            fs = fl[j];
+            esl = es[j];
+          }
+        }
+        const double estimate = val - S;
+        const double avg = (esl + estimate) / 2.0;
+        lst = avg;
+        const double nf = (fs + avg) - esl;
+#pragma unroll
+        for (int j = 0; j < MAXD; ++j)
+          if (j == sl) {
+            fl[j] = nf;
+            es[j] = avg;
+          }
+        st_tag(pay + 2 * (long long)ev.w, nf);
+        st_tag(pay + 2 * (long long)ev.w + 1, avg);
+      }
+      ++p;
+      progressed = true;
+    }
+    done = p == pe || node_tick[p] >= tick_end;
+    if (!done && !progressed) __builtin_amdgcn_s_sleep(2);
+    if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
+      atomicExch(status, 1);
+      break;
+    }
+  }
+  if (done)
+    while (sc < n_snap && snap_ticks[sc] < tick_end) snaps[(long long)sc++ * n + node] = lst;
+#pragma unroll
+  for (int j = 0; j < MAXD; ++j)
+    if (j < deg) {
+      flow[rb + j] = fl[j];
+      est[rb + j] = es[j];
+    }
+  cursor[node] = p;
+  scur[node] = sc;
+  last[node] = lst;
+}
+
+
 template <typename T>
 int dmalloc(T **p, size_t count) {
   if (count == 0) count = 1;
@@ -2869,7 +2988,11 @@ struct fu_replay {
   unsigned long long *pay = nullptr;
   int64_t n_uid = 0;
   bool pers_ready = false;
+  int64_t max_deg = 0;
+  int pers_reg = 1;       // option "persistent_reg": one node per thread, state in registers
+  bool reg_ok = false;    // degree <= kReplayRegDeg and every node's thread resident at once
 };
+constexpr int kReplayRegDeg = 16;
 
 static int replay_build_persistent(fu_replay *r) {
   if (r->pers_ready) return FU_OK;
@@ -2937,6 +3060,12 @@ static int replay_build_persistent(fu_replay *r) {
   // stay below the occupancy bound (the API can over-report by one block per CU)
   const long long cap = std::max(1LL, (long long)std::max(1, per_cu - 1) * ncu);
   r->pers_blocks = (unsigned)std::min<long long>(cap, grid_for(r->n));
+  // the register variant needs one resident thread per node (a node's blocked receive is
+  // retried by its own thread only)
+  int per_cu_reg = 0;
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, k_replay_persist_reg<kReplayRegDeg>, kBlock, 0));
+  const long long cap_reg = (long long)std::max(0, per_cu_reg - 1) * ncu;
+  r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg;
   r->pers_ready = true;
   return FU_OK;
 }
@@ -2979,6 +3108,7 @@ int fu_replay_create(int32_t n, const int64_t *rowptr, const double *value, int3
   r->ticks = ticks;
   r->E = E;
   r->n_msgs = n_msgs;
+  for (int32_t i = 0; i < n; ++i) r->max_deg = std::max<int64_t>(r->max_deg, rowptr[i + 1] - rowptr[i]);
   r->h_tto.assign(tick_task_off, tick_task_off + ticks + 1);
   r->h_tasks.assign(tasks, tasks + 3 * n_tasks);
   r->h_events.assign(events, events + 4 * n_events);
@@ -3037,10 +3167,16 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
     }
     HIP_TRY(hipMemsetAsync(r->scur, 0, sizeof(int) * r->n, r->stream));
     HIP_TRY(hipMemsetAsync(r->status, 0, sizeof(int), r->stream));
-    hipLaunchKernelGGL(k_replay_persist, dim3(r->pers_blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
-                       r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v, r->flow,
-                       r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
-                       (long long)1 << 22);
+    if (r->reg_ok && r->pers_reg)
+      hipLaunchKernelGGL(k_replay_persist_reg<kReplayRegDeg>, dim3(grid_for(r->n)), dim3(kBlock), 0, r->stream,
+                         r->n, tick_end, r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v,
+                         r->flow, r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
+                         (long long)1 << 22);
+    else
+      hipLaunchKernelGGL(k_replay_persist, dim3(r->pers_blocks), dim3(kBlock), 0, r->stream, r->n, tick_end,
+                         r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v, r->flow,
+                         r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
+                         (long long)1 << 22);
     HIP_TRY(hipGetLastError());
     int st = 0;
     HIP_TRY(hipMemcpyAsync(&st, r->status, sizeof(int), hipMemcpyDeviceToHost, r->stream));
@@ -3123,6 +3259,10 @@ int fu_replay_set_option(fu_replay *r, const char *key, int64_t value) {
     // build the per-node event lists now, so that no host work lands inside a timed run
     HIP_TRY(hipSetDevice(r->device));
     return replay_build_persistent(r);
+  }
+  if (!std::strcmp(key, "persistent_reg")) {  // persistent mode: node state in registers (1, default)
+    r->pers_reg = value != 0;
+    return FU_OK;
   }
   return fail(FU_ERR_ARG, std::string("fu_replay_set_option: unknown key '") + key + "'");
 }

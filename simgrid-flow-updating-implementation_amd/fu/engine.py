@@ -259,7 +259,8 @@ class Trace:
 class Replay:
     """GPU replay of a Trace with node values."""
 
-    def __init__(self, trace: Trace, values, device: int = 0, persistent: bool = False):
+    def __init__(self, trace: Trace, values, device: int = 0, persistent: bool = False,
+                 registers: bool = True):
         self.trace = trace
         self.values = np.ascontiguousarray(values, dtype=np.float64)
         if len(self.values) != trace.n:
@@ -272,6 +273,7 @@ class Replay:
         self.E = trace.n_union_edges
         if persistent:
             L.call("fu_replay_set_option", self._h, b"persistent", 1)
+            L.call("fu_replay_set_option", self._h, b"persistent_reg", int(registers))
         self.tick = 0
 
     def run(self, tick_end: int, snapshot_ticks=()):

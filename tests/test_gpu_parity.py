@@ -135,14 +135,14 @@ def test_option_errors():
     eng.run(2)
 
 
-@pytest.mark.parametrize("persistent", [False, True])
+@pytest.mark.parametrize("persistent", [False, True, "noreg"])
 @pytest.mark.parametrize("name,fn", tick_fixtures())
 def test_replay_matches_reference_snapshots(name, fn, persistent):
     d = load_json(fn)
     names, vals, rp, col = fixture_decl_csr(d)
     tr = fu.Trace(rp, col, "collectall" if d["mode"] == "ca" else "pairwise", d["ticks"],
                   d["order"])
-    rep = fu.Replay(tr, vals, persistent=persistent)
+    rep = fu.Replay(tr, vals, persistent=bool(persistent), registers=persistent != "noreg")
     snaps = rep.run(d["ticks"], snapshot_ticks=range(d["ticks"]))
     for t in range(d["ticks"]):
         keys = d["snap_keys"][t]
@@ -154,7 +154,7 @@ def test_replay_matches_reference_snapshots(name, fn, persistent):
         assert list(est[a["rowptr"][i]:a["rowptr"][i + 1]]) == d["estimates"][i]
 
 
-@pytest.mark.parametrize("persistent", [False, True])
+@pytest.mark.parametrize("persistent", [False, True, "noreg"])
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
 def test_replay_rr64k_vs_c_oracle(mode, persistent):
     """BASELINE config 3: pairwise on a 64K-node random regular graph (and collect-all)."""
@@ -162,7 +162,7 @@ def test_replay_rr64k_vs_c_oracle(mode, persistent):
     v = fu.uniform_values(g.n, seed=0)
     tr = fu.Trace(g.rowptr, g.col, mode, 160, "rand:3")
     a = tr.arrays()
-    rep = fu.Replay(tr, v, persistent=persistent)
+    rep = fu.Replay(tr, v, persistent=bool(persistent), registers=persistent != "noreg")
     snaps = rep.run(160, snapshot_ticks=[60, 120, 159])
     last, flows, est = rep.state()
     l_ref, f_ref, e_ref, s_ref = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"],
@@ -290,14 +290,14 @@ def test_dist_rgg_slabs_local_transport_bitwise():
         e.close()
 
 
-@pytest.mark.parametrize("persistent", [False, True])
+@pytest.mark.parametrize("persistent", [False, True, "noreg"])
 def test_replay_with_faults_vs_c_oracle(persistent):
     """Fault-injected pairwise trace (drops + delays) replayed on the GPU == C oracle."""
     g = fu.Graph.random_regular(4096, 6, seed=2)
     v = fu.uniform_values(g.n, seed=5)
     tr = fu.Trace(g.rowptr, g.col, "pairwise", 300, "rand:1", faults="drop=0.1,delay=4:0.1,seed=3")
     a = tr.arrays()
-    rep = fu.Replay(tr, v, persistent=persistent)
+    rep = fu.Replay(tr, v, persistent=bool(persistent), registers=persistent != "noreg")
     snaps = rep.run(150, snapshot_ticks=[60, 149])
     snaps.update(rep.run(300, snapshot_ticks=[299]))
     l_ref, f_ref, e_ref, s_ref = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"],

@@ -25,13 +25,14 @@ for mode in ("pairwise", "collectall"):
     ev = a["events"]
     upd = int(np.sum(ev[:, 0] == 2) + np.sum(ev[ev[:, 0] == 1, 1]))
     res = {}
-    for pers in (False, True):
-        rep = fu.Replay(tr, v, persistent=pers)
+    for pers in (False, True, "noreg"):
+        rep = fu.Replay(tr, v, persistent=bool(pers), registers=pers != "noreg")
         ms = rep.run_timed(ticks)
         res[pers] = (ms, rep.state())
         rep.close()
     ms, (last, flows, est) = res[False]
     ms_p, (last_p, flows_p, _) = res[True]
+    ms_n, (last_n, flows_n, _) = res["noreg"]
     t0 = time.perf_counter()
     l_ref, f_ref, e_ref, _ = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"], a["events"],
                                             a["out_ids"], tr.n_msgs)
@@ -44,5 +45,7 @@ for mode in ("pairwise", "collectall"):
                       "gpu_persistent_ms": ms_p, "gpu_persistent_us_per_tick": ms_p * 1e3 / ticks,
                       "gpu_persistent_flow_updates_per_s": upd / (ms_p / 1e3),
                       "bitwise_equal": bool(np.array_equal(last, l_ref) and np.array_equal(flows, f_ref)),
-                      "persistent_bitwise_equal": bool(np.array_equal(last_p, l_ref) and np.array_equal(flows_p, f_ref))}),
+                      "persistent_bitwise_equal": bool(np.array_equal(last_p, l_ref) and np.array_equal(flows_p, f_ref)),
+                      "gpu_persistent_noreg_us_per_tick": ms_n * 1e3 / ticks,
+                      "persistent_noreg_bitwise_equal": bool(np.array_equal(last_n, l_ref) and np.array_equal(flows_n, f_ref))}),
           flush=True)
