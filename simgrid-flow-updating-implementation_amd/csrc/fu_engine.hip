@@ -1460,13 +1460,15 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   double lst = last[node];
   long long it = 0;
   bool done = false;
+  // the current event stays in registers across passes (a blocked receive re-reads only
+  // its payload); the next event's loads are issued as soon as p advances
+  int tk = p < pe ? node_tick[p] : INT_MAX;
+  int4 ev = p < pe ? node_ev[p] : make_int4(0, 0, 0, 0);
   while (!done) {
     bool progressed = false;
     while (p < pe) {
-      const int tk = node_tick[p];
       if (tk >= tick_end) break;
       while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
-      const int4 ev = node_ev[p];
       if (ev.x == FU_EV_RECV) {
         const unsigned long long fx = ld_tag(pay + 2 * (long long)ev.z);
         const unsigned long long fy = ld_tag(pay + 2 * (long long)ev.z + 1);
@@ -1525,8 +1527,12 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
       }
       ++p;
       progressed = true;
+      if (p < pe) {
+        tk = node_tick[p];
+        ev = node_ev[p];
+      }
     }
-    done = p == pe || node_tick[p] >= tick_end;
+    done = p == pe || tk >= tick_end;
     if (!done && !progressed) __builtin_amdgcn_s_sleep(2);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
