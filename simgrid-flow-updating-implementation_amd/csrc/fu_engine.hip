@@ -1434,6 +1434,9 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 // payload) instead of also re-reading the node's state from memory on every pass. Same
 // event semantics and order as k_replay_persist; a blocked receive leaves the event loop
 // and is retried on the next pass (no lane spins on another lane of its wave).
+#ifndef FU_REPLAY_SLEEP
+#define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
+#endif
 template <int MAXD>
 __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
     int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_ev,
@@ -1533,7 +1536,7 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
       }
     }
     done = p == pe || tk >= tick_end;
-    if (!done && !progressed) __builtin_amdgcn_s_sleep(2);
+    if (!done && !progressed) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
       break;

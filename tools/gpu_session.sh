@@ -30,6 +30,9 @@ for s in $STEPS; do
                done ;;
     sweepdiag) step sweepdiag 900 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/libfu_diag.so python tools/sweep.py ${SWEEP_ARGS:-} ;;
     replay) step replay 400 python tools/bench_replay.py ;;
+    replaylibs) for lib in ${REPLAY_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...)
+                  step "replay_$lib" 400 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so TICKS=1000 python tools/bench_replay.py
+                done ;;
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;
     rmat)   step bench_rmat 500 python bench.py --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ${RMAT_ARGS:-} ;;
     profrmat) export TMPDIR=/tmp
