@@ -1604,7 +1604,6 @@ struct fu_handle {
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
-  int pg_direct_light = 1;  // kernel 9: light rows at the end gather directly (stream3)
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
@@ -1667,8 +1666,6 @@ struct fu_handle {
   struct TransLayout {
     int P = 0, Q = 0, NB = 0, B = 0;      // slices, blocks per slice, stage blocks, buckets
     int Bh = 0;                           // buckets [0, Bh) hold the mega-hub rows' edges
-    long long Es = 0;                     // edges [0, Es) are staged (the rest: direct light tiles)
-    bool direct = false;                  // light tiles gather directly, on stream3, from the start
     int4 *brange = nullptr;               // stage blocks: {begin, end} in G_A, slice, 0
     unsigned short *colS = nullptr;       // per G_A element: column offset in its slice
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
@@ -1676,8 +1673,6 @@ struct fu_handle {
     double *GA = nullptr, *GB = nullptr;
   };
   TransLayout tr;
-  hipStream_t stream3 = nullptr;          // kernel 9: the direct light tiles
-  hipEvent_t ev_l = nullptr, ev_r3 = nullptr;
   bool tr_ready = false;
   std::string tr_why;
   int n_cu = 256;
@@ -2025,26 +2020,13 @@ int ensure_transpose(fu_handle *h) {
     h->tr_why = E == 0 ? "kernel 9 (pregather): no edges" : "kernel 9 (pregather): more than 2^25 nodes";
     return fail(FU_ERR_GRAPH, h->tr_why);
   }
-  // light rows (tiles of kernel 4's geometry 1) that are the last rows (the degree layout)
-  // gather directly: their neighbours are mostly the hot, L2-resident estimates. Then only
-  // edges [0, Es) are staged and transposed.
-  auto light = [&](int32_t i) {
-    const int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    return d <= h->hub_threshold && d <= kGeoEdges[1] && d <= h->mega_hub;
-  };
-  int32_t lr0 = h->n;
-  while (lr0 > 0 && light(lr0 - 1)) --lr0;
-  bool direct = h->pg_direct_light && lr0 < h->n && h->h_rowptr[lr0] > 0;
-  for (int32_t i = 0; direct && i < lr0; ++i)
-    if (light(i)) direct = false;
-  const int64_t Es = direct ? h->h_rowptr[lr0] : E;
-  const int64_t B = (Es + kTrBE - 1) / kTrBE;
+  const int64_t B = (E + kTrBE - 1) / kTrBE;
   // buckets [0, Bh) hold every mega-hub edge: transposed first, so the hub chains can start
   int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
     if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
   std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < Es; ++e) cnt[h->h_col[e] / SN]++;
+  for (int64_t e = 0; e < E; ++e) cnt[h->h_col[e] / SN]++;
   std::vector<int64_t> reg(P + 1, 0);
   for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
   const int64_t total = reg[P];
@@ -2057,7 +2039,7 @@ int ensure_transpose(fu_handle *h) {
   std::vector<int64_t> cur(reg.begin(), reg.end() - 1);
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
-    const int64_t e1 = std::min<int64_t>(Es, (b + 1) * kTrBE);
+    const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
     for (int64_t e = b * kTrBE; e < e1; ++e) {
       const int32_t c = h->h_col[e];
       const int64_t g = cur[c / SN]++;
@@ -2086,15 +2068,7 @@ int ensure_transpose(fu_handle *h) {
   if (int rc = up(&T.pos16, pos.data(), pos.size())) return rc;
   if (int rc = up(&T.offT, offT.data(), offT.size())) return rc;
   if (int rc = dmalloc(&T.GA, (size_t)total)) return rc;
-  if (int rc = dmalloc(&T.GB, (size_t)std::max<int64_t>(Es, 1))) return rc;
-  T.Es = Es;
-  T.direct = direct;
-  if (direct && !h->stream3) {
-    if (hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_r3, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&h->ev_l, hipEventDisableTiming) != hipSuccess)
-      return fail(FU_ERR_HIP, "hipStreamCreate failed");
-  }
+  if (int rc = dmalloc(&T.GB, (size_t)E)) return rc;
   T.P = (int)P;
   T.Q = (int)Q;
   T.NB = (int)br.size();
@@ -2190,24 +2164,6 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #else
       const bool hubs = nmega;
 #endif
-      // light tiles that gather directly start at once, beside the staging passes
-      const bool direct = h->tr.direct && nl > 0;
-      if (direct) {
-        HIP_TRY(hipEventRecord(h->ev_l, h->stream));
-        HIP_TRY(hipStreamWaitEvent(h->stream3, h->ev_l, 0));
-        if (check)
-          hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 1>), dim3(nl), dim3(kBlock), 0, h->stream3,
-                             tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0,
-                             nullptr);
-        else
-          hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 1>), dim3(nl), dim3(kBlock), 0, h->stream3,
-                             tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0,
-                             nullptr);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(h->ev_r3, h->stream3));
-      }
       StageArgs sa{};
       for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
       sa.P[3] = h->tr.P;
@@ -2229,7 +2185,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       {
         if (bh)
           hipLaunchKernelGGL(k_transpose, dim3(8 * ((bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
-                             h->tr.Es,
+                             (long long)h->E,
                              h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
         if (hubs) {
           HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
@@ -2237,7 +2193,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
         }
         if (h->tr.B > bh)
           hipLaunchKernelGGL(k_transpose, dim3(8 * ((h->tr.B - bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, bh,
-                             h->tr.B - bh, h->tr.P, h->tr.Es, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+                             h->tr.B - bh, h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
       }
       if (hubs) {
         if (check)
@@ -2262,7 +2218,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                          h->stream, tl + nmega, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,  \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
                          h->hrows, 1, Gb);                                                                \
-    if (nl && !direct)                                                                                    \
+    if (nl)                                                                                               \
       hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, h->stream, \
                          tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
@@ -2279,7 +2235,6 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #undef FU_PRE
       HIP_TRY(hipGetLastError());
       if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-      if (direct) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_r3, 0));
     } else {
     // heavy tiles (hubs, heavy rows) lead the tile list: they run as their own launch on the
     // side stream, concurrently with the light tiles' launch (which then keeps kernel 4's
@@ -2639,11 +2594,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->fork_heavy = value != 0;
     return FU_OK;
   }
-  if (!std::strcmp(key, "pg_direct_light")) {  // kernel 9: trailing light rows gather directly (1)
-    h->pg_direct_light = value != 0;
-    free_transpose(h);
-    return FU_OK;
-  }
   if (!std::strcmp(key, "split_hubs")) {  // kernel 4: mega-hub tiles alone on the side stream (1)
     h->split_hubs = value != 0;
     return FU_OK;
@@ -2998,7 +2948,6 @@ int fu_destroy(fu_handle *h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
-  if (h->stream3) hipStreamSynchronize(h->stream3);
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
@@ -3020,9 +2969,6 @@ int fu_destroy(fu_handle *h) {
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
-  for (hipEvent_t e : {h->ev_l, h->ev_r3})
-    if (e) hipEventDestroy(e);
-  if (h->stream3) hipStreamDestroy(h->stream3);
   delete h;
   return FU_OK;
 }

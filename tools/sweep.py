@@ -39,7 +39,6 @@ VARIANTS = {
     "pre_ht512": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 512}),
     "deg_np_ht128": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
     "deg_np_ht256": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
-    "pre_nodirect": ("pregather", {"layout": "degree", "pack": 0, "pg_direct_light": 0}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
