@@ -337,6 +337,17 @@ def run_dist(args, world, rank, local, dist):
     kinfo = eng.info()
     if rank == 0:
         alg = (24 * e_tot + 28 * n_tot) // world  # per GPU, per round
+        # the same workload at one rank, measured earlier on one MI355X (committed line), so
+        # a reader can see weak-scaling efficiency against the same per-GPU graph (the
+        # driver's N = 1 line is the ER-1M headline, a different workload)
+        ref = None
+        ref_path = os.path.join(ROOT, "profiles", "r02", "bench_rggdist_1rank.json")
+        if os.path.exists(ref_path):
+            for ln in open(ref_path):
+                if ln.startswith("{"):
+                    d = json.loads(ln)
+                    ref = {"n_gpus": d["n_gpus"], "edge_updates_per_s": d["value"],
+                           "workload": d["config"]["workload"], "source": "profiles/r02/bench_rggdist_1rank.json"}
         r1 = dev1 / max(1, args.steps - 1)
         achieved = alg / (r1 * 1e-3) / 1e9
         print(json.dumps({
@@ -354,7 +365,9 @@ def run_dist(args, world, rank, local, dist):
                          "frac": achieved / HBM_PEAK_GBS, "traffic": None, "per_gpu": True,
                          "alg_bytes_per_launch": alg, "avg_launch_us": r1 * 1e3,
                          "launch_window": f"rounds 1-{args.steps - 1}, max over ranks (halo included)"},
-            "cpu_baseline": None, "graph_gen_s": t_gen}), flush=True)
+            "cpu_baseline": None, "graph_gen_s": t_gen,
+            "value_per_gpu": e_tot * args.steps / wall / world,
+            "one_rank_reference": ref}), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
