@@ -1209,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
                                                       const double *__restrict__ a_prev2,
                                                       const void *__restrict__ code_prev,
                                                       const PackCtl *__restrict__ ctl, int rslot,
-                                                      double2 *__restrict__ hubxy, const double *__restrict__ Gb) {
+                                                      double2 *__restrict__ hubxy) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
@@ -1220,7 +1220,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
   const int4 hb = hubs[lo];
   const int k = hb.y + (int)(q - hb.w);
   const PackCtl pp = ctl[rslot ^ 1];
-  const double er = Gb ? Gb[k] : ld_est(pp, code_prev, a_prev, col[k]);
+  const double er = ld_est(pp, code_prev, a_prev, col[k]);
   hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
 }
 
@@ -2255,40 +2255,40 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (h->n_hub)
       hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
-                         h->hubxy, Gb);
-#define FU_RECON_G(C, N, D, TE, TN, PR)                                                                   \
+                         h->hubxy);
+#define FU_RECON_G(C, N, D, TE, TN)                                                                   \
   do {                                                                                                    \
     if (nmh)  /* mega hubs (or every heavy tile) on the side stream */                                   \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nmh), dim3(kBlock), 0, \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nmh), dim3(kBlock), 0, \
                          hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
-                         h->hrows, hub_sep, Gb);                                                          \
+                         h->hrows, hub_sep, nullptr);                                                        \
     if (nh - nmh)  /* the other heavy tiles ahead of the light ones on the main stream */                \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2, PR>), dim3(nh - nmh),  \
+      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh - nmh),  \
                          dim3(kBlock), 0, h->stream, h->tiles_geo[h->geo] + nmh, h->rowptr, h->col, h->v, F, ap, \
                          ap2, an, h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl,          \
-                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, Gb);                         \
+                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr);                       \
     if (nb)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, PR>), dim3(nb), dim3(kBlock), 0, h->stream,    \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nb), dim3(kBlock), 0, h->stream,    \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
                          err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
-                         nullptr, nullptr, 0, Gb);                                                        \
+                         nullptr, nullptr, 0, nullptr);                                                      \
     if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
       h->halo_a = an;                                                                                     \
       if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
     }                                                                                                     \
     if (nl - nb)                                                                                          \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, PR>), dim3(nl - nb), dim3(kBlock), 0, h->stream, \
+      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl - nb), dim3(kBlock), 0, h->stream, \
                          h->tiles_geo[h->geo] + nh + nb, h->rowptr, h->col, h->v, F, ap, ap2, an,          \
                          h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1),  \
-                         nullptr, nullptr, nullptr, 0, Gb);                                               \
+                         nullptr, nullptr, nullptr, 0, nullptr);                                             \
   } while (0)
 #define FU_RECON(C, N, D)                                                                                 \
   do {                                                                                                    \
-    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256, false);                                          \
-    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256, false);                                          \
-    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128, false);                                          \
-    else FU_RECON_G(C, N, D, 512, 64, false);                                                             \
+    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                          \
+    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                          \
+    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                          \
+    else FU_RECON_G(C, N, D, 512, 64);                                                             \
   } while (0)
 #ifdef FU_DIAG
     if (h->diag == 1) FU_RECON(false, false, 1);
