@@ -656,3 +656,41 @@ def test_rgg64m_single_gpu_properties():
     mean_v = math.fsum(v.tolist()) / n
     mass = (math.fsum(a.tolist()) + float(np.sum(f))) / n
     assert abs(mass - mean_v) < 1e-9 * mean_v
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_configurations_bitwise(seed):
+    """Seeded random mix of graph family, size, layout, round kernel, the heavy-row / mega-hub
+    thresholds and kernel 4's tile geometry (switched between runs), against the C oracle:
+    every kernel and path must give the same bits."""
+    rng = np.random.default_rng(1000 + seed)
+    fam = rng.choice(["er", "rmat", "rr", "rgg"])
+    if fam == "er":
+        n = int(rng.integers(500, 40000))
+        g = fu.Graph.erdos_renyi(n, int(n * rng.uniform(1, 6)), seed=seed)
+    elif fam == "rmat":
+        g = fu.Graph.rmat(int(rng.integers(9, 15)), int(rng.choice([4, 8, 16])), seed=seed)
+    elif fam == "rr":
+        g = fu.Graph.random_regular(int(rng.integers(64, 20000)) * 2, int(rng.choice([2, 4, 8])), seed=seed)
+    else:
+        g = fu.Graph.random_geometric(int(rng.integers(1000, 30000)), avg_deg=float(rng.uniform(3, 12)), seed=seed)
+    v = fu.uniform_values(g.n, seed=seed)
+    layout = str(rng.choice(["given", "degree"]))
+    eng = fu.CollectAll(g, v, kernel="recon", layout=layout)
+    eng.set_option("hub_threshold", int(rng.choice([16, 64, 128, 512])))
+    eng.set_option("mega_hub", int(rng.choice([64, 300, 2000, 8192])))
+    eng.set_option("pack_every", int(rng.choice([4, 16])))
+    kern = str(rng.choice(["recon", "stage", "pregather"]))
+    try:
+        eng.set_option("kernel", fu.engine.KERNELS[kern])
+    except fu.FuError:
+        eng.set_option("kernel", 4)  # kernel 8 needs a slice layout the graph admits
+    rounds = 0
+    for _ in range(3):  # switch the kernel-4 tile geometry between runs (same state, same bits)
+        eng.set_option("tile_edges", int(rng.choice([2048, 1024, 512])))
+        k = int(rng.integers(3, 12))
+        eng.run(k)
+        rounds += k
+    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, rounds, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref), (fam, layout)
+    assert np.array_equal(eng.flows(), f_ref), (fam, layout)
