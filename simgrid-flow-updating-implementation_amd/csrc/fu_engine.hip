@@ -241,9 +241,23 @@ __device__ __forceinline__ void st_f_full(double *F, int e, double v) {
   st_wt(w + i, (unsigned)__double2hiint(v));
 }
 
+// Flow mode of a round launch (fm): round 0 writes no flows at all. f_{r-2} of round 1 is
+// f_{-1} = -0.0 and f_{r-2} of round 2 is f_0 = (0.0 + a_0[i]) - 0.0 (CA:117 on zero state),
+// a per-row constant of a_{r-2}[i] = own2, so rounds 1 and 2 compute the old flow instead of
+// reading it (fm = 1, 2; fm = 0: read F) and store both words of the new one (the slot holds
+// no earlier value). fu_get_flows after round 0 materialises f_0 (k_round0_flows).
+__device__ __forceinline__ double old_flow(int fm, double own2) { return fm == 1 ? -0.0 : (0.0 + own2) - 0.0; }
+__device__ __forceinline__ double ld_fo(const double *F, int e, int fm, double own2) {
+  return fm == 0 ? ld_f(F, e) : old_flow(fm, own2);
+}
+__device__ __forceinline__ void st_fo(double *F, int e, double v, double f_old, int fm) {
+  if (fm) st_f_full(F, e, v);
+  else st_f(F, e, v, f_old);
+}
+
 // Round 0's flows, one thread per edge: f_0[e] = (0.0 + a_0[row]) - 0.0 into F[0]
-// (CA:117 on zero state) and f_{-1} = -0.0 into F[1], so that round 1's reconstruction
-// reproduces (0.0 + a) - 0.0 (split words). A block owns kR0E consecutive edges: the host
+// (CA:117 on zero state) and, if F1 is given, f_{-1} = -0.0 into F[1] (split words). The
+// rounds never need them (fm above); fu_get_flows after round 0 does. A block owns kR0E consecutive edges: the host
 // listed the row of every block's first edge (blk_row), the block's rows' pointers go to
 // LDS, and each edge's row is a short binary search there (a hub's edges all land in one
 // row; a block whose rows span more than kR0E, runs of isolated nodes, searches rowptr).
@@ -287,6 +301,7 @@ __global__ __launch_bounds__(kBlock) void k_round0_flows(long long E, const int 
   unsigned *w0 = reinterpret_cast<unsigned *>(F0), *w1 = reinterpret_cast<unsigned *>(F1);
   *reinterpret_cast<uint4 *>(w0 + j) = make_uint4(hw[0], hw[1], hw[2], hw[3]);
   *reinterpret_cast<uint4 *>(w0 + j + 32) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+  if (!F1) return;
   const unsigned mh = (unsigned)__double2hiint(-0.0), ml = (unsigned)__double2loint(-0.0);
   *reinterpret_cast<uint4 *>(w1 + j) = make_uint4(mh, mh, mh, mh);
   *reinterpret_cast<uint4 *>(w1 + j + 32) = make_uint4(ml, ml, ml, ml);
@@ -329,8 +344,8 @@ __device__ inline void wave_sync() {
 #ifndef FU_CHAIN_B
 #define FU_CHAIN_B 16  // measured: 8 -> 8.75, 16 -> 7.2, 32 -> 6.4 ns per element (32 costs registers)
 #endif
+template <int B = FU_CHAIN_B>
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
-  constexpr int B = FU_CHAIN_B;
   const bool odd = threadIdx.x & 1;
   const double *src = odd ? es : xs;
   double acc = odd ? T : S;
@@ -380,6 +395,10 @@ __device__ inline T ld_stream(const T *p) {
 #define FU_HEAVY_RL 4
 #endif
 constexpr int kHeavyRL = FU_HEAVY_RL;
+// kernel 9's second heavy launch: rows of 64 x (kHeavyRL, kMidRL] edges keep their operands
+// in registers (no second pass over the row for its flows), at a lower occupancy than the
+// other heavy rows can afford (R-MAT-24: 19 % of the edges sit in rows of 641-1024)
+constexpr int kMidRL = 16;
 
 // DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
 //   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
@@ -393,8 +412,8 @@ constexpr int kHeavyRL = FU_HEAVY_RL;
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
-          bool PRE = false>
-__global__ __launch_bounds__(kBlock) void k_round_recon(
+          bool PRE = false, int HRL = kHeavyRL>
+__global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
     const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
@@ -402,7 +421,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     unsigned long long *__restrict__ err,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
-    const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb) {
+    const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb, int fm) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -434,7 +453,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const double own2 = a_prev2[i];
       double *xs = s_x + w * CH, *es = s_er + w * CH;
       double S = 0.0, T = 0.0;
-      constexpr int RL = kHeavyRL > PL ? kHeavyRL : PL;  // whole chunks (TE 2048: PL = 8)
+      constexpr int RL = HRL > PL ? HRL : PL;  // whole chunks (TE 2048: PL = 8)
       if (d <= 64 * RL) {
         // the whole row in registers (RL elements per lane, all loads in flight at
         // once): the chain runs chunk by chunk through the wave's LDS quarter and the flows
@@ -446,7 +465,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           const int k = lane + 64 * u;
           if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
           else cc[u] = k < d ? col[b + k] : 0;
-          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+          fo[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
         }
         if constexpr (!PRE) {
 #pragma unroll
@@ -462,7 +481,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
               es[lane + 64 * j] = er[c * PL + j];
             }
             wave_sync();
-            if (DIAG != 5) chain_sum(xs, es, min(CH, d - c * CH), S, T);
+            // the register-resident mid launch: 8-element batches (its rows hold 64 VGPRs)
+            if (DIAG != 5) chain_sum<(HRL > kHeavyRL ? 8 : FU_CHAIN_B)>(xs, es, min(CH, d - c * CH), S, T);
           }
         }
         const double a = ((v[i] - S) + T) / (double)(d + 1);
@@ -474,7 +494,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
         for (int u = 0; u < RL; ++u) {  // flows (CA:117-118)
           const int k = lane + 64 * u;
-          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
+          if (k < d) st_fo(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u], fm);
         }
       } else {
       // longer rows: chunk by chunk, the next chunk's loads in flight during this chunk's
@@ -487,7 +507,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           const int k = c0 + lane + 64 * u;
           if constexpr (PRE) ng[u] = k < d ? Gb[b + k] : 0.0;
           else nc[u] = k < d ? col[b + k] : 0;
-          nf[u] = k < d ? ld_f(F, b + k) : 0.0;
+          nf[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
         }
       };
       fetch(0);
@@ -522,7 +542,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
           const int k = k0 + lane + 64 * u;
           if constexpr (PRE) er[u] = k < d ? Gb[b + k] : 0.0;
           else cc[u] = k < d ? col[b + k] : 0;
-          fo[u] = k < d ? ld_f(F, b + k) : 0.0;
+          fo[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
         }
         if constexpr (!PRE) {
 #pragma unroll
@@ -532,7 +552,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int k = k0 + lane + 64 * u;
-          if (k < d) st_f(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u]);
+          if (k < d) st_fo(F, b + k, (recon_fr(fo[u], er[u], own2) + a) - er[u], fo[u], fm);
         }
       }
       }  // rows longer than 64 x kHeavyRL
@@ -560,7 +580,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
       for (int u = 0; u < PL; ++u) {
         const int k = t + 64 * u;
-        nf[u] = k < d ? ld_f(F, b + k) : 0.0;
+        nf[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
         ng[u] = k < d ? Gb[b + k] : 0.0;
       }
       for (int c0 = 0; c0 < d; c0 += CH) {
@@ -574,7 +594,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
 #pragma unroll
         for (int u = 0; u < PL; ++u) {
           const int k = c1 + t + 64 * u;
-          nf[u] = k < d ? ld_f(F, b + k) : 0.0;
+          nf[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
           ng[u] = k < d ? Gb[b + k] : 0.0;
         }
         wave_sync();
@@ -615,8 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       const double a = s_a[0];
       for (int k = t; k < d; k += kBlock) {
         const double2 p2 = xy[k];
-        const double fo = ld_f(F, b + k);
-        st_f(F, b + k, (p2.x + a) - p2.y, fo);
+        st_fo(F, b + k, (p2.x + a) - p2.y, fm ? 0.0 : ld_f(F, b + k), fm);
       }
     }
     if (CHECK) block_max_to(eb, err);
@@ -638,7 +657,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       double *xs = s_x + (c & 1) * CH, *es = s_er + (c & 1) * CH;
       for (int q = tid; q < cn; q += nthr) {
         const double er = PRE ? Gb[c0 + q] : ld_est(pp, code_prev, a_prev, col[c0 + q]);
-        xs[q] = recon_fr(ld_f(F, c0 + q), er, own2);
+        xs[q] = recon_fr(ld_fo(F, c0 + q, fm, own2), er, own2);
         es[q] = er;
       }
     };
@@ -663,8 +682,8 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     const double a = s_a[0];
     for (int k = b + t; k < e; k += kBlock) {
       const double er = PRE ? Gb[k] : ld_est(pp, code_prev, a_prev, col[k]);
-      const double fo = ld_f(F, k);
-      st_f(F, k, (recon_fr(fo, er, own2) + a) - er, fo);
+      const double fo = ld_fo(F, k, fm, own2);
+      st_fo(F, k, (recon_fr(fo, er, own2) + a) - er, fo, fm);
     }
     if (CHECK) block_max_to(eb, err);
     return;
@@ -689,13 +708,13 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
     if (q < ne) {
       if (PRE) {
         g[k] = Gb[e0 + q];
-        x[k] = ld_f(F, e0 + q);
+        x[k] = fm ? 0.0 : ld_f(F, e0 + q);
       } else if (NT) {
         c[k] = ld_stream(col + e0 + q);
-        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_f(F, e0 + q);
+        x[k] = (DIAG == 2 || DIAG == 12 || fm) ? 0.0 : ld_f(F, e0 + q);
       } else {
         c[k] = col[e0 + q];
-        x[k] = (DIAG == 2 || DIAG == 12) ? 0.0 : ld_f(F, e0 + q);
+        x[k] = (DIAG == 2 || DIAG == 12 || fm) ? 0.0 : ld_f(F, e0 + q);
       }
     }
   }
@@ -739,9 +758,10 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
   if (t < nn) {
     const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
     double S = 0.0, T = 0.0;
+    const double fo0 = fm ? old_flow(fm, own2) : 0.0;
     for (int q = qb; q < qe; ++q) {
       const double er = s_er[q];
-      const double fr = recon_fr(s_x[q], er, own2);
+      const double fr = recon_fr(fm ? fo0 : s_x[q], er, own2);
       s_x[q] = fr;
       s_own[q] = (unsigned char)t;
       S = S + fr;
@@ -763,7 +783,7 @@ __global__ __launch_bounds__(kBlock) void k_round_recon(
       if (DIAG == 2 || DIAG == 12) {
         if (fnew == 12345.678) st_f_full(F, e0 + q, fnew);  // keep the value live, store ~never
       } else {
-        st_f(F, e0 + q, fnew, x[k]);
+        st_fo(F, e0 + q, fnew, x[k], fm);
       }
     }
   }
@@ -1090,7 +1110,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
     double *__restrict__ a_new, const double *__restrict__ target,
     unsigned long long *__restrict__ err, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
-    int rslot) {
+    int rslot, int fm) {
   static_assert(TE % kBlock == 0 && TN <= kBlock, "tile geometry");
   static_assert(TE <= 1024, "the u16 staged index holds a 10-bit tile position");
   const PackCtl pp = ctl[rslot ^ 1];
@@ -1123,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
       c16[k] = q < ne ? s16[e0 + q] : (unsigned short)0;
-      x[k] = q < ne ? ld_f(F, e0 + q) : 0.0;
+      x[k] = q < ne && !fm ? ld_f(F, e0 + q) : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -1173,9 +1193,10 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   if (t < nn) {  // phase B (CA:106-113)
     const int qb = s_rp[t] - e0, qe = s_rp[t + 1] - e0;
     double S = 0.0, T = 0.0;
+    const double fo0 = fm ? old_flow(fm, own2) : 0.0;
     for (int q = qb; q < qe; ++q) {
       const double er = s_er[q];
-      const double fr = recon_fr(s_x[q], er, own2);
+      const double fr = recon_fr(fm ? fo0 : s_x[q], er, own2);
       s_x[q] = fr;
       s_own[q] = (unsigned char)t;
       S = S + fr;
@@ -1193,7 +1214,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   for (int k = 0; k < kPer; ++k) {
     const int q = t + k * kBlock;
     if (q < ne) {
-      st_f(F, e0 + q, (s_x[q] + s_a[s_own[q]]) - s_er[q], x[k]);
+      st_fo(F, e0 + q, (s_x[q] + s_a[s_own[q]]) - s_er[q], x[k], fm);
     }
   }
   if (CHECK) block_max_to(eb, err);
@@ -1209,7 +1230,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
                                                       const double *__restrict__ a_prev2,
                                                       const void *__restrict__ code_prev,
                                                       const PackCtl *__restrict__ ctl, int rslot,
-                                                      double2 *__restrict__ hubxy) {
+                                                      double2 *__restrict__ hubxy, int fm) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
@@ -1221,7 +1242,8 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
   const int k = hb.y + (int)(q - hb.w);
   const PackCtl pp = ctl[rslot ^ 1];
   const double er = ld_est(pp, code_prev, a_prev, col[k]);
-  hubxy[q] = make_double2(recon_fr(ld_f(F, k), er, a_prev2[hb.x]), er);
+  const double own2 = a_prev2[hb.x];
+  hubxy[q] = make_double2(recon_fr(ld_fo(F, k, fm, own2), er, own2), er);
 }
 
 
@@ -1232,7 +1254,7 @@ __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__re
                                                       const double2 *__restrict__ hubxy,
                                                       const double *__restrict__ a_new, double *__restrict__ F,
                                                       const double *__restrict__ Gb,
-                                                      const double *__restrict__ a_prev2) {
+                                                      const double *__restrict__ a_prev2, int fm) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
   int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
@@ -1244,12 +1266,13 @@ __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__re
   const int k = hb.y + (int)(q - hb.w);
   const double a = a_new[hb.x];
   if (Gb) {  // kernel 9: (fr, er) rebuilt from the pre-gathered estimate and the old flow
-    const double er = Gb[k], fo = ld_f(F, k);
-    st_f(F, k, (recon_fr(fo, er, a_prev2[hb.x]) + a) - er, fo);
+    const double own2 = a_prev2[hb.x];
+    const double er = Gb[k], fo = ld_fo(F, k, fm, own2);
+    st_fo(F, k, (recon_fr(fo, er, own2) + a) - er, fo, fm);
     return;
   }
   const double2 p2 = hubxy[q];
-  st_f(F, k, (p2.x + a) - p2.y, ld_f(F, k));
+  st_fo(F, k, (p2.x + a) - p2.y, fm ? 0.0 : ld_f(F, k), fm);
 }
 
 // split-word flows -> doubles (fu_get_flows of kernels >= 4)
@@ -1603,6 +1626,7 @@ struct fu_handle {
   int hub_threshold = 128;  // rows above it run as heavy rows (R-MAT-24: 128 beat 64, 256, 512)
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
+  int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
@@ -1624,6 +1648,7 @@ struct fu_handle {
   int ntiles_geo[4] = {0, 0, 0, 0};
   int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
   int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
+  int mid_geo[4][2] = {};            // heavy tiles [mid_geo[0], mid_geo[1]) lead with a row of 64 x (kHeavyRL, kMidRL] edges
   double *halo_a = nullptr;          // multi-GPU: the estimate buffer the round being launched writes
   std::vector<int32_t> h_hrows;
   int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first (per geometry)
@@ -1690,7 +1715,7 @@ constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 // Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
 // block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
 // {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound) {
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound, int *mid) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -1730,9 +1755,17 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     });
     const size_t base = h->h_hrows.size();  // each geometry appends its own list
     h->h_hrows.insert(h->h_hrows.end(), rows.begin(), rows.end());
-    for (size_t q = 0; q < rows.size(); q += 4)
+    // tiles whose longest (first) row fits kMidRL registers per lane but not kHeavyRL
+    auto deg = [&](int32_t x) { return h->h_rowptr[x + 1] - h->h_rowptr[x]; };
+    mid[0] = mid[1] = (int)all.size();
+    for (size_t q = 0; q < rows.size(); q += 4) {
+      const int64_t d0 = deg(rows[q]);
+      if (d0 > 64 * kMidRL) mid[0] = mid[1] = (int)all.size() + 1;
+      else if (d0 > 64 * kHeavyRL) mid[1] = (int)all.size() + 1;
       all.push_back(make_int4((int)(base + q), -4, (int)std::min<size_t>(4, rows.size() - q), 0));
+    }
   } else {
+    mid[0] = mid[1] = (int)hubs.size();
     all.insert(all.end(), heavy.begin(), heavy.end());
   }
   *nheavy = (int)all.size();
@@ -1793,7 +1826,7 @@ int build_tiles(fu_handle *h) {
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
     if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g],
-                                  &h->nbound_geo[g]))
+                                  &h->nbound_geo[g], h->mid_geo[g]))
       return rc;
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
@@ -2087,15 +2120,13 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (int rc = fu__dist_round_hook(h, 0)) return rc;
   }
   const int64_t r = h->rounds;
+  const int fm = r == 1 ? 1 : r == 2 ? 2 : 0;  // rounds 1, 2: the old flows are computed, not read
   if (r == 0) {
-    // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91); f_{-1} = -0.0 and
-    // a_{-1} = 0.0 so that round 1 reproduces round 0's (0.0 + a) - 0.0
+    // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91): a_0 and a_{-1} = 0.0;
+    // no flows are written (rounds 1 and 2 compute f_{-1} and f_0 themselves: fm)
     static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
     hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
                        h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
-    if (h->E)
-      hipLaunchKernelGGL(k_round0_flows, dim3((unsigned)((h->E + kR0E - 1) / kR0E)), dim3(kBlock), 0, h->stream,
-                         (long long)h->E, h->rowptr, h->blk_row, h->a[0], h->f[0], h->f[1]);
     if (check)
       hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
                          h->a[0], h->target, err_slot);
@@ -2122,16 +2153,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check)
         hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                            h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr);
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr, fm);
       else
         hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
                            h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr);
+                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr, fm);
     }
 #define FU_STAGED(C, D)                                                                                  \
   hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
                      h->st_tiles, h->st_ntiles, h->rowptr, h->col, sa, h->stG, h->v, F, ap, ap2, an, h->target, \
-                     err_slot, h->code[r & 1], h->pctl, (int)(r & 1))
+                     err_slot, h->code[r & 1], h->pctl, (int)(r & 1), fm)
     if (h->st_ntiles) {
 #ifdef FU_DIAG
       if (h->diag == 4) FU_STAGED(false, 4);
@@ -2158,6 +2189,9 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       // are transposed first, then the chains (and k_hub_flows) run on the side stream
       // beside the remaining buckets and the other tiles
       const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
+      // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
+      const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
+      const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
       const int4 *tl = h->tiles_geo[1];
 #ifdef FU_DIAG
       const bool hubs = nmega && h->diag != 22;  // 22: timing without the hub path
@@ -2200,29 +2234,33 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
           hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
                              h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
                              h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
-                             1, Gb);
+                             1, Gb, fm);
         else
           hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
                              h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
                              h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
-                             1, Gb);
+                             1, Gb, fm);
         hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2);
+                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2, fm);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
       }
+#define FU_PRE_H(C, D, RL, t0, t1)                                                                         \
+  if ((t1) > (t0))                                                                                        \
+    hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 2, true, RL>), dim3((t1) - (t0)), dim3(kBlock), 0, \
+                       h->stream, tl + (t0), h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,    \
+                       h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,      \
+                       h->hrows, 1, Gb, fm)
 #define FU_PRE(C, D)                                                                                      \
   do {                                                                                                    \
-    if (nh > nmega)                                                                                       \
-      hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 2, true>), dim3(nh - nmega), dim3(kBlock), 0, \
-                         h->stream, tl + nmega, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,  \
-                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
-                         h->hrows, 1, Gb);                                                                \
+    FU_PRE_H(C, D, kHeavyRL, nmega, m0);                                                                  \
+    FU_PRE_H(C, D, kMidRL, m0, m1);                                                                       \
+    FU_PRE_H(C, D, kHeavyRL, m1, nh);                                                                     \
     if (nl)                                                                                               \
       hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, h->stream, \
                          tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
-                         nullptr, 0, Gb);                                                                 \
+                         nullptr, 0, Gb, fm);                                                                 \
   } while (0)
 #ifdef FU_DIAG
       if (h->diag == 20) {  // timing: the staging passes alone
@@ -2233,6 +2271,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       if (check) FU_PRE(true, 0);
       else FU_PRE(false, 0);
 #undef FU_PRE
+#undef FU_PRE_H
       HIP_TRY(hipGetLastError());
       if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
     } else {
@@ -2255,24 +2294,24 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (h->n_hub)
       hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
-                         h->hubxy);
+                         h->hubxy, fm);
 #define FU_RECON_G(C, N, D, TE, TN)                                                                   \
   do {                                                                                                    \
     if (nmh)  /* mega hubs (or every heavy tile) on the side stream */                                   \
       hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nmh), dim3(kBlock), 0, \
                          hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
                          h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
-                         h->hrows, hub_sep, nullptr);                                                        \
+                         h->hrows, hub_sep, nullptr, fm);                                                        \
     if (nh - nmh)  /* the other heavy tiles ahead of the light ones on the main stream */                \
       hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh - nmh),  \
                          dim3(kBlock), 0, h->stream, h->tiles_geo[h->geo] + nmh, h->rowptr, h->col, h->v, F, ap, \
                          ap2, an, h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl,          \
-                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr);                       \
+                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, fm);                       \
     if (nb)                                                                                               \
       hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nb), dim3(kBlock), 0, h->stream,    \
                          h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
                          err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
-                         nullptr, nullptr, 0, nullptr);                                                      \
+                         nullptr, nullptr, 0, nullptr, fm);                                                      \
     if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
       h->halo_a = an;                                                                                     \
       if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
@@ -2281,7 +2320,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl - nb), dim3(kBlock), 0, h->stream, \
                          h->tiles_geo[h->geo] + nh + nb, h->rowptr, h->col, h->v, F, ap, ap2, an,          \
                          h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1),  \
-                         nullptr, nullptr, nullptr, 0, nullptr);                                             \
+                         nullptr, nullptr, nullptr, 0, nullptr, fm);                                             \
   } while (0)
 #define FU_RECON(C, N, D)                                                                                 \
   do {                                                                                                    \
@@ -2309,7 +2348,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #undef FU_RECON_G
     if (hub_sep)
       hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr);
+                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr, fm);
     if (fork) {
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
@@ -2598,6 +2637,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->split_hubs = value != 0;
     return FU_OK;
   }
+  if (!std::strcmp(key, "mid_heavy")) {  // kernel 9: register-resident launch for rows of 257-1024 edges
+    h->mid_heavy = value != 0;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "wave_heavy")) {  // kernel 4: heavy rows one per wave (1) or per block (0)
     h->wave_heavy = value != 0;
     return build_tiles(h);
@@ -2874,10 +2917,17 @@ int fu_get_estimates(fu_handle *h, double *a_out) {
 int fu_get_flows(fu_handle *h, double *f_out) {
   if (!h || (!f_out && h->E)) return fail(FU_ERR_ARG, "fu_get_flows: NULL argument");
   if (h->E == 0) return FU_OK;
+  if (h->rounds == 0) {  // no round yet: every flow is 0.0 (CA:33)
+    std::memset(f_out, 0, sizeof(double) * (size_t)h->E);
+    return FU_OK;
+  }
   if (int rc = set_device(h)) return rc;
   if (!h->ftmp) {
     if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
   }
+  if (h->rounds == 1)  // round 0 writes no flows (fm): f_0 = (0.0 + a_0[i]) - 0.0 on demand
+    hipLaunchKernelGGL(k_round0_flows, dim3((unsigned)((h->E + kR0E - 1) / kR0E)), dim3(kBlock), 0, h->stream,
+                       (long long)h->E, h->rowptr, h->blk_row, h->a[0], h->f[0], nullptr);
   // split words -> doubles
   hipLaunchKernelGGL(k_unsplit, dim3(grid_for(h->E)), dim3(kBlock), 0, h->stream, (long long)h->E, cur_f(h), h->ftmp);
   HIP_TRY(hipGetLastError());
