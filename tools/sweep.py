@@ -27,6 +27,7 @@ VARIANTS = {
     "recon_deg_mega2048": ("recon", {"mega_hub": 2048, "layout": "degree"}),
     "deg_np": ("recon", {"layout": "degree", "pack": 0}),
     "deg_np_pre": ("pregather", {"layout": "degree", "pack": 0}),
+    "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
     "pre_d20": ("pregather", {"layout": "degree", "pack": 0, "diag": 20}),
     "pre_d21": ("pregather", {"layout": "degree", "pack": 0, "diag": 21}),
     "pre_d22": ("pregather", {"layout": "degree", "pack": 0, "diag": 22}),
