@@ -263,10 +263,17 @@ int fu_dist_exchange_local(fu_handle **hs, int32_t nranks) {
       if (cnt != ds[q]->recv_a_off[p + 1] - ds[q]->recv_a_off[p])
         return fail(FU_ERR_ARG, "fu_dist_exchange_local: halo plans of ranks " + std::to_string(p) + " and " +
                                     std::to_string(q) + " disagree");
-      if (cnt && hipMemcpy(a + ds[q]->recv_a_off[p], ds[p]->sbuf_a + ds[p]->send_a_off[q], sizeof(double) * cnt,
-                           hipMemcpyDefault) != hipSuccess)
+      // on the receiver's stream: a device-to-device hipMemcpy may return before the copy has
+      // landed, and the receiver's next round (its stream is non-blocking) would race it
+      if (cnt && (hipSetDevice(fu__handle_device(hs[q])) != hipSuccess ||
+                  hipMemcpyAsync(a + ds[q]->recv_a_off[p], ds[p]->sbuf_a + ds[p]->send_a_off[q], sizeof(double) * cnt,
+                                 hipMemcpyDefault, fu__handle_stream(hs[q])) != hipSuccess))
         return fail(FU_ERR_HIP, "fu_dist_exchange_local: copy failed");
     }
+  }
+  for (int q = 0; q < nranks; ++q) {  // landed before any sender's next pack reuses its buffer
+    if (hipSetDevice(fu__handle_device(hs[q])) != hipSuccess || hipStreamSynchronize(fu__handle_stream(hs[q])) != hipSuccess)
+      return fail(FU_ERR_HIP, "fu_dist_exchange_local: sync failed");
   }
   return FU_OK;
 }

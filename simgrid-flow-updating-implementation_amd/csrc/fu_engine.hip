@@ -165,10 +165,13 @@ __device__ inline void gather_packed(const int (&c)[KP], double (&g)[KP], int t,
 // window [centre - 2^(W-1), centre + 2^(W-1) - 2] holds >= 99.5 % of the sample; else 0.
 constexpr int kPlanSamples = 4096;
 
-__global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__ a,
-                                                      const int *__restrict__ sample,
-                                                      PackCtl *__restrict__ ctl) {
-  constexpr int kPer = kPlanSamples / kBlock;
+// NT threads (every lane in flight: kPlanSamples / NT sample loads, then as many gathers).
+// pw_host (pinned host memory, or null) receives the width for the autotuner's poll, so no
+// copy sits on the round's stream.
+template <int NT>
+__device__ __forceinline__ void plan_body(const double *__restrict__ a, const int *__restrict__ sample,
+                                          PackCtl *ctl, int *pw_host) {
+  constexpr int kPer = kPlanSamples / NT;
   __shared__ unsigned long long s_centre;
   __shared__ int s_cnt[3];
   const int t = threadIdx.x;
@@ -176,7 +179,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
   int idx[kPer];
   unsigned long long key[kPer];
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) idx[k] = sample[t + k * kBlock];  // all loads in flight
+  for (int k = 0; k < kPer; ++k) idx[k] = sample[t + k * NT];  // all loads in flight
 #pragma unroll
   for (int k = 0; k < kPer; ++k) key[k] = dkey(a[idx[k]]);
   if (t < 64) {  // median of samples 0..63: rank by comparison against every lane
@@ -197,9 +200,17 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
     n16 += d + 2 <= (1ull << 15);
     n32 += d + 2 <= (1ull << 31);
   }
-  atomicAdd(&s_cnt[0], n8);
-  atomicAdd(&s_cnt[1], n16);
-  atomicAdd(&s_cnt[2], n32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {  // wave sums, then one LDS add per wave
+    n8 += __shfl_xor(n8, o, 64);
+    n16 += __shfl_xor(n16, o, 64);
+    n32 += __shfl_xor(n32, o, 64);
+  }
+  if ((t & 63) == 0) {
+    atomicAdd(&s_cnt[0], n8);
+    atomicAdd(&s_cnt[1], n16);
+    atomicAdd(&s_cnt[2], n32);
+  }
   __syncthreads();
   if (t == 0) {
     const int need = kPlanSamples - kPlanSamples / 200;
@@ -209,7 +220,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
     p.width = w;
     p.pad = 0;
     ctl[2] = p;
+    if (pw_host) *pw_host = w;
   }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__ a,
+                                                      const int *__restrict__ sample,
+                                                      PackCtl *__restrict__ ctl, int *pw_host) {
+  plan_body<kBlock>(a, sample, ctl, pw_host);
 }
 
 // ------------------------------------------------------------------------------------
@@ -946,15 +964,27 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
 __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         const double *__restrict__ a_prev,
                                                         const void *__restrict__ code_prev,
-                                                        const PackCtl *__restrict__ ctl, int rslot,
-                                                        void *__restrict__ G) {
+                                                        PackCtl *ctl, int rslot,
+                                                        void *__restrict__ G, const int *__restrict__ psample,
+                                                        int *pw_host) {
   __shared__ __align__(16) unsigned char s_tab[kStageLds];
+  // the packing plan from a_{r-1} (the table staged here; due after round r-1) rides on the
+  // stage launch: k_round_staged, the plan's first reader, starts after this launch, so the
+  // plan needs no launch (and stream slot) of its own. Its block is block 0, dispatched
+  // first so its dependent loads overlap the staging; blocks 1-7 exit and the stage blocks
+  // follow from block 8 on, on the XCDs (blockIdx % 8) they have without the plan.
+  int bid = (int)blockIdx.x;
+  if (psample) {
+    if (bid == 0) plan_body<kStageThreads>(a_prev, psample, ctl, pw_host);
+    if (bid < 8) return;
+    bid -= 8;
+  }
   const PackCtl pp = ctl[rslot ^ 1];
   // bytes per element of the table gathered (kernel 9 stages the doubles, always written)
   const int wb = (pp.width && !sa.f64) ? pp.width / 8 : 8;
   const int li = sa.f64 ? 3 : sa.sel[width_index(pp.width)];
-  if ((int)blockIdx.x >= sa.NB[li]) return;
-  const int4 rg = sa.brange[li][blockIdx.x];
+  if (bid >= sa.NB[li]) return;
+  const int4 rg = sa.brange[li][bid];
   if (rg.x >= rg.y) return;  // no slice here (grid rounded to whole XCD rows) or empty region
   const int LB = 1 << li;  // bytes per element the layout was built for
   const int SN = sa.SN[li];
@@ -1639,6 +1669,8 @@ struct fu_handle {
   int tune_cache[4] = {-1, -1, -1, -1};  // winner per packing width (0, 8, 16, 32), kept across fu_reset
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
   bool pw_pending = false;
+  int *pw_dev = nullptr;      // h_pw as the device sees it (the plan kernels write the width there)
+  bool plan_pending = false;  // a packing plan is due before the next round (from its table)
   int diag = 0;  // timing-only ablations (-DFU_DIAG builds only; wrong results)
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_col;
@@ -2121,6 +2153,18 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   }
   const int64_t r = h->rounds;
   const int fm = r == 1 ? 1 : r == 2 ? 2 : 0;  // rounds 1, 2: the old flows are computed, not read
+  // a packing plan due from a_{r-1}: the stage launch of kernels 8 and 9 carries it (one more
+  // block); every other path runs it first as a launch of its own
+  bool plan = h->plan_pending && r > 0;
+  h->plan_pending = false;
+  const bool plan_done = plan;
+  auto plan_alone = [&]() {
+    if (!plan) return;
+    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, h->a[(r - 1) % 3], h->psample, h->pctl,
+                       h->pw_dev);
+    plan = false;
+  };
+  if (h->kernel != 8 && h->kernel != 9) plan_alone();
   if (r == 0) {
     // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91): a_0 and a_{-1} = 0.0;
     // no flows are written (rounds 1 and 2 compute f_{-1} and f_0 themselves: fm)
@@ -2146,9 +2190,12 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #else
     const bool stage = true;
 #endif
-    if (h->st_ntiles && stage)
-      hipLaunchKernelGGL(k_stage, dim3(sgrid), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp, h->pctl,
-                         (int)(r & 1), h->stG);
+    if (h->st_ntiles && stage) {
+      hipLaunchKernelGGL(k_stage, dim3(sgrid + (plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp,
+                         h->pctl, (int)(r & 1), h->stG, plan ? h->psample : nullptr, h->pw_dev);
+      plan = false;
+    }
+    plan_alone();
     if (h->st_nheavy) {
       if (check)
         hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
@@ -2210,8 +2257,13 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #ifdef FU_DIAG
       if (h->diag != 21 && h->diag != 23)
 #endif
-      hipLaunchKernelGGL(k_stage, dim3(h->tr.NB), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
-                         h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA);
+      {
+        hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
+                           h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA, plan ? h->psample : nullptr,
+                           h->pw_dev);
+        plan = false;
+      }
+      plan_alone();
       const int bh = hubs ? h->tr.Bh : 0;
 #ifdef FU_DIAG
       if (h->diag != 21 && h->diag != 24)
@@ -2357,20 +2409,16 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     }  // kernel 4
   }
   HIP_TRY(hipGetLastError());
-  h->rounds++;
-  // refresh the packing plan from a_r (the round kernels encode with it from the next round
-  // on); once the host has seen the narrowest width (8), every 8th time only: the plan and
-  // its width copy stall the stream for ~20 us
-  const int every = h->seen_width == 8 ? 8 * h->pack_every : h->pack_every;
-  if (h->pack && !h->dist && h->n_psample > 0 && h->rounds % every == 0) {
-    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample, h->pctl);
-    HIP_TRY(hipGetLastError());
-    if (!h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
-      HIP_TRY(hipMemcpyAsync(h->h_pw, &h->pctl[2].width, sizeof(int), hipMemcpyDeviceToHost, h->stream));
-      HIP_TRY(hipEventRecord(h->ev_pw, h->stream));
-      h->pw_pending = true;
-    }
+  if (plan_done && !h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
+    HIP_TRY(hipEventRecord(h->ev_pw, h->stream));
+    h->pw_pending = true;
   }
+  h->rounds++;
+  // a packing plan from a_r is due: the next round runs it ahead of its round kernels (on
+  // its stage launch where it has one) and encodes a_{r+1} with it; once the host has seen
+  // the narrowest width (8), every 8th time only
+  const int every = h->seen_width == 8 ? 8 * h->pack_every : h->pack_every;
+  if (h->pack && !h->dist && h->n_psample > 0 && h->rounds % every == 0) h->plan_pending = true;
   return FU_OK;
 }
 
@@ -2465,6 +2513,8 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
   *h->h_pw = 0;
+  if (hipHostGetDevicePointer(reinterpret_cast<void **>(&h->pw_dev), h->h_pw, 0) != hipSuccess)
+    return cleanup(fail(FU_ERR_HIP, "hipHostGetDevicePointer failed"));
   const int64_t fe = (e + 31) / 32 * 32;  // split-word flows: whole 32-edge blocks
   if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (rc = dmalloc(&h->v, n)) ||
       (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) || (rc = dmalloc(&h->a[0], na)) ||
@@ -2609,7 +2659,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "pack")) {
     h->pack = value != 0;
-    if (!h->pack) HIP_TRY(hipMemsetAsync(h->pctl + 2, 0, sizeof(PackCtl), h->stream));  // stop encoding
+    if (!h->pack) {  // stop encoding (and drop a plan still due)
+      h->plan_pending = false;
+      HIP_TRY(hipMemsetAsync(h->pctl + 2, 0, sizeof(PackCtl), h->stream));
+    }
     return FU_OK;
   }
   if (!std::strcmp(key, "pack_every")) {
@@ -2667,7 +2720,8 @@ int fu_reset(fu_handle *h) {
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
-  h->pw_pending = false;  // the stream is idle: no plan copy in flight
+  h->pw_pending = false;  // the stream is idle: no plan in flight
+  h->plan_pending = false;  // round 0 clears the plan
   *h->h_pw = 0;           // round 0 clears the packing plan
   h->seen_width = 0;
   if (h->autotune && h->tuned && h->tune_cache[0] >= 0) {  // unpacked again: its winner
@@ -2970,6 +3024,11 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
 int fu_get_pack(fu_handle *h, int32_t width[3]) {
   if (!h || !width) return fail(FU_ERR_ARG, "fu_get_pack: NULL argument");
   if (int rc = set_device(h)) return rc;
+  if (h->plan_pending && h->rounds > 0) {  // the plan due after the last round, as the next round would run it
+    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, cur_a(h), h->psample, h->pctl, h->pw_dev);
+    HIP_TRY(hipGetLastError());
+    h->plan_pending = false;
+  }
   PackCtl p[3];
   HIP_TRY(hipMemcpyAsync(p, h->pctl, sizeof(p), hipMemcpyDeviceToHost, h->stream));
   HIP_TRY(hipStreamSynchronize(h->stream));
