@@ -430,7 +430,7 @@ constexpr int kMidRL = 16;
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
 template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
-          bool PRE = false, int HRL = kHeavyRL>
+          bool PRE = false, int HRL = kHeavyRL, bool RF = true>
 __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
     const int *__restrict__ col, const double *__restrict__ v, double *__restrict__ F,
@@ -717,30 +717,57 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
   constexpr int kPer = TE / kBlock;
   int c[kPer];
   double x[kPer], g[kPer];
+  int rp, rp_last = 0;
+  double vv, own2;
+  if constexpr (PRE) {
 #pragma unroll
-  for (int k = 0; k < kPer; ++k) {
-    const int q = t + k * kBlock;
-    c[k] = 0;
-    x[k] = 0.0;
-    g[k] = 0.0;
-    if (q < ne) {
-      if (PRE) {
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      c[k] = 0;
+      x[k] = 0.0;
+      g[k] = 0.0;
+      if (q < ne) {
         g[k] = Gb[e0 + q];
         x[k] = fm ? 0.0 : ld_f(F, e0 + q);
-      } else if (NT) {
-        c[k] = ld_stream(col + e0 + q);
-        x[k] = (DIAG == 2 || DIAG == 12 || fm) ? 0.0 : ld_f(F, e0 + q);
-      } else {
-        c[k] = col[e0 + q];
-        x[k] = (DIAG == 2 || DIAG == 12 || fm) ? 0.0 : ld_f(F, e0 + q);
       }
     }
+    rp = t <= nn ? rowptr[nb + t] : 0;
+    if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
+    vv = t < nn ? v[nb + t] : 0.0;
+    own2 = t < nn ? a_prev2[nb + t] : 0.0;
+  } else {
+    // the column indices first, then the flows (RF: round >= 3) and node words, every load
+    // unconditional from a clamped index (col and F hold at least one element / 32-edge
+    // block), so the gathers wait for the indices alone (in-order completion, vmcnt(N))
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      const int ci = q < ne ? e0 + q : (ne > 0 ? e0 : 0);
+      const int cv = NT ? ld_stream(col + ci) : col[ci];
+      c[k] = q < ne ? cv : 0;
+      g[k] = 0.0;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      if constexpr (RF && DIAG != 2 && DIAG != 12) {
+        const double f = ld_f(F, q < ne ? e0 + q : 0);
+        x[k] = q < ne ? f : 0.0;
+      } else {
+        x[k] = 0.0;
+      }
+    }
+    const int tn = min(t, nn - 1);  // a light tile has at least one node
+    const int rp0 = rowptr[nb + min(t, nn)];
+    const double v0 = v[nb + tn], o0 = a_prev2[nb + tn];
+    int rl0 = 0;
+    if constexpr (TN == kBlock) rl0 = rowptr[nb + nn];  // the tile's end (256-node tiles)
+    asm volatile("" ::: "memory");  // the loads above are issued before the first wait
+    rp = t <= nn ? rp0 : 0;
+    if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rl0 : 0;
+    vv = t < nn ? v0 : 0.0;
+    own2 = t < nn ? o0 : 0.0;
   }
-  const int rp = t <= nn ? rowptr[nb + t] : 0;
-  int rp_last = 0;
-  if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rowptr[nb + kBlock] : 0;
-  const double vv = t < nn ? v[nb + t] : 0.0;
-  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
   if (PRE) {
   } else if (DIAG != 0 || pp.width == 0) {
 #pragma unroll
@@ -1132,7 +1159,7 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P
 // DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
 // 2 = no stage launch and G read as in 1 (prices the round without staging), 3 = 2 without
 // the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
-template <bool CHECK, int TE, int TN, int DIAG = 0>
+template <bool CHECK, int TE, int TN, int DIAG = 0, bool RF = true, bool LO = true>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
     const int4 *__restrict__ tiles, int ntl,
     const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -1166,6 +1193,51 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   unsigned si[kPer];  // position in the tile
   double x[kPer], g[kPer];
   int gi[kPer];
+  // Load order (LO): the run offsets and staged indices first, the flows and node words
+  // after them, so the G loads (which need only the former) issue while the flows are in
+  // flight (in-order completion: waiting for a load waits for every load issued before it).
+  int rp;
+  double vv, own2;
+  if constexpr (LO) {
+  {  // u16 position | run << 10; G index = m + D[run] (lane `run` holds D)
+    const int dl = sa.dtab[lsel][(size_t)tile * kStageRuns + (t & 63)];
+    unsigned short c16[kPer];
+    // unconditional loads from clamped (always valid) indices, so the compiler can wait for
+    // the staged indices alone (vmcnt(N)) instead of for every load (a skipped load would
+    // change the count)
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      const unsigned short c = s16[q < ne ? e0 + q : 0];
+      c16[k] = q < ne ? c : (unsigned short)0;
+    }
+    if constexpr (RF) {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int q = t + k * kBlock;
+        const double f = ld_f(F, q < ne ? e0 + q : 0);
+        x[k] = q < ne ? f : 0.0;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) x[k] = 0.0;
+    }
+    const int tn = min(t, nn - 1);  // a light tile has at least one node
+    const int rp0 = rowptr[nb + min(t, nn)];
+    const double v0 = v[nb + tn], o0 = a_prev2[nb + tn];
+    asm volatile("" ::: "memory");  // every load above issued before the first wait (no sinking)
+    rp = t <= nn ? rp0 : 0;
+    vv = t < nn ? v0 : 0.0;
+    own2 = t < nn ? o0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int q = t + k * kBlock;
+      const int dd = __shfl(dl, (int)(c16[k] >> 10));
+      si[k] = c16[k] & 1023u;
+      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : q + dd) : -1;
+    }
+  }
+  } else {  // the round-1 order: indices and flows interleaved (measured against LO)
   {  // u16 position | run << 10; G index = m + D[run] (lane `run` holds D)
     const int dl = sa.dtab[lsel][(size_t)tile * kStageRuns + (t & 63)];
     unsigned short c16[kPer];
@@ -1173,7 +1245,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
       c16[k] = q < ne ? s16[e0 + q] : (unsigned short)0;
-      x[k] = q < ne && !fm ? ld_f(F, e0 + q) : 0.0;
+      x[k] = q < ne && RF ? ld_f(F, e0 + q) : 0.0;
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -1183,9 +1255,10 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
       gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : q + dd) : -1;
     }
   }
-  const int rp = t <= nn ? rowptr[nb + t] : 0;
-  const double vv = t < nn ? v[nb + t] : 0.0;
-  const double own2 = t < nn ? a_prev2[nb + t] : 0.0;
+  rp = t <= nn ? rowptr[nb + t] : 0;
+  vv = t < nn ? v[nb + t] : 0.0;
+  own2 = t < nn ? a_prev2[nb + t] : 0.0;
+  }
   // every G load of the tile first, then decode (escapes gather the double via col)
   if (pp.width == 0) {
 #pragma unroll
@@ -1657,6 +1730,7 @@ struct fu_handle {
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
+  int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
@@ -2206,10 +2280,17 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                            h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
                            cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr, fm);
     }
-#define FU_STAGED(C, D)                                                                                  \
-  hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
+#define FU_STAGED_RF(C, D, RF)                                                                            \
+  if (h->staged_lo) FU_STAGED_RFL(C, D, RF, true); else FU_STAGED_RFL(C, D, RF, false)
+#define FU_STAGED_RFL(C, D, RF, LO)                                                                       \
+  hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D, RF, LO>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
                      h->st_tiles, h->st_ntiles, h->rowptr, h->col, sa, h->stG, h->v, F, ap, ap2, an, h->target, \
                      err_slot, h->code[r & 1], h->pctl, (int)(r & 1), fm)
+#define FU_STAGED(C, D)                                                                                  \
+  do {                                                                                                    \
+    if (fm) FU_STAGED_RF(C, D, false);                                                                    \
+    else FU_STAGED_RF(C, D, true);                                                                        \
+  } while (0)
     if (h->st_ntiles) {
 #ifdef FU_DIAG
       if (h->diag == 4) FU_STAGED(false, 4);
@@ -2221,6 +2302,8 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       else FU_STAGED(false, 0);
     }
 #undef FU_STAGED
+#undef FU_STAGED_RF
+#undef FU_STAGED_RFL
   } else {
     double *F = h->f[r & 1];
     const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
@@ -2347,6 +2430,17 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
       hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
                          h->hubxy, fm);
+// light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
+#define FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, RF)                                                         \
+  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, false, kHeavyRL, RF>), dim3(cnt), dim3(kBlock), 0,     \
+                     h->stream, tp, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
+                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, \
+                     nullptr, fm)
+#define FU_LIGHT(C, N, D, TE, TN, cnt, tp)                                                                \
+  do {                                                                                                    \
+    if (fm) FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, false);                                                 \
+    else FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, true);                                                     \
+  } while (0)
 #define FU_RECON_G(C, N, D, TE, TN)                                                                   \
   do {                                                                                                    \
     if (nmh)  /* mega hubs (or every heavy tile) on the side stream */                                   \
@@ -2359,20 +2453,12 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                          dim3(kBlock), 0, h->stream, h->tiles_geo[h->geo] + nmh, h->rowptr, h->col, h->v, F, ap, \
                          ap2, an, h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl,          \
                          (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, fm);                       \
-    if (nb)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nb), dim3(kBlock), 0, h->stream,    \
-                         h->tiles_geo[h->geo] + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target,     \
-                         err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr,     \
-                         nullptr, nullptr, 0, nullptr, fm);                                                      \
+    if (nb) FU_LIGHT(C, N, D, TE, TN, nb, h->tiles_geo[h->geo] + nh);                                    \
     if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
       h->halo_a = an;                                                                                     \
       if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
     }                                                                                                     \
-    if (nl - nb)                                                                                          \
-      hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1>), dim3(nl - nb), dim3(kBlock), 0, h->stream, \
-                         h->tiles_geo[h->geo] + nh + nb, h->rowptr, h->col, h->v, F, ap, ap2, an,          \
-                         h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1),  \
-                         nullptr, nullptr, nullptr, 0, nullptr, fm);                                             \
+    if (nl - nb) FU_LIGHT(C, N, D, TE, TN, nl - nb, h->tiles_geo[h->geo] + nh + nb);                     \
   } while (0)
 #define FU_RECON(C, N, D)                                                                                 \
   do {                                                                                                    \
@@ -2398,6 +2484,8 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     }
 #undef FU_RECON
 #undef FU_RECON_G
+#undef FU_LIGHT
+#undef FU_LIGHT_RF
     if (hub_sep)
       hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr, fm);
@@ -2515,7 +2603,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
   *h->h_pw = 0;
   if (hipHostGetDevicePointer(reinterpret_cast<void **>(&h->pw_dev), h->h_pw, 0) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipHostGetDevicePointer failed"));
-  const int64_t fe = (e + 31) / 32 * 32;  // split-word flows: whole 32-edge blocks
+  const int64_t fe = std::max<int64_t>(32, (e + 31) / 32 * 32);  // split-word flows: whole 32-edge blocks (one at least: clamped loads read edge 0)
   if ((rc = dmalloc(&h->rowptr, n + 1)) || (rc = dmalloc(&h->col, e)) || (rc = dmalloc(&h->v, n)) ||
       (rc = dmalloc(&h->f[0], fe)) || (rc = dmalloc(&h->f[1], fe)) || (rc = dmalloc(&h->a[0], na)) ||
       (rc = dmalloc(&h->a[1], na)) || (rc = dmalloc(&h->a[2], na)) || (rc = dmalloc(&h->target, n)) ||
@@ -2688,6 +2776,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "split_hubs")) {  // kernel 4: mega-hub tiles alone on the side stream (1)
     h->split_hubs = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
+    h->staged_lo = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "mid_heavy")) {  // kernel 9: register-resident launch for rows of 257-1024 edges

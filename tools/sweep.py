@@ -28,6 +28,8 @@ VARIANTS = {
     "deg_np": ("recon", {"layout": "degree", "pack": 0}),
     "deg_np_pre": ("pregather", {"layout": "degree", "pack": 0}),
     "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
+    "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
+    "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_d20": ("pregather", {"layout": "degree", "pack": 0, "diag": 20}),
     "pre_d21": ("pregather", {"layout": "degree", "pack": 0, "diag": 21}),
     "pre_d22": ("pregather", {"layout": "degree", "pack": 0, "diag": 22}),
@@ -43,6 +45,7 @@ VARIANTS = {
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
+    "stage_lo0": ("stage", {"staged_lo": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
     # timing-only ablations (WRONG results): need the -DFU_DIAG library (make DIAG=1,
     # FU_LIBRARY=.../libfu_diag.so)
