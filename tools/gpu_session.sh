@@ -25,8 +25,10 @@ for s in $STEPS; do
     prof)   export TMPDIR=/tmp
             step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOTDIR/bench.py" --cpu-seconds 0 ${BENCH_ARGS:-} ;;
     sweep)  step sweep 900 python tools/sweep.py ${SWEEP_ARGS:-} ;;
-    sweeplibs) for lib in ${SWEEP_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...)
-                 step "sweep_$lib" 600 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so python tools/sweep.py ${SWEEP_ARGS:-}
+    sweeplibs) i=0
+               for lib in ${SWEEP_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...), in the order given
+                 i=$((i+1))
+                 step "sweep_${i}_$lib" 600 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so python tools/sweep.py ${SWEEP_ARGS:-}
                done ;;
     sweepdiag) step sweepdiag 900 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/libfu_diag.so python tools/sweep.py ${SWEEP_ARGS:-} ;;
     replay) step replay 400 python tools/bench_replay.py ;;
