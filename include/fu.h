@@ -122,6 +122,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster
  *                 (default 1); "pack_every" rounds between encoding plans (default 16).
  * "stage_layout"  kernel 8, tests: -1 = by packing width, 0..3 = the 1/2/4/8-byte layout.
+ * "staged_lo"     kernel 8: staged indices loaded ahead of the flows (1, default) or
+ *                 interleaved with them (0; the round-1 order, kept for A/B and tests).
  * Timing-only ablations ("diag") exist only in a -DFU_DIAG build (tools/). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
