@@ -91,6 +91,27 @@ def test_err_trace_and_max_err():
         assert tr[r - 1] == np.max(np.abs(a_ref - tgt))
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_first_rounds_flows_each_round(kernel):
+    """Round 0 writes no flows and rounds 1-2 compute the old flows instead of reading them
+    (fm): the flows read back after every one of the first rounds (f_0 materialised on
+    demand) and before any round (all 0.0) equal the C oracle, also after a reset."""
+    g = fu.Graph.rmat(12, 16, seed=4)
+    v = fu.uniform_values(g.n, seed=4)
+    eng = fu.CollectAll(g, v, kernel=kernel, hub_threshold=32)
+    eng.set_option("mega_hub", 300)  # mega-hub chains and k_hub_stage / k_hub_flows too
+    assert g.max_deg > 300
+    for attempt in range(2):
+        assert not np.any(eng.flows())
+        for r in range(1, 6):
+            eng.run(1)
+            a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, r)
+            assert np.array_equal(eng.estimates(), a_ref), (kernel, r)
+            assert np.array_equal(eng.flows(), f_ref), (kernel, r)
+        eng.reset()
+    eng.close()
+
+
 def test_nan_propagates_to_err():
     g = fu.Graph.random_regular(256, 4, seed=1)
     v = fu.uniform_values(g.n, seed=0)
