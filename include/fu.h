@@ -118,6 +118,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "split_hubs"    kernel 4: only the mega-hub tiles on the side stream (default 1).
  * "mid_heavy"     kernel 9: heavy rows of 257-1024 edges in a launch of their own that keeps
  *                 the whole row in registers (default 1).
+ * "tr_bpx"        kernel 9: transpose blocks per XCD, each looping over buckets (default 32;
+ *                 0 = one block per bucket).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).
  * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster
  *                 (default 1); "pack_every" rounds between encoding plans (default 16).

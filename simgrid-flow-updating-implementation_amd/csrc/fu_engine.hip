@@ -1057,6 +1057,11 @@ static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 po
 constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
 constexpr int kTrThreads = 1024;
 
+// Persistent over its buckets: grid = 8 x (blocks per XCD); XCD x owns the contiguous
+// bucket range [x per, (x + 1) per) and its blocks take every nj-th bucket of it. The next
+// bucket's run starts (offT) are loaded while this bucket's G_A loads are in flight, and its
+// G_B stores drain while the next bucket is scanned (with one block per bucket, each block
+// paid the offT round trip first and held its slot until its stores were done).
 __global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
@@ -1071,19 +1076,26 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P
   // XCD-contiguous buckets (block b runs on XCD b % 8): a G_A line that ends one bucket's
   // run and starts the next bucket's is fetched into one L2, not two
   const int per = (nbk + 7) >> 3;
-  const int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  if (bk >= nbk) return;
+  const int nj = (int)(gridDim.x >> 3);
+  int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
+  if (bk >= bend) return;
+  // runs: thread t owns slices 2t, 2t + 1
+  int o[2], len[2];
+  auto load_runs = [&](int bkk, int (&oo)[2], int (&ll)[2]) {
+    const int bb = b0 + bkk;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int sl = 2 * t + j;
+      oo[j] = sl < P ? offT[(long long)bb * P + sl] : 0;
+      ll[j] = sl < P ? offT[(long long)(bb + 1) * P + sl] - oo[j] : 0;
+    }
+  };
+  load_runs(bk, o, len);
+  for (;;) {
   const int bb = b0 + bk;
   const long long e0 = (long long)bb * kTrBE;
   const int ne = (int)min((long long)kTrBE, E - e0);
-  // runs: thread t owns slices 2t, 2t + 1
-  int o[2], len[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int sl = 2 * t + j;
-    o[j] = sl < P ? offT[(long long)bb * P + sl] : 0;
-    len[j] = sl < P ? offT[(long long)(bb + 1) * P + sl] - o[j] : 0;
-  }
   // exclusive scan of len0 + len1 over the block: wave shuffles, then the 16 wave totals
   int x = len[0] + len[1];
 #pragma unroll
@@ -1149,11 +1161,17 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P
     val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
+  const int next = bk + nj;
+  if (next < bend) load_runs(next, o, len);  // in flight beside this bucket's loads
 #pragma unroll
   for (int k = 0; k < kPerT; ++k)
     if (g[k] >= 0) s_v[pos[k]] = val[k];
   __syncthreads();
   for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
+  if (next >= bend) break;
+  __syncthreads();  // the shared tables and s_v are rewritten for the next bucket
+  bk = next;
+  }
 }
 
 // DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
@@ -1730,6 +1748,7 @@ struct fu_handle {
   int mega_hub = 8192;   // degree above which a row's (fr, er) pairs are staged by many blocks
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
+  int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
@@ -2219,6 +2238,13 @@ int ensure_transpose(fu_handle *h) {
 
 inline unsigned grid_for(long long work) { return (unsigned)((work + kBlock - 1) / kBlock); }
 
+// k_transpose grid for nbk buckets: 8 XCDs x min(buckets per XCD, tr_bpx blocks per XCD)
+// (tr_bpx 0: one block per bucket)
+inline unsigned tr_grid(fu_handle *h, int nbk) {
+  const int per = (nbk + 7) / 8;
+  return 8u * (unsigned)(h->tr_bpx > 0 ? std::min(per, h->tr_bpx) : per);
+}
+
 // One round: state of round r-1 -> round r. err_slot: nullptr = no check.
 int launch_round(fu_handle *h, unsigned long long *err_slot) {
   const bool check = err_slot != nullptr;
@@ -2353,7 +2379,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #endif
       {
         if (bh)
-          hipLaunchKernelGGL(k_transpose, dim3(8 * ((bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
+          hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
                              (long long)h->E,
                              h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
         if (hubs) {
@@ -2361,7 +2387,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
           HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
         }
         if (h->tr.B > bh)
-          hipLaunchKernelGGL(k_transpose, dim3(8 * ((h->tr.B - bh + 7) / 8)), dim3(kTrThreads), 0, h->stream, bh,
+          hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh,
                              h->tr.B - bh, h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
       }
       if (hubs) {
@@ -2780,6 +2806,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
     h->staged_lo = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "tr_bpx")) {  // kernel 9: transpose blocks per XCD (0 = one per bucket)
+    if (value < 0 || value > 1 << 20) return fail(FU_ERR_ARG, "fu_set_option: tr_bpx must be in [0, 2^20]");
+    h->tr_bpx = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "mid_heavy")) {  // kernel 9: register-resident launch for rows of 257-1024 edges
