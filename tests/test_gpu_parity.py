@@ -432,6 +432,23 @@ def test_packed_gather_long_run_bitwise(kind, kernel):
     assert np.array_equal(off.estimates(), a_ref)
 
 
+@pytest.mark.parametrize("opts", [{"staged_lo": 0}, {"staged_lo": 0, "pack": 0}, {"tr_bpx": 0}])
+def test_load_order_and_transpose_options_bitwise(opts):
+    """The A/B options of this round (kernel 8's interleaved load order; kernel 9's
+    one-block-per-bucket transpose) give the C oracle's bits over a 300-round run with packing
+    and escapes."""
+    g, v = _er_with_outlier_pairs(100_000, 400_000, 64, seed=5)
+    rounds = 300
+    eng = fu.CollectAll(g, v, kernel="pregather" if "tr_bpx" in opts else "stage", hub_threshold=16)
+    eng.set_option("pack_every", 4)
+    for k, val in opts.items():
+        eng.set_option(k, val)
+    eng.run(rounds)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+
+
 def test_packed_gather_with_kernel_switches():
     """recon, stage and auto (which switches kernels and geometries mid-run, re-tuning at each
     packing width) give the same bits over a run long enough for packing to engage."""
