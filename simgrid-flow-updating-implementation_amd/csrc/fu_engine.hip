@@ -1351,14 +1351,14 @@ __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__re
                                                       const double *__restrict__ a_prev2,
                                                       const void *__restrict__ code_prev,
                                                       const PackCtl *__restrict__ ctl, int rslot,
-                                                      double2 *__restrict__ hubxy, int fm) {
+                                                      double2 *__restrict__ hubxy, int fm,
+                                                      const int *__restrict__ hub_blk) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
-  int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (hubs[mid].w <= q) lo = mid; else hi = mid - 1;
-  }
+  // hubs[h] = {node, row begin, row end, offset}: the block's first edge's hub from the host
+  // table (a hub of > mega_hub edges spans whole blocks), then at most a step or two on
+  int lo = hub_blk[blockIdx.x];
+  while (lo + 1 < nhub && hubs[lo + 1].w <= q) ++lo;
   const int4 hb = hubs[lo];
   const int k = hb.y + (int)(q - hb.w);
   const PackCtl pp = ctl[rslot ^ 1];
@@ -1375,14 +1375,14 @@ __global__ __launch_bounds__(kBlock) void k_hub_flows(int nhub, const int4 *__re
                                                       const double2 *__restrict__ hubxy,
                                                       const double *__restrict__ a_new, double *__restrict__ F,
                                                       const double *__restrict__ Gb,
-                                                      const double *__restrict__ a_prev2, int fm) {
+                                                      const double *__restrict__ a_prev2, int fm,
+                                                      const int *__restrict__ hub_blk) {
   const long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q >= total) return;
-  int lo = 0, hi = nhub - 1;  // hubs[h] = {node, row begin, row end, offset}
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (hubs[mid].w <= q) lo = mid; else hi = mid - 1;
-  }
+  // hubs[h] = {node, row begin, row end, offset}: the block's first edge's hub from the host
+  // table (a hub of > mega_hub edges spans whole blocks), then at most a step or two on
+  int lo = hub_blk[blockIdx.x];
+  while (lo + 1 < nhub && hubs[lo + 1].w <= q) ++lo;
   const int4 hb = hubs[lo];
   const int k = hb.y + (int)(q - hb.w);
   const double a = a_new[hb.x];
@@ -1780,6 +1780,7 @@ struct fu_handle {
   int n_hub = 0;
   int64_t hub_total = 0;
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
+  int *hub_blk = nullptr;    // per 256-edge block of the hub edges: the hub of its first edge
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -1917,8 +1918,9 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
 
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
-  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy})
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk})
     if (p) hipFree(p);
+  h->hub_blk = nullptr;
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
@@ -1941,6 +1943,14 @@ int build_hubs(fu_handle *h) {
   if (int rc = dmalloc(&h->hubxy, (size_t)tot)) return rc;
   HIP_TRY(hipMemcpy(h->hub_rows, rows.data(), sizeof(int4) * rows.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(h->hub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
+  std::vector<int32_t> blk((size_t)((tot + kBlock - 1) / kBlock));
+  for (size_t b = 0, hh = 0; b < blk.size(); ++b) {
+    const int64_t q0 = (int64_t)b * kBlock;
+    while (hh + 1 < off.size() && off[hh + 1] <= q0) ++hh;
+    blk[b] = (int32_t)hh;
+  }
+  if (int rc = dmalloc(&h->hub_blk, blk.size())) return rc;
+  HIP_TRY(hipMemcpy(h->hub_blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
   return FU_OK;
 }
 
@@ -2402,7 +2412,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
                              h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
                              1, Gb, fm);
         hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2, fm);
+                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2, fm, h->hub_blk);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
       }
@@ -2455,7 +2465,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (h->n_hub)
       hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
-                         h->hubxy, fm);
+                         h->hubxy, fm, h->hub_blk);
 // light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
 #define FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, RF)                                                         \
   hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, false, kHeavyRL, RF>), dim3(cnt), dim3(kBlock), 0,     \
@@ -2514,7 +2524,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 #undef FU_LIGHT_RF
     if (hub_sep)
       hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr, fm);
+                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr, fm, h->hub_blk);
     if (fork) {
       HIP_TRY(hipGetLastError());
       HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
@@ -3183,7 +3193,7 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
-                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->code[0], h->code[1], h->pctl,
+                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG};
   free_transpose(h);
   for (const auto &L : h->st) {
