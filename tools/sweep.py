@@ -28,6 +28,8 @@ VARIANTS = {
     "deg_np": ("recon", {"layout": "degree", "pack": 0}),
     "deg_np_pre": ("pregather", {"layout": "degree", "pack": 0}),
     "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
+    "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
+    "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_tr0": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 0}),
     "pre_tr16": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 16}),
     "pre_tr48": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 48}),
