@@ -30,6 +30,8 @@ VARIANTS = {
     "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
+    "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
+    "pre_mega64k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 65536}),
     "pre_tr0": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 0}),
     "pre_tr16": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 16}),
     "pre_tr48": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 48}),
@@ -37,6 +39,8 @@ VARIANTS = {
     "pre_tr128": ("pregather", {"layout": "degree", "pack": 0, "tr_bpx": 128}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
+    "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
+    "pre_mega64k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 65536}),
     "pre_d20": ("pregather", {"layout": "degree", "pack": 0, "diag": 20}),
     "pre_d21": ("pregather", {"layout": "degree", "pack": 0, "diag": 21}),
     "pre_d22": ("pregather", {"layout": "degree", "pack": 0, "diag": 22}),
