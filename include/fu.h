@@ -273,18 +273,24 @@ int fu_dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                    const int32_t *send_a_idx, const int64_t *recv_a_off,
                    const uint8_t *unique_id, int32_t device, fu_handle **out);
 
-/* Test transport (one process, e.g. all ranks on one GPU): the same rank handle without a
- * communicator. After each round the handle packs its boundary estimates; the caller runs
- * one round on every rank, then fu_dist_exchange_local(hs, nranks) copies the packed slots
- * into the peers' ghost slots (device copies, the order RCCL uses). The error all-reduce is
- * left to the caller. This exercises the ghost-slot reads of the round kernels and the pack
- * kernel without a multi-GPU box. */
+/* In-process transport (one process, e.g. all ranks on one GPU): the same rank handle
+ * without a communicator, and the same comm-stream / event chain as RCCL. Each round packs
+ * the rank's boundary estimates on its comm stream behind the boundary tiles; after every
+ * rank has launched round r, fu_dist_exchange_local(hs, nranks) queues, on each receiver's
+ * comm stream, device copies of its peers' packed slots into its ghost slots (the order
+ * RCCL uses), beside the interior tiles of round r; round r + 1 waits for them. No host
+ * synchronisation. Errors: FU_ERR_STATE if the ranks have run different numbers of rounds
+ * or round r's halo was already exchanged. fu_dist_run_local runs `rounds` rounds of every
+ * rank, each followed by the exchange. The error all-reduce is left to the caller. This
+ * exercises the ghost-slot reads, the pack kernel and the overlapped halo ordering without
+ * a multi-GPU box (two RCCL ranks cannot share one GPU). */
 int fu_dist_create_local(int32_t n_local, int64_t e_local, const int64_t *rowptr,
                          const int32_t *col, const double *value, int32_t n_ghost_a,
                          int32_t nranks, int32_t rank, const int64_t *send_a_off,
                          const int32_t *send_a_idx, const int64_t *recv_a_off, int32_t device,
                          fu_handle **out);
 int fu_dist_exchange_local(fu_handle **hs, int32_t nranks);
+int fu_dist_run_local(fu_handle **hs, int32_t nranks, int32_t rounds);
 
 /* Partition-aware random geometric graph: rank `part` of `nparts` generates only its slab
  * of cell columns (plus the two halo columns) of the graph fu_graph_gen_rgg(n_total, radius,

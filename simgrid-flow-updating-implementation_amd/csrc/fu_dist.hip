@@ -32,7 +32,7 @@ extern "C" int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, co
 namespace {
 
 struct DistState {
-  ncclComm_t comm = nullptr;
+  ncclComm_t comm = nullptr;  // null: the in-process transport (fu_dist_create_local)
   int nranks = 0, rank = 0;
   int32_t n_local = 0;
   int64_t e_local = 0;
@@ -40,12 +40,17 @@ struct DistState {
   int *send_a_idx = nullptr;
   double *sbuf_a = nullptr;
   int64_t n_send_a = 0;
-  // every RCCL call goes on comm_stream (one stream per communicator): the halo of round r
-  // runs there beside round r's interior tiles, behind ev_bnd (boundary tiles done); the
-  // next round waits for ev_halo
+  // Both transports run the halo of round r on comm_stream beside round r's interior tiles:
+  // behind ev_bnd (boundary tiles done) the rank packs a_r of its boundary nodes there. RCCL
+  // then sends / receives in one group on that stream. The in-process transport records
+  // ev_packed instead, and fu_dist_exchange_local copies every peer's packed slots into this
+  // rank's ghost slots on this rank's comm_stream (after ev_packed of the peer). Either way
+  // ev_halo marks the ghost slots of a_r as written, and the next round waits for it.
   hipStream_t comm_stream = nullptr;
-  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr;
+  hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_packed = nullptr;
   bool halo_pending = false;
+  int64_t packed_round = -1;     // in-process transport: round whose packed halo awaits the exchange
+  int64_t exchanged_round = -1;  // in-process transport: last round whose halo was exchanged
 };
 
 __global__ void k_pack(long long cnt, const int *__restrict__ idx, const double *__restrict__ src,
@@ -64,6 +69,7 @@ extern "C" unsigned long long *fu__handle_err(fu_handle *h);
 extern "C" int fu__handle_device(fu_handle *h);
 extern "C" double *fu__handle_cur_a(fu_handle *h);
 extern "C" double *fu__handle_halo_a(fu_handle *h);
+extern "C" int64_t fu__handle_rounds(fu_handle *h);
 
 #define NCCL_TRY(expr)                                                                     \
   do {                                                                                     \
@@ -116,18 +122,20 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
     return FU_OK;
   }
   double *a = fu__handle_halo_a(h);
-  hipStream_t cs = d->comm ? d->comm_stream : s;
-  if (d->comm) {
-    HIPD_TRY(hipEventRecord(d->ev_bnd, s));
-    HIPD_TRY(hipStreamWaitEvent(cs, d->ev_bnd, 0));
-  }
+  hipStream_t cs = d->comm_stream;
+  HIPD_TRY(hipEventRecord(d->ev_bnd, s));
+  HIPD_TRY(hipStreamWaitEvent(cs, d->ev_bnd, 0));
   if (d->n_send_a > 0) {
     hipLaunchKernelGGL(k_pack, dim3((unsigned)((d->n_send_a + 255) / 256)), dim3(256), 0, cs,
                        (long long)d->n_send_a, d->send_a_idx, a, d->sbuf_a);
   }
   hipError_t he = hipGetLastError();
   if (he != hipSuccess) return fail(FU_ERR_HIP, std::string("halo pack: ") + hipGetErrorString(he));
-  if (!d->comm) return FU_OK;  // local transport: fu_dist_exchange_local moves the packed estimates
+  if (!d->comm) {  // in-process transport: fu_dist_exchange_local moves the packed estimates
+    HIPD_TRY(hipEventRecord(d->ev_packed, cs));
+    d->packed_round = fu__handle_rounds(h);  // the round being launched
+    return FU_OK;
+  }
   NCCL_TRY(ncclGroupStart());
   for (int p = 0; p < d->nranks; ++p) {
     if (p == d->rank) continue;
@@ -149,6 +157,7 @@ void fu__dist_free(fu_handle *h) {
   if (d->comm) ncclCommDestroy(d->comm);
   if (d->ev_bnd) hipEventDestroy(d->ev_bnd);
   if (d->ev_halo) hipEventDestroy(d->ev_halo);
+  if (d->ev_packed) hipEventDestroy(d->ev_packed);
   if (d->comm_stream) hipStreamDestroy(d->comm_stream);
   void *ptrs[] = {d->send_a_idx, d->sbuf_a};
   for (void *p : ptrs)
@@ -195,16 +204,17 @@ static int dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, 
     return bail(fail(FU_ERR_ALLOC, "fu_dist_create: halo buffers"));
   if (nsa && hipMemcpy(d->send_a_idx, send_a_idx, sizeof(int) * nsa, hipMemcpyHostToDevice) != hipSuccess)
     return bail(fail(FU_ERR_HIP, "fu_dist_create: upload halo plan"));
-  if (!unique_id) {  // fu_dist_create_local: no communicator (test transport). Kernel 4 pinned:
-    // an autotune pass would run rounds with no exchange between them
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_bnd, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess)
+    return bail(fail(FU_ERR_HIP, "fu_dist_create: communication stream"));
+  if (!unique_id) {  // fu_dist_create_local: no communicator (in-process transport). Kernel 4
+    // pinned: an autotune pass would run rounds with no exchange between them
     if (int rc = fu_set_option(h, "kernel", 4)) return bail(rc);
     *out = h;
     return FU_OK;
   }
-  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&d->ev_bnd, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess)
-    return bail(fail(FU_ERR_HIP, "fu_dist_create: communication stream"));
   ncclUniqueId id;
   std::memcpy(&id, unique_id, sizeof(id));
   ncclResult_t r = ncclCommInitRank(&d->comm, nranks, id, rank);
@@ -240,9 +250,16 @@ int fu_dist_create_local(int32_t n_local, int64_t e_local, const int64_t *rowptr
                      z.data(), send_a_off, send_a_idx, recv_a_off, nullptr, device, out);
 }
 
-// Test transport: the ranks of one process (handles on any devices of this process) swap
-// their packed boundary estimates with device copies, in the slot order RCCL would use.
+// In-process transport: the ranks of one process (handles on any devices of this process)
+// exchange the halo of the round every rank has just launched, asynchronously, through the
+// same comm_stream / event chain as RCCL. For every receiver q, on q's comm_stream: wait for
+// each sender's ev_packed, copy its packed slots into q's ghost slots (the slot order RCCL
+// uses), record q's ev_halo (q's next round waits for it). Then every sender's comm_stream
+// waits for the ev_halo of the receivers it feeds, so its next pack cannot overwrite sbuf_a
+// before they have copied it. No host synchronisation: many rounds can be queued per call
+// (fu_dist_run_local), and the copies run beside the interior tiles of the round.
 int fu_dist_exchange_local(fu_handle **hs, int32_t nranks) {
+  FU_TRY_BEGIN
   if (!hs || nranks < 1) return fail(FU_ERR_ARG, "fu_dist_exchange_local: bad arguments");
   std::vector<DistState *> ds(nranks);
   for (int p = 0; p < nranks; ++p) {
@@ -251,29 +268,53 @@ int fu_dist_exchange_local(fu_handle **hs, int32_t nranks) {
       return fail(FU_ERR_ARG, "fu_dist_exchange_local: handle " + std::to_string(p) + " is not local-transport rank " +
                                   std::to_string(p) + " of " + std::to_string(nranks));
   }
-  for (int p = 0; p < nranks; ++p) {  // every rank's pack has landed
-    if (hipSetDevice(fu__handle_device(hs[p])) != hipSuccess || hipStreamSynchronize(fu__handle_stream(hs[p])) != hipSuccess)
-      return fail(FU_ERR_HIP, "fu_dist_exchange_local: sync failed");
+  // every rank must have launched the same round r >= 0 and not yet exchanged its halo
+  const int64_t r = fu__handle_rounds(hs[0]) - 1;
+  for (int p = 0; p < nranks; ++p) {
+    if (fu__handle_rounds(hs[p]) - 1 != r || r < 0)
+      return fail(FU_ERR_STATE, "fu_dist_exchange_local: ranks have run different numbers of rounds (or none)");
+    if (ds[p]->packed_round != r || ds[p]->exchanged_round == r)
+      return fail(FU_ERR_STATE, "fu_dist_exchange_local: round " + std::to_string(r) + " of rank " +
+                                    std::to_string(p) + " has no packed halo pending");
   }
-  for (int q = 0; q < nranks; ++q) {
-    double *a = fu__handle_cur_a(hs[q]) + ds[q]->n_local;
-    for (int p = 0; p < nranks; ++p) {
-      if (p == q) continue;
-      const int64_t cnt = ds[p]->send_a_off[q + 1] - ds[p]->send_a_off[q];
-      if (cnt != ds[q]->recv_a_off[p + 1] - ds[q]->recv_a_off[p])
+  for (int q = 0; q < nranks; ++q)
+    for (int p = 0; p < nranks; ++p)
+      if (p != q && ds[p]->send_a_off[q + 1] - ds[p]->send_a_off[q] != ds[q]->recv_a_off[p + 1] - ds[q]->recv_a_off[p])
         return fail(FU_ERR_ARG, "fu_dist_exchange_local: halo plans of ranks " + std::to_string(p) + " and " +
                                     std::to_string(q) + " disagree");
-      // on the receiver's stream: a device-to-device hipMemcpy may return before the copy has
-      // landed, and the receiver's next round (its stream is non-blocking) would race it
-      if (cnt && (hipSetDevice(fu__handle_device(hs[q])) != hipSuccess ||
-                  hipMemcpyAsync(a + ds[q]->recv_a_off[p], ds[p]->sbuf_a + ds[p]->send_a_off[q], sizeof(double) * cnt,
-                                 hipMemcpyDefault, fu__handle_stream(hs[q])) != hipSuccess))
-        return fail(FU_ERR_HIP, "fu_dist_exchange_local: copy failed");
+  for (int q = 0; q < nranks; ++q) {
+    HIPD_TRY(hipSetDevice(fu__handle_device(hs[q])));
+    hipStream_t cs = ds[q]->comm_stream;
+    double *a = fu__handle_halo_a(hs[q]) + ds[q]->n_local;  // a_r of the round just launched
+    for (int p = 0; p < nranks; ++p) {
+      const int64_t cnt = p == q ? 0 : ds[q]->recv_a_off[p + 1] - ds[q]->recv_a_off[p];
+      if (!cnt) continue;
+      HIPD_TRY(hipStreamWaitEvent(cs, ds[p]->ev_packed, 0));
+      HIPD_TRY(hipMemcpyAsync(a + ds[q]->recv_a_off[p], ds[p]->sbuf_a + ds[p]->send_a_off[q], sizeof(double) * cnt,
+                              hipMemcpyDefault, cs));
     }
+    HIPD_TRY(hipEventRecord(ds[q]->ev_halo, cs));
+    ds[q]->halo_pending = true;
+    ds[q]->exchanged_round = r;
   }
-  for (int q = 0; q < nranks; ++q) {  // landed before any sender's next pack reuses its buffer
-    if (hipSetDevice(fu__handle_device(hs[q])) != hipSuccess || hipStreamSynchronize(fu__handle_stream(hs[q])) != hipSuccess)
-      return fail(FU_ERR_HIP, "fu_dist_exchange_local: sync failed");
+  for (int p = 0; p < nranks; ++p) {  // sbuf_a of p is free again once its receivers copied it
+    HIPD_TRY(hipSetDevice(fu__handle_device(hs[p])));
+    for (int q = 0; q < nranks; ++q)
+      if (q != p && ds[p]->send_a_off[q + 1] > ds[p]->send_a_off[q])
+        HIPD_TRY(hipStreamWaitEvent(ds[p]->comm_stream, ds[q]->ev_halo, 0));
+  }
+  return FU_OK;
+  FU_TRY_END
+}
+
+// `rounds` rounds of every rank of the in-process transport, each followed by its halo
+// exchange, all queued without a host synchronisation.
+int fu_dist_run_local(fu_handle **hs, int32_t nranks, int32_t rounds) {
+  if (!hs || nranks < 1 || rounds < 0) return fail(FU_ERR_ARG, "fu_dist_run_local: bad arguments");
+  for (int32_t k = 0; k < rounds; ++k) {
+    for (int p = 0; p < nranks; ++p)
+      if (int rc = fu_run_collectall(hs[p], 1, 0, nullptr)) return rc;
+    if (int rc = fu_dist_exchange_local(hs, nranks)) return rc;
   }
   return FU_OK;
 }

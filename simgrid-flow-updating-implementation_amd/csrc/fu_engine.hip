@@ -1713,6 +1713,17 @@ int dmalloc(T **p, size_t count) {
 
 }  // namespace
 
+// One round's launch context (state of round r-1 -> round r).
+struct RoundCtx {
+  int64_t r;
+  int fm;                     // flow mode: rounds 1, 2 compute the old flows instead of reading them
+  double *F;                  // F[r & 1]: f_{r-2} in, f_r out
+  const double *ap, *ap2;     // a_{r-1}, a_{r-2}
+  double *an;                 // a_r
+  unsigned long long *err;    // error slot (nullptr: no check)
+  bool plan;                  // a packing plan from a_{r-1} is still to run
+};
+
 // ======================================================================================
 // handle
 // ======================================================================================
@@ -1764,7 +1775,9 @@ struct fu_handle {
   bool pw_pending = false;
   int *pw_dev = nullptr;      // h_pw as the device sees it (the plan kernels write the width there)
   bool plan_pending = false;  // a packing plan is due before the next round (from its table)
-  int diag = 0;  // timing-only ablations (-DFU_DIAG builds only; wrong results)
+  // timing-only ablations (-DFU_DIAG builds: fu_set_option("diag", k); wrong results): the
+  // round body launch_body<k>; null = the product path
+  int (*diag_body)(fu_handle *, RoundCtx &) = nullptr;
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_col;
   // kernel 4 tiles per geometry (all four built up front so autotuning can switch between
@@ -2255,283 +2268,299 @@ inline unsigned tr_grid(fu_handle *h, int nbk) {
   return 8u * (unsigned)(h->tr_bpx > 0 ? std::min(per, h->tr_bpx) : per);
 }
 
+
+// the packing plan as a one-block launch ahead of the round (paths without a stage launch)
+void plan_alone(fu_handle *h, RoundCtx &c) {
+  if (!c.plan) return;
+  hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, c.ap, h->psample, h->pctl, h->pw_dev);
+  c.plan = false;
+}
+
+// Round 0 = the timeout fire on zero state (CA:33-34, CA:87-91): a_0 and a_{-1} = 0.0; no
+// flows are written (rounds 1 and 2 compute f_{-1} and f_0 themselves: fm).
+int launch_round0(fu_handle *h, RoundCtx &c) {
+  static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
+  hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
+                     h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
+  if (c.err)
+    hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
+                       h->a[0], h->target, c.err);
+  if (h->dist) {  // a_0 of the boundary nodes to the peers
+    h->halo_a = h->a[0];
+    if (int rc = fu__dist_round_hook(h, 2)) return rc;
+  }
+  return FU_OK;
+}
+
+// Kernel 8: k_stage (carrying the packing plan), heavy rows as kernel 4 tiles, then the light
+// tiles reading the staged estimates. D: timing-only ablations (FU_DIAG builds; 0 = product):
+// 1 = G read at the edge's own index, 2 = 1 without k_stage, 3 = 2 without the XCD tile
+// order, 4 = no k_stage, G read as usual.
+template <int D>
+int launch_k8(fu_handle *h, RoundCtx &c) {
+  constexpr bool C0 = false;
+  const int r1 = (int)(c.r & 1);
+  unsigned sgrid = 1;
+  const StageArgs sa = stage_args(h, &sgrid);
+  const void *cp = h->code[(c.r - 1) & 1];
+  if (h->st_ntiles && D < 2) {
+    hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap, cp,
+                       h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
+    c.plan = false;
+  }
+  plan_alone(h, c);
+  auto heavy = [&](auto chk) {
+    hipLaunchKernelGGL((k_round_recon<decltype(chk)::value, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy),
+                       dim3(kBlock), 0, h->stream, h->st_heavy, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
+                       h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr, c.fm);
+  };
+  if (h->st_nheavy) {
+    if (c.err && !D) heavy(std::true_type{});
+    else heavy(std::false_type{});
+  }
+  // light tiles: rounds 1 and 2 (fm) read no flows (RF = false); LO = staged indices first
+  auto light = [&](auto chk, auto rf, auto lo) {
+    hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, D, decltype(rf)::value,
+                                       decltype(lo)::value>),
+                       dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, h->st_tiles, h->st_ntiles, h->rowptr, h->col,
+                       sa, h->stG, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
+  };
+  auto light_lo = [&](auto chk, auto rf) {
+    if (h->staged_lo) light(chk, rf, std::true_type{});
+    else light(chk, rf, std::false_type{});
+  };
+  auto light_rf = [&](auto chk) {
+    if (c.fm) light_lo(chk, std::false_type{});
+    else light_lo(chk, std::true_type{});
+  };
+  if (h->st_ntiles) {
+    if (c.err && !D) light_rf(std::true_type{});
+    else light_rf(std::integral_constant<bool, C0>{});
+  }
+  return FU_OK;
+}
+
+// Kernel 9: k_stage -> k_transpose (the mega-hub buckets first) -> kernel 4's tiles reading
+// the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
+// the remaining buckets and tiles. D (FU_DIAG builds): 5 = hub chains skipped, 6 = the flow
+// pass of multi-chunk heavy rows skips its estimate reads, 20 = the staging passes alone,
+// 21 = the round tiles alone, 22 = no hub path, 23 = no k_stage, 24 = no k_transpose.
+template <int D>
+int launch_k9(fu_handle *h, RoundCtx &c) {
+  if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
+  const double *Gb = h->tr.GB;
+  if (!Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
+  const int r1 = (int)(c.r & 1);
+  const void *cp = h->code[(c.r - 1) & 1];
+  const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
+  // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
+  const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
+  const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
+  const int4 *tl = h->tiles_geo[1];
+  const bool hubs = nmega && D != 22;
+  StageArgs sa{};
+  for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
+  sa.P[3] = h->tr.P;
+  sa.Q[3] = h->tr.Q;
+  sa.SN[3] = kStageLds / 8;
+  sa.NB[3] = h->tr.NB;
+  sa.brange[3] = h->tr.brange;
+  sa.colS[3] = h->tr.colS;
+  sa.f64 = 1;
+  if (D != 21 && D != 23) {
+    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap,
+                       cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
+    c.plan = false;
+  }
+  plan_alone(h, c);
+  const int bh = hubs ? h->tr.Bh : 0;
+  if (D != 21 && D != 24 && bh)
+    hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
+                       (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+  if (hubs) {
+    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+  }
+  if (D != 21 && D != 24 && h->tr.B > bh)
+    hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh, h->tr.B - bh,
+                       h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+  const bool chk = c.err && !D;
+  if (hubs) {
+    auto chains = [&](auto C) {
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
+                         0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm);
+    };
+    if (chk) chains(std::true_type{});
+    else chains(std::false_type{});
+    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
+                       (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+  }
+  // heavy tiles [t0, t1) with RL register elements per lane; DH = the heavy-row ablation
+  constexpr int DH = (D == 5 || D == 6) ? D : 0;
+  auto heavy = [&](auto C, auto RL, int t0, int t1) {
+    if (t1 > t0)
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, DH, 1024, 128, 2, true, decltype(RL)::value>),
+                         dim3(t1 - t0), dim3(kBlock), 0, h->stream, tl + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
+                         c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
+                         c.fm);
+  };
+  auto tiles = [&](auto C) {
+    heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
+    heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
+    heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
+    if (nl)
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+                         h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
+  };
+  if (D != 20) {
+    if (chk) tiles(std::true_type{});
+    else tiles(std::false_type{});
+  }
+  HIP_TRY(hipGetLastError());
+  if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  return FU_OK;
+}
+
+// Kernel 4: heavy tiles (mega hubs, heavy rows) lead the tile list; with fork_heavy they run
+// on the side stream beside the light tiles' launch (which keeps kernel 4's light-path
+// register budget). Multi-GPU: the heavy tiles stay on the main stream, then the boundary
+// light tiles, then the halo goes out beside the interior light tiles. D (FU_DIAG builds):
+// 1 = the gather replaced by a coalesced read, 2 = no flow load/store, 3 / 4 = the gather
+// folded into n/2 / n/4 estimates, 5 = hub chains skipped, 6 = the heavy flow pass without
+// its gathers, 12 = 1 and 2.
+template <int TE, int TN, int D>
+int launch_k4_geo(fu_handle *h, RoundCtx &c) {
+  const int r1 = (int)(c.r & 1);
+  const void *cp = h->code[(c.r - 1) & 1];
+  const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
+  const int hub_sep = h->n_hub ? 1 : 0;  // k_hub_flows writes the hubs' flows after the chains
+  const int nb = h->nbound_geo[h->geo];  // boundary light tiles (multi-GPU), then the interior
+  const bool fork = nh > 0 && h->fork_heavy && !h->dist;
+  hipStream_t hs = fork ? h->stream2 : h->stream;
+  // with mega hubs, only their tiles go to the side stream (k_hub_stage -> chains ->
+  // k_hub_flows), so the other heavy tiles need not wait for k_hub_stage
+  const int nmh = fork && h->n_hub && h->split_hubs ? h->n_hub : nh;
+  const int4 *tiles = h->tiles_geo[h->geo];
+  if (fork) {
+    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
+  }
+  if (h->n_hub)
+    hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
+                       (long long)h->hub_total, h->col, c.F, c.ap, c.ap2, cp, h->pctl, r1, h->hubxy, c.fm, h->hub_blk);
+  constexpr int DH = (D == 5 || D == 6) ? D : 0;
+  auto heavy = [&](auto C, hipStream_t st, int t0, int cnt) {
+    if (cnt)
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, DH, TE, TN, 2>), dim3(cnt), dim3(kBlock), 0, st,
+                         tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp, h->code[r1],
+                         h->pctl, r1, h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, c.fm);
+  };
+  // light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
+  auto light = [&](auto C, auto NT, auto RF, int t0, int cnt) {
+    if (cnt)
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, decltype(NT)::value, D, TE, TN, 1, false, kHeavyRL,
+                                        decltype(RF)::value>),
+                         dim3(cnt), dim3(kBlock), 0, h->stream, tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
+                         c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr,
+                         c.fm);
+  };
+  auto light_rf = [&](auto C, auto NT, int t0, int cnt) {
+    if (c.fm) light(C, NT, std::false_type{}, t0, cnt);
+    else light(C, NT, std::true_type{}, t0, cnt);
+  };
+  auto body = [&](auto C, auto NT) -> int {
+    heavy(C, hs, 0, nmh);             // mega hubs (or every heavy tile) on the side stream
+    heavy(C, h->stream, nmh, nh - nmh);  // the other heavy tiles ahead of the light ones
+    light_rf(C, NT, nh, nb);
+    if (h->dist) {  // boundary rows done: their estimates go out beside the interior tiles
+      h->halo_a = c.an;
+      if (int rc = fu__dist_round_hook(h, 2)) return rc;
+    }
+    light_rf(C, NT, nh + nb, nl - nb);
+    return FU_OK;
+  };
+  int rc;
+  if (D) rc = body(std::false_type{}, std::false_type{});
+  else if (c.err) rc = h->nt ? body(std::true_type{}, std::true_type{}) : body(std::true_type{}, std::false_type{});
+  else rc = h->nt ? body(std::false_type{}, std::true_type{}) : body(std::false_type{}, std::false_type{});
+  if (rc) return rc;
+  if (hub_sep)
+    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
+                       (long long)h->hub_total, h->hubxy, c.an, c.F, nullptr, nullptr, c.fm, h->hub_blk);
+  if (fork) {
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  }
+  return FU_OK;
+}
+
+template <int D>
+int launch_k4(fu_handle *h, RoundCtx &c) {
+  plan_alone(h, c);
+  if (h->geo == 0) return launch_k4_geo<2048, 256, D>(h, c);
+  if (h->geo == 2) return launch_k4_geo<1024, 256, D>(h, c);
+  if (h->geo == 1) return launch_k4_geo<1024, 128, D>(h, c);
+  return launch_k4_geo<512, 64, D>(h, c);
+}
+
+// The round body of rounds >= 1 for the handle's kernel (D = 0: the product path).
+template <int D>
+int launch_body(fu_handle *h, RoundCtx &c) {
+  if (h->kernel == 8) return launch_k8<D>(h, c);
+  if (h->kernel == 9) return launch_k9<D>(h, c);
+  return launch_k4<D>(h, c);
+}
+
+#ifdef FU_DIAG
+// -DFU_DIAG builds: fu_set_option("diag", k) selects launch_body<k> (timing only, WRONG results)
+int (*diag_body(int k))(fu_handle *, RoundCtx &) {
+  switch (k) {
+    case 1: return launch_body<1>;
+    case 2: return launch_body<2>;
+    case 3: return launch_body<3>;
+    case 4: return launch_body<4>;
+    case 5: return launch_body<5>;
+    case 6: return launch_body<6>;
+    case 12: return launch_body<12>;
+    case 20: return launch_body<20>;
+    case 21: return launch_body<21>;
+    case 22: return launch_body<22>;
+    case 23: return launch_body<23>;
+    case 24: return launch_body<24>;
+    default: return nullptr;
+  }
+}
+#endif
+
 // One round: state of round r-1 -> round r. err_slot: nullptr = no check.
 int launch_round(fu_handle *h, unsigned long long *err_slot) {
-  const bool check = err_slot != nullptr;
   if (h->dist) {
     if (int rc = fu__dist_round_hook(h, 0)) return rc;
   }
   const int64_t r = h->rounds;
-  const int fm = r == 1 ? 1 : r == 2 ? 2 : 0;  // rounds 1, 2: the old flows are computed, not read
+  RoundCtx c;
+  c.r = r;
+  c.fm = r == 1 ? 1 : r == 2 ? 2 : 0;  // rounds 1, 2: the old flows are computed, not read
+  c.F = h->f[r & 1];
+  c.ap = r > 0 ? h->a[(r - 1) % 3] : nullptr;
+  c.ap2 = h->a[(r + 1) % 3];
+  c.an = h->a[r % 3];
+  c.err = err_slot;
   // a packing plan due from a_{r-1}: the stage launch of kernels 8 and 9 carries it (one more
   // block); every other path runs it first as a launch of its own
-  bool plan = h->plan_pending && r > 0;
+  c.plan = h->plan_pending && r > 0;
   h->plan_pending = false;
-  const bool plan_done = plan;
-  auto plan_alone = [&]() {
-    if (!plan) return;
-    hipLaunchKernelGGL(k_pack_plan, dim3(1), dim3(kBlock), 0, h->stream, h->a[(r - 1) % 3], h->psample, h->pctl,
-                       h->pw_dev);
-    plan = false;
-  };
-  if (h->kernel != 8 && h->kernel != 9) plan_alone();
-  if (r == 0) {
-    // round 0 = the timeout fire on zero state (CA:33-34, CA:87-91): a_0 and a_{-1} = 0.0;
-    // no flows are written (rounds 1 and 2 compute f_{-1} and f_0 themselves: fm)
-    static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
-    hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
-                       h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
-    if (check)
-      hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
-                         h->a[0], h->target, err_slot);
-    if (h->dist) {  // a_0 of the boundary nodes to the peers
-      h->halo_a = h->a[0];
-      if (int rc = fu__dist_round_hook(h, 2)) return rc;
-    }
-  } else if (h->kernel == 8) {
-    double *F = h->f[r & 1];
-    const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-    double *an = h->a[r % 3];
-    unsigned sgrid = 1;
-    const StageArgs sa = stage_args(h, &sgrid);
-    const void *cp = h->code[(r - 1) & 1];
-#ifdef FU_DIAG
-    const bool stage = h->diag < 2;
-#else
-    const bool stage = true;
-#endif
-    if (h->st_ntiles && stage) {
-      hipLaunchKernelGGL(k_stage, dim3(sgrid + (plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, ap, cp,
-                         h->pctl, (int)(r & 1), h->stG, plan ? h->psample : nullptr, h->pw_dev);
-      plan = false;
-    }
-    plan_alone();
-    if (h->st_nheavy) {
-      if (check)
-        hipLaunchKernelGGL((k_round_recon<true, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
-                           h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr, fm);
-      else
-        hipLaunchKernelGGL((k_round_recon<false, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy), dim3(kBlock), 0,
-                           h->stream, h->st_heavy, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                           cp, h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, nullptr, fm);
-    }
-#define FU_STAGED_RF(C, D, RF)                                                                            \
-  if (h->staged_lo) FU_STAGED_RFL(C, D, RF, true); else FU_STAGED_RFL(C, D, RF, false)
-#define FU_STAGED_RFL(C, D, RF, LO)                                                                       \
-  hipLaunchKernelGGL((k_round_staged<C, kStageTE, kStageTN, D, RF, LO>), dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, \
-                     h->st_tiles, h->st_ntiles, h->rowptr, h->col, sa, h->stG, h->v, F, ap, ap2, an, h->target, \
-                     err_slot, h->code[r & 1], h->pctl, (int)(r & 1), fm)
-#define FU_STAGED(C, D)                                                                                  \
-  do {                                                                                                    \
-    if (fm) FU_STAGED_RF(C, D, false);                                                                    \
-    else FU_STAGED_RF(C, D, true);                                                                        \
-  } while (0)
-    if (h->st_ntiles) {
-#ifdef FU_DIAG
-      if (h->diag == 4) FU_STAGED(false, 4);
-      else if (h->diag == 3) FU_STAGED(false, 3);
-      else if (h->diag) FU_STAGED(false, 1);
-      else
-#endif
-      if (check) FU_STAGED(true, 0);
-      else FU_STAGED(false, 0);
-    }
-#undef FU_STAGED
-#undef FU_STAGED_RF
-#undef FU_STAGED_RFL
-  } else {
-    double *F = h->f[r & 1];
-    const double *ap = h->a[(r - 1) % 3], *ap2 = h->a[(r + 1) % 3];
-    double *an = h->a[r % 3];
-    const bool pre = h->kernel == 9;  // kernel 9: stage + transpose, then kernel 4 reading Gb
-    if (pre) {
-      if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
-    }
-    const double *Gb = pre ? h->tr.GB : nullptr;
-    if (pre && !Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
-    if (pre) {
-      // the mega hubs' chains read the pre-gathered estimates too: the buckets holding them
-      // are transposed first, then the chains (and k_hub_flows) run on the side stream
-      // beside the remaining buckets and the other tiles
-      const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
-      // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
-      const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-      const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
-      const int4 *tl = h->tiles_geo[1];
-#ifdef FU_DIAG
-      const bool hubs = nmega && h->diag != 22;  // 22: timing without the hub path
-#else
-      const bool hubs = nmega;
-#endif
-      StageArgs sa{};
-      for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
-      sa.P[3] = h->tr.P;
-      sa.Q[3] = h->tr.Q;
-      sa.SN[3] = kStageLds / 8;
-      sa.NB[3] = h->tr.NB;
-      sa.brange[3] = h->tr.brange;
-      sa.colS[3] = h->tr.colS;
-      sa.f64 = 1;
-#ifdef FU_DIAG
-      if (h->diag != 21 && h->diag != 23)
-#endif
-      {
-        hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, ap,
-                           h->code[(r - 1) & 1], h->pctl, (int)(r & 1), h->tr.GA, plan ? h->psample : nullptr,
-                           h->pw_dev);
-        plan = false;
-      }
-      plan_alone();
-      const int bh = hubs ? h->tr.Bh : 0;
-#ifdef FU_DIAG
-      if (h->diag != 21 && h->diag != 24)
-#endif
-      {
-        if (bh)
-          hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
-                             (long long)h->E,
-                             h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
-        if (hubs) {
-          HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-          HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-        }
-        if (h->tr.B > bh)
-          hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh,
-                             h->tr.B - bh, h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
-      }
-      if (hubs) {
-        if (check)
-          hipLaunchKernelGGL((k_round_recon<true, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
-                             h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
-                             1, Gb, fm);
-        else
-          hipLaunchKernelGGL((k_round_recon<false, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock), 0,
-                             h->stream2, tl, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,
-                             h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, h->hrows,
-                             1, Gb, fm);
-        hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub,
-                           h->hub_rows, (long long)h->hub_total, nullptr, an, F, Gb, ap2, fm, h->hub_blk);
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
-      }
-#define FU_PRE_H(C, D, RL, t0, t1)                                                                         \
-  if ((t1) > (t0))                                                                                        \
-    hipLaunchKernelGGL((k_round_recon<C, false, D, 1024, 128, 2, true, RL>), dim3((t1) - (t0)), dim3(kBlock), 0, \
-                       h->stream, tl + (t0), h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,    \
-                       h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,      \
-                       h->hrows, 1, Gb, fm)
-#define FU_PRE(C, D)                                                                                      \
-  do {                                                                                                    \
-    FU_PRE_H(C, D, kHeavyRL, nmega, m0);                                                                  \
-    FU_PRE_H(C, D, kMidRL, m0, m1);                                                                       \
-    FU_PRE_H(C, D, kHeavyRL, m1, nh);                                                                     \
-    if (nl)                                                                                               \
-      hipLaunchKernelGGL((k_round_recon<C, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, h->stream, \
-                         tl + nh, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
-                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr,        \
-                         nullptr, 0, Gb, fm);                                                                 \
-  } while (0)
-#ifdef FU_DIAG
-      if (h->diag == 20) {  // timing: the staging passes alone
-      } else if (h->diag == 5) FU_PRE(false, 5);
-      else if (h->diag == 6) FU_PRE(false, 6);
-      else
-#endif
-      if (check) FU_PRE(true, 0);
-      else FU_PRE(false, 0);
-#undef FU_PRE
-#undef FU_PRE_H
-      HIP_TRY(hipGetLastError());
-      if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-    } else {
-    // heavy tiles (hubs, heavy rows) lead the tile list: they run as their own launch on the
-    // side stream, concurrently with the light tiles' launch (which then keeps kernel 4's
-    // light-path register budget)
-    const int nh = h->nheavy_geo[h->geo], nl = h->ntiles_geo[h->geo] - nh;
-    const int hub_sep = h->n_hub ? 1 : 0;  // k_hub_flows writes the hubs' flows after the chains
-    const int nb = h->nbound_geo[h->geo];  // boundary light tiles (multi-GPU), then the interior
-    // multi-GPU: heavy tiles stay on the main stream, ahead of the boundary tiles and the halo
-    const bool fork = nh > 0 && h->fork_heavy && !h->dist;
-    hipStream_t hs = fork ? h->stream2 : h->stream;
-    // with mega hubs, only their tiles go to the side stream (k_hub_stage -> chains ->
-    // k_hub_flows), so the other heavy tiles need not wait for k_hub_stage
-    const int nmh = fork && h->n_hub && h->split_hubs ? h->n_hub : nh;
-    if (fork) {
-      HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
-      HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
-    }
-    if (h->n_hub)
-      hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, h->col, F, ap, ap2, h->code[(r - 1) & 1], h->pctl, (int)(r & 1),
-                         h->hubxy, fm, h->hub_blk);
-// light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
-#define FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, RF)                                                         \
-  hipLaunchKernelGGL((k_round_recon<C, N, D, TE, TN, 1, false, kHeavyRL, RF>), dim3(cnt), dim3(kBlock), 0,     \
-                     h->stream, tp, h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot,              \
-                     h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), nullptr, nullptr, nullptr, 0, \
-                     nullptr, fm)
-#define FU_LIGHT(C, N, D, TE, TN, cnt, tp)                                                                \
-  do {                                                                                                    \
-    if (fm) FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, false);                                                 \
-    else FU_LIGHT_RF(C, N, D, TE, TN, cnt, tp, true);                                                     \
-  } while (0)
-#define FU_RECON_G(C, N, D, TE, TN)                                                                   \
-  do {                                                                                                    \
-    if (nmh)  /* mega hubs (or every heavy tile) on the side stream */                                   \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nmh), dim3(kBlock), 0, \
-                         hs, h->tiles_geo[h->geo], h->rowptr, h->col, h->v, F, ap, ap2, an, h->target, err_slot, \
-                         h->code[(r - 1) & 1], h->code[r & 1], h->pctl, (int)(r & 1), h->hubxy, h->hub_off,    \
-                         h->hrows, hub_sep, nullptr, fm);                                                        \
-    if (nh - nmh)  /* the other heavy tiles ahead of the light ones on the main stream */                \
-      hipLaunchKernelGGL((k_round_recon<C, false, (D == 5 || D == 6 ? D : 0), TE, TN, 2>), dim3(nh - nmh),  \
-                         dim3(kBlock), 0, h->stream, h->tiles_geo[h->geo] + nmh, h->rowptr, h->col, h->v, F, ap, \
-                         ap2, an, h->target, err_slot, h->code[(r - 1) & 1], h->code[r & 1], h->pctl,          \
-                         (int)(r & 1), h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, fm);                       \
-    if (nb) FU_LIGHT(C, N, D, TE, TN, nb, h->tiles_geo[h->geo] + nh);                                    \
-    if (h->dist) {  /* boundary rows done: their estimates go out beside the interior tiles */          \
-      h->halo_a = an;                                                                                     \
-      if (int rc = fu__dist_round_hook(h, 2)) return rc;                                                  \
-    }                                                                                                     \
-    if (nl - nb) FU_LIGHT(C, N, D, TE, TN, nl - nb, h->tiles_geo[h->geo] + nh + nb);                     \
-  } while (0)
-#define FU_RECON(C, N, D)                                                                                 \
-  do {                                                                                                    \
-    if (h->geo == 0) FU_RECON_G(C, N, D, 2048, 256);                                          \
-    else if (h->geo == 2) FU_RECON_G(C, N, D, 1024, 256);                                          \
-    else if (h->geo == 1) FU_RECON_G(C, N, D, 1024, 128);                                          \
-    else FU_RECON_G(C, N, D, 512, 64);                                                             \
-  } while (0)
-#ifdef FU_DIAG
-    if (h->diag == 1) FU_RECON(false, false, 1);
-    else if (h->diag == 2) FU_RECON(false, false, 2);
-    else if (h->diag == 3) FU_RECON(false, false, 3);
-    else if (h->diag == 4) FU_RECON(false, false, 4);
-    else if (h->diag == 5) FU_RECON(false, false, 5);
-    else if (h->diag == 6) FU_RECON(false, false, 6);
-    else if (h->diag == 12) FU_RECON(false, false, 12);
-    else
-#endif
-    if (check) {
-      if (h->nt) FU_RECON(true, true, 0); else FU_RECON(true, false, 0);
-    } else {
-      if (h->nt) FU_RECON(false, true, 0); else FU_RECON(false, false, 0);
-    }
-#undef FU_RECON
-#undef FU_RECON_G
-#undef FU_LIGHT
-#undef FU_LIGHT_RF
-    if (hub_sep)
-      hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, h->hubxy, an, F, nullptr, nullptr, fm, h->hub_blk);
-    if (fork) {
-      HIP_TRY(hipGetLastError());
-      HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
-      HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
-    }
-    }  // kernel 4
-  }
+  const bool plan_done = c.plan;
+  int rc;
+  if (r == 0) rc = launch_round0(h, c);
+  else if (h->diag_body) rc = h->diag_body(h, c);
+  else rc = launch_body<0>(h, c);
+  if (rc) return rc;
   HIP_TRY(hipGetLastError());
   if (plan_done && !h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
     HIP_TRY(hipEventRecord(h->ev_pw, h->stream));
@@ -2770,7 +2799,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "diag")) {  // timing-only ablations (wrong results): tools builds only
 #ifdef FU_DIAG
-    h->diag = (int)value;
+    if (value && !diag_body((int)value)) return fail(FU_ERR_ARG, "fu_set_option: unknown diag");
+    h->diag_body = value ? diag_body((int)value) : nullptr;
     return FU_OK;
 #else
     (void)value;
@@ -3027,6 +3057,9 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
   if (int rc = set_device(h)) return rc;
   HIP_TRY(hipEventRecord(h->ev2, h->stream));
   if (int rc = run_rounds(h, rounds, 0, 0)) return rc;
+  if (h->dist) {  // the last round's halo (comm stream) inside the timed window
+    if (int rc = fu__dist_round_hook(h, 0)) return rc;
+  }
   HIP_TRY(hipEventRecord(h->ev3, h->stream));
   HIP_TRY(hipEventSynchronize(h->ev3));
   HIP_TRY(hipEventElapsedTime(ms, h->ev2, h->ev3));
@@ -3055,6 +3088,9 @@ int fu_mark(fu_handle *h, int32_t slot) {
   if (!h || slot < 0 || slot >= 64) return fail(FU_ERR_ARG, "fu_mark: slot must be in [0, 64)");
   if (int rc = set_device(h)) return rc;
   if (!h->marks[slot]) HIP_TRY(hipEventCreate(&h->marks[slot]));
+  if (h->dist) {  // a mark after a round includes that round's halo (comm stream)
+    if (int rc = fu__dist_round_hook(h, 0)) return rc;
+  }
   HIP_TRY(hipEventRecord(h->marks[slot], h->stream));
   return FU_OK;
 }
@@ -3544,5 +3580,6 @@ unsigned long long *fu__handle_err(fu_handle *h) { return h->err; }
 int fu__handle_device(fu_handle *h) { return h->device; }
 double *fu__handle_cur_a(fu_handle *h) { return cur_a(h); }
 double *fu__handle_halo_a(fu_handle *h) { return h->halo_a; }
+int64_t fu__handle_rounds(fu_handle *h) { return h->rounds; }
 
 }

@@ -92,6 +92,7 @@ _SIGS = {
     "fu_replay_set_option": ([vp, cp, i64], ctypes.c_int),
     "fu_dist_create_local": ([i32, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, i32, P(vp)], ctypes.c_int),
     "fu_dist_exchange_local": ([vp, i32], ctypes.c_int),
+    "fu_dist_run_local": ([vp, i32, i32], ctypes.c_int),
     "fu_part_gen_rgg": ([i64, f64, u64, i32, i32, P(vp)], ctypes.c_int),
     "fu_part_info": ([vp, vp], ctypes.c_int),
     "fu_part_export": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),

@@ -293,10 +293,10 @@ class DistCollectAll:
 
 
 def run_local(engines, rounds: int):
-    """Local test transport: `rounds` rounds of every rank (DistCollectAll(..., uid=None)),
-    one round at a time, each followed by fu_dist_exchange_local."""
+    """In-process transport: `rounds` rounds of every rank (DistCollectAll(..., uid=None)),
+    each followed by its halo exchange (fu_dist_run_local). Everything is queued
+    asynchronously on the ranks' main and comm streams, as with RCCL: the copies into the
+    ghost slots run beside each round's interior tiles, and no host sync happens between
+    rounds."""
     arr = (ctypes.c_void_p * len(engines))(*[e._h.value for e in engines])
-    for _ in range(rounds):
-        for e in engines:
-            L.call("fu_run_collectall", e._h, 1, 0, None)
-        L.call("fu_dist_exchange_local", arr, len(engines))
+    L.call("fu_dist_run_local", arr, len(engines), int(rounds))

@@ -267,9 +267,10 @@ def test_dist_single_rank_rccl_matches_engine():
 @pytest.mark.parametrize("kind", ["rgg", "er"])
 def test_dist_ghost_slots_local_transport_bitwise(world, kind):
     """Every rank of a partitioned graph as its own handle on GPU 0, the halo moved by the
-    test transport (device copies in RCCL's slot order): the round kernels read ghost slots
-    (col >= n_local), k_pack packs non-empty send lists. Gathered estimates and flows equal
-    the C oracle bitwise. ER cuts most edges (every rank talks to every rank)."""
+    in-process transport through the RCCL path's comm-stream / event chain (pack on the comm
+    stream behind the boundary tiles, copies into the peers' ghost slots beside the interior
+    tiles, the next round behind ev_halo), 100 rounds queued with no host sync. Estimates and
+    flows equal the C oracle bitwise. ER cuts most edges (every rank talks to every rank)."""
     from fu.dist import DistCollectAll, partition, run_local
 
     if kind == "rgg":
@@ -280,12 +281,69 @@ def test_dist_ghost_slots_local_transport_bitwise(world, kind):
     plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
     assert all(p.n_ghost_a > 0 and len(p.send_a_idx) > 0 for p in plans)
     engs = [DistCollectAll(p, v[p.lo:p.hi], None) for p in plans]
-    rounds = 25
+    rounds = 100
     run_local(engs, rounds)
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
     for p, e in zip(plans, engs):
         assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), p.rank
         assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), p.rank
+    for e in engs:
+        e.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("geo", [(1024, 0), (2048, 0), (512, 0)])
+def test_dist_rmat_heavy_rows_and_hubs_with_ghosts_bitwise(world, geo):
+    """Partitioned R-MAT (scale 14) on the in-process transport with hub_threshold 32 and
+    mega_hub 256: hundreds of heavy rows and mega hubs per rank have ghost columns, so the
+    heavy tiles, k_hub_stage (gathers through col into ghost slots), the hub chains and
+    k_hub_flows all read halo estimates. 100 rounds bitwise against the C oracle."""
+    from fu.dist import DistCollectAll, partition, run_local
+
+    g = fu.Graph.rmat(14, 16, seed=3)
+    v = fu.uniform_values(g.n, seed=4)
+    plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
+    engs = []
+    for p in plans:
+        e = DistCollectAll(p, v[p.lo:p.hi], None)
+        for key, val in (("hub_threshold", 32), ("mega_hub", 256), ("tile_edges", geo[0])):
+            fu._lib.call("fu_set_option", e._h, key.encode(), val)
+        ld = np.diff(p.rowptr)
+        ghost = [(p.col[p.rowptr[i]:p.rowptr[i + 1]] >= p.n_local).any() for i in range(p.n_local)]
+        assert sum(1 for i in range(p.n_local) if ld[i] > 256 and ghost[i]) > 50  # mega hubs at the cut
+        engs.append(e)
+    assert all(e.info()["mega_hubs"] > 0 for e in engs)
+    rounds = 100
+    run_local(engs, rounds)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
+    for p, e in zip(plans, engs):
+        assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), p.rank
+        assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), p.rank
+    for e in engs:
+        e.close()
+
+
+def test_dist_exchange_local_checks_round_counts():
+    """fu_dist_exchange_local refuses ranks that ran different numbers of rounds, no round,
+    or a round whose halo was already exchanged (it would copy into the wrong generation)."""
+    import ctypes
+
+    from fu.dist import DistCollectAll, partition
+
+    g = fu.Graph.erdos_renyi(20_000, 80_000, seed=2)
+    v = fu.uniform_values(g.n, seed=2)
+    plans = [partition(g.rowptr, g.col, g.rev, 2, r) for r in range(2)]
+    engs = [DistCollectAll(p, v[p.lo:p.hi], None) for p in plans]
+    arr = (ctypes.c_void_p * 2)(*[e._h.value for e in engs])
+    with pytest.raises(fu.FuError, match="different numbers of rounds"):
+        fu._lib.call("fu_dist_exchange_local", arr, 2)  # no round yet
+    engs[0].run(1)
+    with pytest.raises(fu.FuError, match="different numbers of rounds"):
+        fu._lib.call("fu_dist_exchange_local", arr, 2)
+    engs[1].run(1)
+    fu._lib.call("fu_dist_exchange_local", arr, 2)
+    with pytest.raises(fu.FuError, match="no packed halo pending"):
+        fu._lib.call("fu_dist_exchange_local", arr, 2)
     for e in engs:
         e.close()
 
