@@ -181,12 +181,9 @@ def round_kernels(kinfo):
         return "k_round_recon %dx%d%s" % (kinfo["tile"][0], kinfo["tile"][1], "+nt" if kinfo["nt"] else "")
     if k == "stage":
         return "k_stage + k_round_staged 1024x128"
-    if k == "pipe_stage":
-        return "k_stage + k_round_pipe<staged> 1024x128"
-    if k == "pipe":
-        return "k_round_pipe<recon> 1024x128"
-    if k == "split2":
-        return "k_gather_part0 + k_round_split"
+    if k == "pregather":
+        return ("k_stage + k_transpose (hub buckets, rest) + k_round_recon<PRE> 1024x128 (heavy rows, "
+                "register-resident rows, light tiles) + mega-hub chains + k_hub_flows (side stream)")
     return k
 
 
@@ -251,16 +248,10 @@ def run_single(args, wl):
     kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
     roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, args.steps), round_kernels(kinfo))
 
-    rounds_to = final_err = n_comp = None
+    conv = {"rounds_to_1e-9": None, "err_after_conv_rounds": None, "conv_rounds": None,
+            "components": None}
     if not args.no_conv:  # rounds to 1e-9 vs the per-component means (untimed)
-        tgt, comp = fu.component_means(g.rowptr, g.col, v)
-        eng.reset()
-        eng.set_targets(tgt)
-        tr = eng.run(args.conv_rounds, err_every=1)
-        below = np.nonzero(tr < 1e-9)[0]
-        rounds_to = int(below[0]) + 1 if len(below) else None
-        final_err = float(tr[-1])
-        n_comp = int(comp.max()) + 1
+        conv = convergence(eng, g.rowptr, g.col, v, args.conv_rounds)
     cpu = cpu_baseline(g, v, args.cpu_seconds) if args.cpu_seconds > 0 else None
     out = {
         "metric": METRIC, "value": value, "unit": "edge-updates/s", "n_gpus": 1,
@@ -277,12 +268,51 @@ def run_single(args, wl):
             "pack_width_after": pack_after, "setup_s": t_setup, "phases": phases,
             "parallelism": "single GPU",
         },
-        "roofline": roof, "cpu_baseline": cpu, "rounds_to_1e-9": rounds_to,
-        "err_after_conv_rounds": final_err, "conv_rounds": args.conv_rounds,
-        "components": n_comp, "graph_gen_s": t_gen,
+        "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen,
     }
+    out.update(conv)
     print(json.dumps(out), flush=True)
     eng.close()
+
+
+def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_total, per, kinfo,
+              halo_us, round_us, t_gen, conv):
+    """The N > 1 (rgg-dist) JSON line. Per GPU and round the algorithmic bytes are the §8(d)
+    figure of the rank's rows (24 E + 28 N) plus the halo: 8 B per ghost estimate received
+    (the RCCL payload written into the ghost slots; halo = ghost slots over all ranks)."""
+    alg = (24 * e_tot + 28 * n_tot + 8 * halo) // world  # per GPU, per round
+    r1 = dev1_ms / max(1, steps - 1)
+    achieved = alg / (r1 * 1e-3) / 1e9
+    line = {
+        "metric": METRIC, "value": e_tot * steps / wall, "unit": "edge-updates/s",
+        "n_gpus": world, "steps": steps, "warmup": warmup,
+        "ms_per_step": wall * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded RGG, U[0,100) values)",
+        "config": {"workload": f"rgg-dist:n={n_total} ({per} per GPU), deg=8, x-slabs, "
+                               "RCCL estimates-only halo every round",
+                   "n_total": n_total, "E_directed": e_tot,
+                   "rounds_timed": f"0-{steps - 1} from the zero state",
+                   "kernel_selected": kinfo["kernel"], "tile_selected": kinfo["tile"],
+                   "halo_estimates_per_round": halo, "halo_bytes_per_round": 8 * halo,
+                   "parallelism": f"graph partition x{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "per_gpu": True,
+                     "alg_bytes_per_launch": alg, "avg_launch_us": r1 * 1e3,
+                     "kernel": "k_round_recon (heavy, boundary tiles) -> k_pack + RCCL group on the "
+                               "comm stream beside the interior tiles",
+                     "launch_window": f"rounds 1-{steps - 1}, max over ranks, the last halo included"},
+        # halo: device time on the comm stream from the start of the pack (boundary tiles
+        # done) to the ghost slots written, max over ranks; it overlaps the interior tiles
+        "halo": {"us_per_round": halo_us, "share_of_round": (halo_us / round_us) if round_us else None,
+                 "overlapped_with": "interior tiles of the same round",
+                 "sample": "20 rounds after the timed region, one halo read per round"},
+        "cpu_baseline": None,
+        "cpu_baseline_note": "reported on the N = 1 line only (rank 0 at N = 1)",
+        "graph_gen_s": t_gen,
+        "value_per_gpu": e_tot * steps / wall / world,
+    }
+    line.update(conv)
+    return line
 
 
 def run_dist(args, world, rank, local, dist):
@@ -291,6 +321,7 @@ def run_dist(args, world, rank, local, dist):
     with the estimates-only RCCL halo. value = all ranks' edge updates / max-over-ranks time."""
     import torch
 
+    import fu
     from fu.dist import DistCollectAll, RggPart, unique_id
 
     per = args.n or (1 << 23)
@@ -322,55 +353,59 @@ def run_dist(args, world, rank, local, dist):
     barrier()
     wall, dev_ms, b = timed_rounds(eng, args.steps)
     barrier()
-    t3 = torch.tensor([wall, sum(dev_ms[1:]), float(part.e_local), float(part.n_local),
+    # the halo's device time per round (untimed): one round per call, then its halo events
+    hs = []
+    for _ in range(20):
+        eng.run(1)
+        hs.append(eng.halo_ms())
+    halo_us = 1e3 * sum(hs) / len(hs)
+    t3 = torch.tensor([wall, sum(dev_ms[1:]), halo_us, float(part.e_local), float(part.n_local),
                        float(part.n_ghost_a)], dtype=torch.float64)
     if dist is not None:
-        mx = t3[:2].clone()
+        mx = t3[:3].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = t3[2:].clone()
+        sm = t3[3:].clone()
         dist.all_reduce(sm)
-        wall, dev1 = float(mx[0]), float(mx[1])
+        wall, dev1, halo_us = (float(x) for x in mx.tolist())
         e_tot, n_tot, halo = (int(x) for x in sm.tolist())
     else:
         dev1 = sum(dev_ms[1:])
         e_tot, n_tot, halo = part.e_local, part.n_local, part.n_ghost_a
     kinfo = eng.info()
+    # rounds to 1e-9 against the per-component means (math.fsum): they need the global graph,
+    # which only the one-rank unit holds (no rank builds the global graph at N > 1)
+    conv = {"rounds_to_1e-9": None, "err_after_conv_rounds": None, "conv_rounds": None,
+            "components": None}
+    if world == 1 and not args.no_conv:
+        conv = convergence(eng, part.rowptr, part.col, v, args.conv_rounds)
+    elif world > 1:
+        conv["conv_note"] = ("per-component targets need the global graph; see the one-rank line "
+                             "of the same per-GPU unit")
     if rank == 0:
-        alg = (24 * e_tot + 28 * n_tot) // world  # per GPU, per round
-        # the same workload at one rank, measured earlier on one MI355X (committed line), so
-        # a reader can see weak-scaling efficiency against the same per-GPU graph (the
-        # driver's N = 1 line is the ER-1M headline, a different workload)
-        ref = None
-        ref_path = os.path.join(ROOT, "profiles", "r02", "bench_rggdist_1rank.json")
-        if os.path.exists(ref_path):
-            for ln in open(ref_path):
-                if ln.startswith("{"):
-                    d = json.loads(ln)
-                    ref = {"n_gpus": d["n_gpus"], "edge_updates_per_s": d["value"],
-                           "workload": d["config"]["workload"], "source": "profiles/r02/bench_rggdist_1rank.json"}
-        r1 = dev1 / max(1, args.steps - 1)
-        achieved = alg / (r1 * 1e-3) / 1e9
-        print(json.dumps({
-            "metric": METRIC, "value": e_tot * args.steps / wall, "unit": "edge-updates/s",
-            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": wall * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded RGG, U[0,100) values)",
-            "config": {"workload": f"rgg-dist:n={n_total} ({per} per GPU), deg=8, x-slabs, "
-                                   "RCCL estimates-only halo every round",
-                       "n_total": n_total, "E_directed": e_tot,
-                       "rounds_timed": f"0-{args.steps - 1} from the zero state",
-                       "kernel_selected": kinfo["kernel"], "tile_selected": kinfo["tile"],
-                       "halo_estimates_per_round": halo, "parallelism": f"graph partition x{world}"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None, "per_gpu": True,
-                         "alg_bytes_per_launch": alg, "avg_launch_us": r1 * 1e3,
-                         "launch_window": f"rounds 1-{args.steps - 1}, max over ranks (halo included)"},
-            "cpu_baseline": None, "graph_gen_s": t_gen,
-            "value_per_gpu": e_tot * args.steps / wall / world,
-            "one_rank_reference": ref}), flush=True)
+        print(json.dumps(dist_line(world=world, steps=args.steps, warmup=args.warmup, wall=wall,
+                                   dev1_ms=dev1, e_tot=e_tot, n_tot=n_tot, halo=halo,
+                                   n_total=n_total, per=per, kinfo=kinfo, halo_us=halo_us,
+                                   round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
+                                   conv=conv)), flush=True)
     eng.close()
     if dist is not None:
         dist.destroy_process_group()
+
+
+def convergence(eng, rowptr, col, v, rounds):
+    """Rounds to max |a - mean of the node's component| < 1e-9 (per-component means with
+    math.fsum; the watcher's last_avg, CA:139-142), from an untimed run of `rounds` rounds
+    from the zero state with the fused error check every round; the error reached if never."""
+    import fu
+
+    tgt, comp = fu.component_means(rowptr, col, v)
+    eng.reset()
+    eng.set_targets(tgt)
+    tr = eng.run(rounds, err_every=1)
+    below = np.nonzero(tr < 1e-9)[0]
+    return {"rounds_to_1e-9": int(below[0]) + 1 if len(below) else None,
+            "err_after_conv_rounds": float(tr[-1]), "conv_rounds": rounds,
+            "components": int(comp.max()) + 1}
 
 
 def pairwise_bytes(events, rowptr, tasks):
@@ -432,7 +467,7 @@ def run_pairwise(args):
                    "events": int(len(win)), "pairwise_updates": upd, "trace_build_s": t_build},
         "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
-                     "alg_bytes_per_launch": alg, "kernel": "k_replay_persist",
+                     "alg_bytes_per_launch": alg, "kernel": "k_replay_persist_reg",
                      "avg_launch_us": ms * 1e3, "launch_window": f"one launch, {args.steps} ticks"},
         "cpu_baseline": cpu}), flush=True)
 

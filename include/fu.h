@@ -291,6 +291,10 @@ int fu_dist_create_local(int32_t n_local, int64_t e_local, const int64_t *rowptr
                          fu_handle **out);
 int fu_dist_exchange_local(fu_handle **hs, int32_t nranks);
 int fu_dist_run_local(fu_handle **hs, int32_t nranks, int32_t rounds);
+/* Device time (ms) of the last round's halo on the rank's communication stream: from the
+ * start of the pack (boundary tiles done) to the ghost slots written. The halo overlaps the
+ * round's interior tiles. Waits for that halo. FU_ERR_STATE before the first exchange. */
+int fu_dist_halo_time(fu_handle *h, float *ms);
 
 /* Partition-aware random geometric graph: rank `part` of `nparts` generates only its slab
  * of cell columns (plus the two halo columns) of the graph fu_graph_gen_rgg(n_total, radius,

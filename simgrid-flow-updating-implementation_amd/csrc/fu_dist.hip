@@ -48,6 +48,10 @@ struct DistState {
   // ev_halo marks the ghost slots of a_r as written, and the next round waits for it.
   hipStream_t comm_stream = nullptr;
   hipEvent_t ev_bnd = nullptr, ev_halo = nullptr, ev_packed = nullptr;
+  // timing events on comm_stream: from the start of the pack (boundary tiles done) to the
+  // ghost slots written (fu_dist_halo_time)
+  hipEvent_t ev_h0 = nullptr, ev_h1 = nullptr;
+  bool timed_once = false;
   bool halo_pending = false;
   int64_t packed_round = -1;     // in-process transport: round whose packed halo awaits the exchange
   int64_t exchanged_round = -1;  // in-process transport: last round whose halo was exchanged
@@ -125,6 +129,7 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
   hipStream_t cs = d->comm_stream;
   HIPD_TRY(hipEventRecord(d->ev_bnd, s));
   HIPD_TRY(hipStreamWaitEvent(cs, d->ev_bnd, 0));
+  HIPD_TRY(hipEventRecord(d->ev_h0, cs));
   if (d->n_send_a > 0) {
     hipLaunchKernelGGL(k_pack, dim3((unsigned)((d->n_send_a + 255) / 256)), dim3(256), 0, cs,
                        (long long)d->n_send_a, d->send_a_idx, a, d->sbuf_a);
@@ -146,6 +151,8 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
   }
   NCCL_TRY(ncclGroupEnd());
   HIPD_TRY(hipEventRecord(d->ev_halo, cs));
+  HIPD_TRY(hipEventRecord(d->ev_h1, cs));
+  d->timed_once = true;
   d->halo_pending = true;
   return FU_OK;
 }
@@ -158,6 +165,8 @@ void fu__dist_free(fu_handle *h) {
   if (d->ev_bnd) hipEventDestroy(d->ev_bnd);
   if (d->ev_halo) hipEventDestroy(d->ev_halo);
   if (d->ev_packed) hipEventDestroy(d->ev_packed);
+  if (d->ev_h0) hipEventDestroy(d->ev_h0);
+  if (d->ev_h1) hipEventDestroy(d->ev_h1);
   if (d->comm_stream) hipStreamDestroy(d->comm_stream);
   void *ptrs[] = {d->send_a_idx, d->sbuf_a};
   for (void *p : ptrs)
@@ -207,7 +216,8 @@ static int dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, 
   if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&d->comm_stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&d->ev_bnd, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&d->ev_halo, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&d->ev_packed, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreate(&d->ev_h0) != hipSuccess || hipEventCreate(&d->ev_h1) != hipSuccess)
     return bail(fail(FU_ERR_HIP, "fu_dist_create: communication stream"));
   if (!unique_id) {  // fu_dist_create_local: no communicator (in-process transport). Kernel 4
     // pinned: an autotune pass would run rounds with no exchange between them
@@ -294,6 +304,8 @@ int fu_dist_exchange_local(fu_handle **hs, int32_t nranks) {
                               hipMemcpyDefault, cs));
     }
     HIPD_TRY(hipEventRecord(ds[q]->ev_halo, cs));
+    HIPD_TRY(hipEventRecord(ds[q]->ev_h1, cs));
+    ds[q]->timed_once = true;
     ds[q]->halo_pending = true;
     ds[q]->exchanged_round = r;
   }
@@ -305,6 +317,20 @@ int fu_dist_exchange_local(fu_handle **hs, int32_t nranks) {
   }
   return FU_OK;
   FU_TRY_END
+}
+
+// Device time of the last round's halo on this rank's comm stream: from the start of its pack
+// (behind the boundary tiles) to its ghost slots written (RCCL group or in-process copies).
+// It overlaps the round's interior tiles. Waits for that halo.
+int fu_dist_halo_time(fu_handle *h, float *ms) {
+  if (!h || !ms) return fail(FU_ERR_ARG, "fu_dist_halo_time: NULL argument");
+  auto *d = static_cast<DistState *>(fu__handle_dist(h));
+  if (!d) return fail(FU_ERR_ARG, "fu_dist_halo_time: not a multi-GPU handle");
+  if (!d->timed_once) return fail(FU_ERR_STATE, "fu_dist_halo_time: no halo exchanged yet");
+  HIPD_TRY(hipSetDevice(fu__handle_device(h)));
+  HIPD_TRY(hipEventSynchronize(d->ev_h1));
+  HIPD_TRY(hipEventElapsedTime(ms, d->ev_h0, d->ev_h1));
+  return FU_OK;
 }
 
 // `rounds` rounds of every rank of the in-process transport, each followed by its halo

@@ -93,6 +93,7 @@ _SIGS = {
     "fu_dist_create_local": ([i32, i64, vp, vp, vp, i32, i32, i32, vp, vp, vp, i32, P(vp)], ctypes.c_int),
     "fu_dist_exchange_local": ([vp, i32], ctypes.c_int),
     "fu_dist_run_local": ([vp, i32, i32], ctypes.c_int),
+    "fu_dist_halo_time": ([vp, P(ctypes.c_float)], ctypes.c_int),
     "fu_part_gen_rgg": ([i64, f64, u64, i32, i32, P(vp)], ctypes.c_int),
     "fu_part_info": ([vp, vp], ctypes.c_int),
     "fu_part_export": ([vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),

@@ -278,6 +278,13 @@ class DistCollectAll:
     def synchronize(self):
         L.call("fu_synchronize", self._h)
 
+    def halo_ms(self) -> float:
+        """Device time of the last round's halo on the comm stream (pack start to ghost
+        slots written; it overlaps the interior tiles). Waits for that halo."""
+        ms = L.f32()
+        L.call("fu_dist_halo_time", self._h, ctypes.byref(ms))
+        return float(ms.value)
+
     def info(self) -> dict:
         from .engine import handle_info
 

@@ -171,8 +171,15 @@ def component_means(rowptr, col, values):
     order = np.argsort(comp, kind="stable")
     bounds = np.searchsorted(comp[order], np.arange(nc + 1))
     vals = np.asarray(values, dtype=np.float64)[order]
+    size = np.diff(bounds)
     means = np.empty(nc)
-    for k in range(nc):
+    # components of one or two nodes (isolated nodes, pairs: millions on R-MAT-24) without a
+    # Python loop: fsum of one value is the value, fsum of two is their correctly rounded sum
+    one = size == 1
+    means[one] = vals[bounds[:-1][one]]
+    two = size == 2
+    means[two] = (vals[bounds[:-1][two]] + vals[bounds[:-1][two] + 1]) / 2
+    for k in np.nonzero(size > 2)[0]:
         seg = vals[bounds[k]:bounds[k + 1]]
         means[k] = math.fsum(seg.tolist()) / len(seg)
     return means[comp], comp

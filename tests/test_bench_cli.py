@@ -48,3 +48,29 @@ def test_pairwise_bytes_model():
     assert bench.pairwise_bytes(ev, None, None) == 32 + (8 * 8 + 56) + (48 * 3 + 16)
     # receive + pairwise fire at degree 8 = SURVEY §8(d)'s 136 B per exchange (+16 B of state)
     assert 32 + 8 * 8 + 56 == 152
+
+
+def test_dist_line_schema():
+    """The N > 1 (rgg-dist) line is self-contained: halo bytes inside the per-GPU roofline
+    bytes, the halo's measured share of the round, no number read from a committed file,
+    cpu_baseline left to the N = 1 line."""
+    kinfo = {"kernel": "recon", "tile": (1024, 128)}
+    line = bench.dist_line(world=4, steps=20, warmup=5, wall=0.01, dev1_ms=6.0, e_tot=4 * 67_000_000,
+                           n_tot=4 * 8_388_608, halo=4 * 40_000, n_total=4 * 8_388_608, per=8_388_608,
+                           kinfo=kinfo, halo_us=12.0, round_us=6.0e3 / 19, t_gen=1.0,
+                           conv={"rounds_to_1e-9": None, "conv_note": "x"})
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline", "cpu_baseline", "halo", "rounds_to_1e-9"):
+        assert key in line, key
+    assert line["n_gpus"] == 4 and line["scaling"] == "weak"
+    assert line["value"] == 4 * 67_000_000 * 20 / 0.01
+    roof = line["roofline"]
+    assert roof["alg_bytes_per_launch"] == (24 * 67_000_000 + 28 * 8_388_608 + 8 * 40_000)
+    assert abs(roof["frac"] - roof["achieved"] / roof["peak"]) < 1e-12
+    assert roof["avg_launch_us"] == 6.0e3 / 19
+    assert line["config"]["halo_bytes_per_round"] == 8 * 4 * 40_000
+    assert abs(line["halo"]["share_of_round"] - 12.0 / (6.0e3 / 19)) < 1e-12
+    assert line["cpu_baseline"] is None and "one_rank_reference" not in line
+    json_text = __import__("json").dumps(line)
+    assert "profiles/" not in json_text  # nothing read from committed files

@@ -41,6 +41,8 @@ for s in $STEPS; do
             step profrmat 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profrmat" -o run -- python3 "$ROOTDIR/bench.py" --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ${RMAT_ARGS:-} ;;
     ubench) step ubench 200 tools/bin/ubench_gather ;;
     rggdist) step bench_rggdist 500 python bench.py --workload rgg-dist --steps 100 --warmup 5 ;;
+    rmatline) step bench_rmatline 900 python bench.py --workload rmat --steps 20 --warmup 5 ;;
+    rgg23line) step bench_rgg23line 600 python bench.py --workload rgg --n 8388608 --steps 20 --warmup 5 ;;
     pairwise) step bench_pairwise 400 python bench.py --workload pairwise --steps 400 --warmup 50 ;;
     profpw) export TMPDIR=/tmp
             step profpw 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/profpw" -o run -- python3 "$ROOTDIR/bench.py" --workload pairwise --steps 400 --warmup 50 --cpu-seconds 0 ;;
