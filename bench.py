@@ -466,7 +466,10 @@ def run_pairwise(args):
                                f"{t0_tick}-{ticks - 1}, persistent dataflow kernel",
                    "events": int(len(win)), "pairwise_updates": upd, "trace_build_s": t_build},
         "roofline": {"bound": "hbm", "achieved": alg / (ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "unit": "GB/s", "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                     # the PMC passes of this window (tools/pmc.sh, prof_target.py --pairwise
+                     # WARMUP:STEPS), when they match it
+                     "traffic": pmc_traffic(g.n, g.E, "pairwise", args.steps) if args.warmup == 50 else None,
                      "alg_bytes_per_launch": alg, "kernel": "k_replay_persist_reg",
                      "avg_launch_us": ms * 1e3, "launch_window": f"one launch, {args.steps} ticks"},
         "cpu_baseline": cpu}), flush=True)

@@ -1342,6 +1342,135 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 }
 
 
+// ------------------------------------------------------------------------------------
+// Kernel 9's heavy rows (degree > 64 x kHeavyRL, <= mega_hub), many rows per chain wave.
+// A row's two sums are exact left-to-right chains (CA:106, CA:110), so each element costs
+// one dependent fp64 add per sum. With one row per wave (k_round_recon's heavy tiles) a
+// wave64 v_add_f64 advances two chains (even lanes S, odd lanes T), and on R-MAT-24 the
+// chains of these rows kept the SIMDs busy for ~1.2 ms per round beside their memory
+// traffic. Here a block takes kMR rows of similar length (the rows are sorted by degree),
+// its four waves stage chunks of kMCH elements of every row, (fr, er) into LDS, and ONE
+// wave runs all 2 kMR chains at once (lane 2r: S of row r, lane 2r + 1: T), with the loads
+// of the next chunk in flight meanwhile. Then a flow pass re-reads the old flows and the
+// pre-gathered estimates (CA:117-118). Same operations in the same order as every other
+// path: the results are bitwise equal.
+// ------------------------------------------------------------------------------------
+constexpr int kMR = 16;   // rows per block
+constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
+template <bool CHECK>
+__global__ __launch_bounds__(kBlock) void k_heavy_multi(
+    const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
+    double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
+    const double *__restrict__ target, unsigned long long *__restrict__ err, void *__restrict__ code_new,
+    PackCtl *__restrict__ ctl, const double *__restrict__ Gb, int fm) {
+  // sh[buf][2 r + {0: fr, 1: er}][q]; a row stride of kMCH + 1 doubles puts the 32 chain lanes'
+  // reads of one step on 32 different bank pairs
+  __shared__ double sh[2][2 * kMR][kMCH + 1];
+  __shared__ int s_b[kMR], s_d[kMR];
+  __shared__ double s_o2[kMR], s_a[kMR];
+  const PackCtl pc = ctl[2];  // packing of a_r (the table written here)
+  const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+  const int r0 = blockIdx.x * kMR;
+  if (t < kMR) {
+    const bool ok = r0 + t < nrows;
+    const int i = ok ? hrows[r0 + t] : 0;
+    const int b = ok ? rowptr[i] : 0;
+    s_b[t] = b;
+    s_d[t] = ok ? rowptr[i + 1] - b : 0;
+    s_o2[t] = ok ? a_prev2[i] : 0.0;
+  }
+  __syncthreads();
+  // wave w stages rows 4 w .. 4 w + 3; element c kMCH + lane of each
+  int rb[4], rd[4];
+  double ro2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    rb[j] = s_b[4 * w + j];
+    rd[j] = s_d[4 * w + j];
+    ro2[j] = s_o2[4 * w + j];
+  }
+  const int nch = (s_d[0] + kMCH - 1) / kMCH;  // rows sorted longest first
+  double fo[4], er[4];
+  auto load = [&](int c) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = c * kMCH + lane;
+      const bool in = k < rd[j];
+      er[j] = in ? Gb[rb[j] + k] : 0.0;
+      fo[j] = in ? ld_fo(F, rb[j] + k, fm, ro2[j]) : 0.0;
+    }
+  };
+  auto put = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int r = 4 * w + j;
+      sh[buf][2 * r][lane] = recon_fr(fo[j], er[j], ro2[j]);
+      sh[buf][2 * r + 1][lane] = er[j];
+    }
+  };
+  // chain lanes: lane 2 r + h (wave 0, lanes < 2 kMR)
+  const int cr = lane >> 1, ch = lane & 1;
+  double acc = 0.0;
+  if (nch > 0) {
+    load(0);
+    put(0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1);  // in flight during the chain
+    if (w == 0 && lane < 2 * kMR) {
+      const int len = min(kMCH, max(0, s_d[cr] - c * kMCH));
+      const double *src = sh[c & 1][lane];
+      int q = 0;
+      for (; q + 8 <= len; q += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = src[q + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + x[u];
+      }
+      for (; q < len; ++q) acc = acc + src[q];
+    }
+    __syncthreads();
+    if (c + 1 < nch) put((c + 1) & 1);
+    __syncthreads();
+  }
+  unsigned long long eb = 0;
+  if (w == 0) {
+    const double T = __shfl(acc, (lane & ~1) + 1);  // row cr's T (lane 2 cr + 1)
+    if (lane < 2 * kMR && ch == 0 && r0 + cr < nrows) {
+      const int i = hrows[r0 + cr];
+      const double a = ((v[i] - acc) + T) / (double)(s_d[cr] + 1);
+      s_a[cr] = a;
+      st_wt(a_new + i, a);
+      if (pc.width) put_code(pc, code_new, i, a);
+      if (CHECK) eb = err_bits(a, target[i]);
+    }
+  }
+  __syncthreads();
+  // flows (CA:117-118): wave w, its rows, 8 elements per lane in flight
+#pragma unroll 1
+  for (int j = 0; j < 4; ++j) {
+    const int b = rb[j], d = rd[j];
+    const double own2 = ro2[j], a = s_a[4 * w + j];
+    for (int k0 = 0; k0 < d; k0 += 8 * 64) {
+      double f8[8], e8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + lane + 64 * u;
+        e8[u] = k < d ? Gb[b + k] : 0.0;
+        f8[u] = k < d ? ld_fo(F, b + k, fm, own2) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int k = k0 + lane + 64 * u;
+        if (k < d) st_fo(F, b + k, (recon_fr(f8[u], e8[u], own2) + a) - e8[u], f8[u], fm);
+      }
+    }
+  }
+  if (CHECK) block_max_to(eb, err);
+}
+
 // Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
 // reconstruction of kernel 4), so k_round_recon's hub block only runs the chain.
 __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__restrict__ hubs,
@@ -1581,7 +1710,7 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 #ifndef FU_REPLAY_SLEEP
 #define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
 #endif
-template <int MAXD>
+template <int MAXD, bool CA>
 __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
     int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_ev,
     const int *__restrict__ node_tick, const int *__restrict__ out_uid,
@@ -1607,26 +1736,41 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   double lst = last[node];
   long long it = 0;
   bool done = false;
-  // the current event stays in registers across passes (a blocked receive re-reads only
-  // its payload); the next event's loads are issued as soon as p advances
+  // The wave advances in lock step, one event per lane per iteration, until every lane is
+  // done: a lane whose receive is not ready polls its payload again in the same iteration
+  // (checked in the next one), so a blocked lane re-polls every iteration instead of
+  // waiting for the other lanes to drain their backlogs. The head event's descriptor and
+  // payload are loaded one iteration ahead: after each event the next descriptor is
+  // requested and, if the new head is a receive, its payload.
   int tk = p < pe ? node_tick[p] : INT_MAX;
-  int4 ev = p < pe ? node_ev[p] : make_int4(0, 0, 0, 0);
-  while (!done) {
-    bool progressed = false;
-    while (p < pe) {
-      if (tk >= tick_end) break;
+  int4 ev = p < pe ? node_ev[p] : make_int4(-1, 0, 0, 0);
+  int tk1 = p + 1 < pe ? node_tick[p + 1] : INT_MAX;
+  int4 ev1 = p + 1 < pe ? node_ev[p + 1] : make_int4(-1, 0, 0, 0);
+  unsigned long long px = kMsgSentinel, py = kMsgSentinel;
+  if (ev.x == FU_EV_RECV) {
+    px = ld_tag(pay + 2 * (long long)ev.z);
+    py = ld_tag(pay + 2 * (long long)ev.z + 1);
+  }
+  for (;;) {
+    done = p == pe || tk >= tick_end;
+    if (__all(done)) break;
+    bool prog = false;
+    if (!done) {
       while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
       if (ev.x == FU_EV_RECV) {
-        const unsigned long long fx = ld_tag(pay + 2 * (long long)ev.z);
-        const unsigned long long fy = ld_tag(pay + 2 * (long long)ev.z + 1);
-        if (fx == kMsgSentinel || fy == kMsgSentinel) break;  // not sent yet: retry next pass
+        if (px != kMsgSentinel && py != kMsgSentinel) {
 #pragma unroll
-        for (int j = 0; j < MAXD; ++j)
-          if (j == ev.y) {
-            es[j] = __longlong_as_double((long long)fy);
-            fl[j] = -__longlong_as_double((long long)fx);
-          }
-      } else if (ev.x == FU_EV_FIRE_CA) {
+          for (int j = 0; j < MAXD; ++j)
+            if (j == ev.y) {
+              es[j] = __longlong_as_double((long long)py);
+              fl[j] = -__longlong_as_double((long long)px);
+            }
+          prog = true;
+        } else {  // not sent yet: poll again, checked in the next iteration
+          px = ld_tag(pay + 2 * (long long)ev.z);
+          py = ld_tag(pay + 2 * (long long)ev.z + 1);
+        }
+      } else if (CA && ev.x == FU_EV_FIRE_CA) {  // CA: the trace has collect-all fires
         const int k = ev.y;
         double S = 0.0, T = 0.0;
 #pragma unroll
@@ -1648,7 +1792,8 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
             st_tag(pay + 2 * m, nf);
             st_tag(pay + 2 * m + 1, avg);
           }
-      } else {
+        prog = true;
+      } else {  // FIRE_PW
         const int sl = ev.y, k = ev.z;
         double S = 0.0, fs = 0.0, esl = 0.0;
 #pragma unroll
@@ -1671,16 +1816,22 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
           }
         st_tag(pay + 2 * (long long)ev.w, nf);
         st_tag(pay + 2 * (long long)ev.w + 1, avg);
+        prog = true;
       }
-      ++p;
-      progressed = true;
-      if (p < pe) {
-        tk = node_tick[p];
-        ev = node_ev[p];
+      if (prog) {
+        ++p;
+        tk = tk1;
+        ev = ev1;
+        tk1 = p + 1 < pe ? node_tick[p + 1] : INT_MAX;
+        ev1 = p + 1 < pe ? node_ev[p + 1] : make_int4(-1, 0, 0, 0);
+        px = py = kMsgSentinel;
+        if (ev.x == FU_EV_RECV && tk < tick_end) {
+          px = ld_tag(pay + 2 * (long long)ev.z);
+          py = ld_tag(pay + 2 * (long long)ev.z + 1);
+        }
       }
     }
-    done = p == pe || tk >= tick_end;
-    if (!done && !progressed) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
+    if (!__any(prog)) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
       break;
@@ -1787,6 +1938,8 @@ struct fu_handle {
   int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
   int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
   int mid_geo[4][2] = {};            // heavy tiles [mid_geo[0], mid_geo[1]) lead with a row of 64 x (kHeavyRL, kMidRL] edges
+  int multi_geo[4][2] = {};          // hrows offset and count of this geometry's sorted heavy rows
+  int multi_heavy = 1;               // kernel 9: rows > 64 x kHeavyRL as k_heavy_multi blocks
   double *halo_a = nullptr;          // multi-GPU: the estimate buffer the round being launched writes
   std::vector<int32_t> h_hrows;
   int *hrows = nullptr;  // heavy rows of the wave-per-row tiles, longest first (per geometry)
@@ -1854,7 +2007,8 @@ constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 // Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
 // block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
 // {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound, int *mid) {
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound, int *mid,
+                     int *multi) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -1894,6 +2048,8 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     });
     const size_t base = h->h_hrows.size();  // each geometry appends its own list
     h->h_hrows.insert(h->h_hrows.end(), rows.begin(), rows.end());
+    multi[0] = (int)base;  // this geometry's sorted heavy rows (k_heavy_multi takes a prefix)
+    multi[1] = (int)rows.size();
     // tiles whose longest (first) row fits kMidRL registers per lane but not kHeavyRL
     auto deg = [&](int32_t x) { return h->h_rowptr[x + 1] - h->h_rowptr[x]; };
     mid[0] = mid[1] = (int)all.size();
@@ -1905,6 +2061,7 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     }
   } else {
     mid[0] = mid[1] = (int)hubs.size();
+    multi[0] = multi[1] = 0;
     all.insert(all.end(), heavy.begin(), heavy.end());
   }
   *nheavy = (int)all.size();
@@ -1974,7 +2131,7 @@ int build_tiles(fu_handle *h) {
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
     if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g],
-                                  &h->nbound_geo[g], h->mid_geo[g]))
+                                  &h->nbound_geo[g], h->mid_geo[g], h->multi_geo[g]))
       return rc;
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
@@ -2407,9 +2564,20 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                          c.fm);
   };
+  // the rows of the heavy tiles [nmega, m1) (4 rows each, longest first: every row of more
+  // than 64 x kHeavyRL edges, and the few shorter ones sharing the last tile) as
+  // k_heavy_multi blocks, many rows per chain wave
+  const int n_multi = std::min(h->multi_geo[1][1], 4 * (m1 - nmega));
+  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && D == 0 && n_multi > 0;
   auto tiles = [&](auto C) {
-    heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
-    heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
+    if (multi) {
+      hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value>), dim3((n_multi + kMR - 1) / kMR), dim3(kBlock), 0,
+                         h->stream, h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F, c.ap2, c.an,
+                         h->target, c.err, h->code[r1], h->pctl, Gb, c.fm);
+    } else {
+      heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
+      heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
+    }
     heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
     if (nl)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
@@ -2853,6 +3021,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->tr_bpx = (int)value;
     return FU_OK;
   }
+  if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
+    h->multi_heavy = value != 0;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "mid_heavy")) {  // kernel 9: register-resident launch for rows of 257-1024 edges
     h->mid_heavy = value != 0;
     return FU_OK;
@@ -3278,8 +3450,21 @@ struct fu_replay {
   int64_t max_deg = 0;
   int pers_reg = 1;       // option "persistent_reg": one node per thread, state in registers
   bool reg_ok = false;    // degree <= kReplayRegDeg and every node's thread resident at once
+  bool has_ca = false;    // the trace holds collect-all fires
 };
 constexpr int kReplayRegDeg = 16;
+
+// The register variant for the trace: row registers for degree <= 8 or <= 16, the collect-all
+// fire path only when the trace has one (both cost registers, and the variant must keep
+// every node's thread resident).
+using ReplayRegKernel = void (*)(int, int, const long long *, const int4 *, const int *, const int *,
+                                 const long long *, const double *, double *, double *, double *,
+                                 unsigned long long *, long long *, int *, int, const int *, double *, int *,
+                                 long long);
+static ReplayRegKernel replay_reg_kernel(const fu_replay *r) {
+  if (r->max_deg <= 8) return r->has_ca ? k_replay_persist_reg<8, true> : k_replay_persist_reg<8, false>;
+  return r->has_ca ? k_replay_persist_reg<16, true> : k_replay_persist_reg<16, false>;
+}
 
 static int replay_build_persistent(fu_replay *r) {
   if (r->pers_ready) return FU_OK;
@@ -3300,6 +3485,7 @@ static int replay_build_persistent(fu_replay *r) {
       for (int32_t p = r->h_tasks[3 * q + 1]; p < r->h_tasks[3 * q + 2]; ++p) {
         const int32_t *e = &r->h_events[4 * (int64_t)p];
         int4 o = make_int4(e[0], e[1], e[2], e[3]);
+        r->has_ca |= e[0] == FU_EV_FIRE_CA;
         if (e[0] == FU_EV_RECV) {
           const int64_t u = slot_uid[e[2]];
           if (u < 0) return fail(FU_ERR_ARG, "replay: RECV of a message slot never written");
@@ -3350,7 +3536,7 @@ static int replay_build_persistent(fu_replay *r) {
   // the register variant needs one resident thread per node (a node's blocked receive is
   // retried by its own thread only)
   int per_cu_reg = 0;
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, k_replay_persist_reg<kReplayRegDeg>, kBlock, 0));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, replay_reg_kernel(r), kBlock, 0));
   const long long cap_reg = (long long)std::max(0, per_cu_reg - 1) * ncu;
   r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg;
   r->pers_ready = true;
@@ -3455,7 +3641,7 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
     HIP_TRY(hipMemsetAsync(r->scur, 0, sizeof(int) * r->n, r->stream));
     HIP_TRY(hipMemsetAsync(r->status, 0, sizeof(int), r->stream));
     if (r->reg_ok && r->pers_reg)
-      hipLaunchKernelGGL(k_replay_persist_reg<kReplayRegDeg>, dim3(grid_for(r->n)), dim3(kBlock), 0, r->stream,
+      hipLaunchKernelGGL(replay_reg_kernel(r), dim3(grid_for(r->n)), dim3(kBlock), 0, r->stream,
                          r->n, tick_end, r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v,
                          r->flow, r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
                          (long long)1 << 22);

@@ -21,7 +21,20 @@ ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1
 ap.add_argument("--diag", type=int, default=0)
 ap.add_argument("--layout", default="given")
 ap.add_argument("--opt", action="append", default=[], help="extra engine option key=value (repeatable)")
+ap.add_argument("--pairwise", default="", help="WARMUP:STEPS: bench.py's pairwise window instead (RR-64K "
+                "tick replay: ticks 0..51+WARMUP in one launch, then the STEPS timed ticks in a second)")
 a = ap.parse_args()
+if a.pairwise:
+    warm, steps = (int(x) for x in a.pairwise.split(":"))
+    g = fu.Graph.random_regular(65536, 8, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    t0 = 51 + warm
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", t0 + steps, "rand:3")
+    rep = fu.Replay(tr, v, persistent=True)
+    rep.run(t0)
+    rep.run(t0 + steps)
+    print("pairwise", g.n, g.E, "ticks", t0, t0 + steps)
+    sys.exit(0)
 g = fu.Graph.from_spec(a.spec, seed=1)
 v = fu.uniform_values(g.n, seed=0)
 eng = fu.CollectAll(g, v, kernel=a.kernel, layout=a.layout)
