@@ -1390,37 +1390,34 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     ro2[j] = s_o2[4 * w + j];
   }
   const int nch = (s_d[0] + kMCH - 1) / kMCH;  // rows sorted longest first
-  double fo[4], er[4];
-  auto load = [&](int c) {
+  // two register sets, each one chunk of the wave's 4 rows: the loads run two chunks ahead of
+  // the chain. Loads are unconditional from clamped indices (the compiler then waits for a
+  // set by count, vmcnt(N), not for everything)
+  double fo0[4], er0[4], fo1[4], er1[4];
+  auto load = [&](double (&fo)[4], double (&er)[4], int c) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const int k = c * kMCH + lane;
-      const bool in = k < rd[j];
-      er[j] = in ? Gb[rb[j] + k] : 0.0;
-      fo[j] = in ? ld_fo(F, rb[j] + k, fm, ro2[j]) : 0.0;
+      const int k = min(c * kMCH + lane, max(rd[j] - 1, 0));
+      er[j] = Gb[rb[j] + k];
+      fo[j] = ld_fo(F, rb[j] + k, fm, ro2[j]);
     }
   };
-  auto put = [&](int buf) {
+  auto put = [&](const double (&fo)[4], const double (&er)[4], int c, int buf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = 4 * w + j;
-      sh[buf][2 * r][lane] = recon_fr(fo[j], er[j], ro2[j]);
-      sh[buf][2 * r + 1][lane] = er[j];
+      const bool in = c * kMCH + lane < rd[j];
+      sh[buf][2 * r][lane] = in ? recon_fr(fo[j], er[j], ro2[j]) : 0.0;
+      sh[buf][2 * r + 1][lane] = in ? er[j] : 0.0;
     }
   };
   // chain lanes: lane 2 r + h (wave 0, lanes < 2 kMR)
   const int cr = lane >> 1, ch = lane & 1;
   double acc = 0.0;
-  if (nch > 0) {
-    load(0);
-    put(0);
-  }
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    if (c + 1 < nch) load(c + 1);  // in flight during the chain
+  auto chain = [&](int c, int buf) {
     if (w == 0 && lane < 2 * kMR) {
       const int len = min(kMCH, max(0, s_d[cr] - c * kMCH));
-      const double *src = sh[c & 1][lane];
+      const double *src = sh[buf][lane];
       int q = 0;
       for (; q + 8 <= len; q += 8) {
         double x[8];
@@ -1431,8 +1428,27 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       }
       for (; q < len; ++q) acc = acc + src[q];
     }
+  };
+  if (nch > 0) {
+    load(fo0, er0, 0);
+    load(fo1, er1, 1);
+    put(fo0, er0, 0, 0);
+  }
+  __syncthreads();
+  for (int c = 0; c < nch; c += 2) {
+    // chunk c in buffer 0, chunk c + 1 in flight in set 1
+    if (c + 2 < nch) load(fo0, er0, c + 2);
+    chain(c, 0);
     __syncthreads();
-    if (c + 1 < nch) put((c + 1) & 1);
+    if (c + 1 >= nch) break;
+    put(fo1, er1, c + 1, 1);
+    __syncthreads();
+    // chunk c + 1 in buffer 1, chunk c + 2 in flight in set 0
+    if (c + 3 < nch) load(fo1, er1, c + 3);
+    chain(c + 1, 1);
+    __syncthreads();
+    if (c + 2 >= nch) break;
+    put(fo0, er0, c + 2, 0);
     __syncthreads();
   }
   unsigned long long eb = 0;
