@@ -1062,7 +1062,10 @@ constexpr int kTrThreads = 1024;
 // bucket's run starts (offT) are loaded while this bucket's G_A loads are in flight, and its
 // G_B stores drain while the next bucket is scanned (with one block per bucket, each block
 // paid the offT round trip first and held its slot until its stores were done).
-__global__ __launch_bounds__(kTrThreads) void k_transpose(int b0, int nbk, int P, long long E,
+#ifndef FU_TR_WAVES
+#define FU_TR_WAVES 1
+#endif
+__global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
@@ -1719,24 +1722,44 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 
 // k_replay_persist with one node per thread and the node's state (its row of flows and
 // estimate caches, cursor, snapshot cursor, last average) kept in registers for the whole
-// run (degree <= MAXD): an event costs its own loads (event, tick, and for a receive the
-// payload) instead of also re-reading the node's state from memory on every pass. Same
-// event semantics and order as k_replay_persist; a blocked receive leaves the event loop
-// and is retried on the next pass (no lane spins on another lane of its wave).
+// run (degree <= MAXD): an event costs its own loads instead of also re-reading the node's
+// state from memory on every pass. Same event semantics and order as k_replay_persist.
+//
+// The replay is bound by the time one lock-step iteration of a wave takes, not by the
+// trace's dependence depth (RR-64K pairwise: ~6 message hops per 100 ticks; a node runs
+// {receive, fire} every other tick), and an iteration ends waiting for its vector-memory
+// operations, which retire in issue order: loads, and the write-through message stores.
+// So an iteration issues as few of them as it can, in a fixed order:
+//   * the lane's next events sit in an 8-entry LDS ring, refilled 4 packed descriptors
+//     (64 contiguous bytes: {type, slot | k << 8, msg, tick}) at a time; they land during
+//     one iteration and are written to the ring at the head of the next;
+//   * the pairwise path (CA = false) ends every iteration with exactly ONE 16-byte sc1 poll
+//     (the head receive's payload, both tagged halves) and then exactly ONE 16-byte sc1
+//     store (the iteration's message {flow, avg}), each aimed at the node's scratch slot
+//     when there is none: the next iteration waits for the poll and leaves the youngest
+//     store in flight (vmcnt(1)), instead of waiting for every store's write-through;
+//   * an iteration runs up to kRW events in program order: a receive only as its first
+//     event (the poll issued for it), at most one pairwise fire.
+// The collect-all path (k messages per fire) stores its messages as it goes.
 #ifndef FU_REPLAY_SLEEP
 #define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
 #endif
+constexpr int kRW = 3;       // events per iteration at most
+constexpr int kRing = 8;     // LDS ring entries per lane
+constexpr int kRefill = 4;   // events per refill
 template <int MAXD, bool CA>
 __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
-    int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_ev,
-    const int *__restrict__ node_tick, const int *__restrict__ out_uid,
+    int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_evt,
+    const int *__restrict__ out_uid, int n_uid,
     const long long *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ flow,
     double *__restrict__ est, double *__restrict__ last, unsigned long long *__restrict__ pay,
     long long *__restrict__ cursor, int *__restrict__ scur, int n_snap,
     const int *__restrict__ snap_ticks, double *__restrict__ snaps, int *__restrict__ status,
     long long max_iters) {
+  __shared__ int4 s_ring[kRing * kBlock];  // entry k of lane t at k * kBlock + t
   const int node = blockIdx.x * kBlock + threadIdx.x;
-  if (node >= n) return;
+  if (node >= n) return;  // (no block barrier below)
+  int4 *ring = s_ring + threadIdx.x;
   long long p = cursor[node];
   const long long pe = node_off[node + 1];
   int sc = scur[node];
@@ -1750,103 +1773,157 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   }
   const double val = v[node];
   double lst = last[node];
+  // ring: events p .. p + rv - 1 at entries rh, rh + 1, ... (mod kRing); fill = next event to load
+  int rh = 0, rv = 0;
+  long long fill = p;
+  int4 r0, r1, r2, r3;  // the refill in flight (kRefill = 4 named registers: no private array)
+  bool pend = false;
+  int pcnt = 0;
+#define FU_RING_REFILL()                                                    \
+  do {                                                                      \
+    const long long lo = max(0ll, pe - 1);                                  \
+    r0 = node_evt[max(0ll, min(fill, lo))];                                 \
+    r1 = node_evt[max(0ll, min(fill + 1, lo))];                             \
+    r2 = node_evt[max(0ll, min(fill + 2, lo))];                             \
+    r3 = node_evt[max(0ll, min(fill + 3, lo))];                             \
+    pcnt = (int)max(0ll, min((long long)kRefill, pe - fill));               \
+    fill += kRefill;                                                        \
+    pend = true;                                                            \
+  } while (0)
+#define FU_RING_COMMIT()                                                    \
+  do {                                                                      \
+    ring[((rh + rv) & (kRing - 1)) * kBlock] = r0;                          \
+    ring[((rh + rv + 1) & (kRing - 1)) * kBlock] = r1;                      \
+    ring[((rh + rv + 2) & (kRing - 1)) * kBlock] = r2;                      \
+    ring[((rh + rv + 3) & (kRing - 1)) * kBlock] = r3;                      \
+    rv += pcnt;                                                             \
+    pend = false;                                                           \
+  } while (0)
+  static_assert(kRefill == 4, "four refill registers");
+  FU_RING_REFILL();
+  FU_RING_COMMIT();
+  FU_RING_REFILL();
+  FU_RING_COMMIT();
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pay, 0, 0x7FFFFFF0, 0x00020000);
+  const int scratch = n_uid + node;  // this node's scratch slot (idle polls and stores)
+  unsigned long long px = kMsgSentinel, py = kMsgSentinel;
+  int polled = -1;  // the slot px, py were loaded from
+  auto poll = [&](int msg) {  // one 16-byte sc1 load (aux 16): both tagged halves of the slot
+    polled = msg;
+    const u4 w = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(prs, msg * 16, 0, 16));
+    px = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
+    py = (unsigned long long)w.z | ((unsigned long long)w.w << 32);
+  };
+  // a message = one 16-byte sc1 store (write-through, aux 16) of {flow, avg}: one fabric write
+  // instead of two 8-byte ones (narrow sc1 stores cost 2.7x per byte, MI355X_MICROARCH.md)
+  auto send = [&](int msg, double f, double a) {
+    const unsigned long long fb = (unsigned long long)__double_as_longlong(f);
+    const unsigned long long ab = (unsigned long long)__double_as_longlong(a);
+    const u4 w = {(unsigned)fb, (unsigned)(fb >> 32), (unsigned)ab, (unsigned)(ab >> 32)};
+    __builtin_amdgcn_raw_buffer_store_b128(w, prs, msg * 16, 0, 16);
+  };
+  {
+    const int4 h = ring[rh * kBlock];
+    poll(rv > 0 && h.w < tick_end && h.x == FU_EV_RECV ? h.z : scratch);
+    if (!CA) send(scratch, 0.0, 0.0);
+  }
   long long it = 0;
   bool done = false;
-  // The wave advances in lock step, one event per lane per iteration, until every lane is
-  // done: a lane whose receive is not ready polls its payload again in the same iteration
-  // (checked in the next one), so a blocked lane re-polls every iteration instead of
-  // waiting for the other lanes to drain their backlogs. The head event's descriptor and
-  // payload are loaded one iteration ahead: after each event the next descriptor is
-  // requested and, if the new head is a receive, its payload.
-  int tk = p < pe ? node_tick[p] : INT_MAX;
-  int4 ev = p < pe ? node_ev[p] : make_int4(-1, 0, 0, 0);
-  int tk1 = p + 1 < pe ? node_tick[p + 1] : INT_MAX;
-  int4 ev1 = p + 1 < pe ? node_ev[p + 1] : make_int4(-1, 0, 0, 0);
-  unsigned long long px = kMsgSentinel, py = kMsgSentinel;
-  if (ev.x == FU_EV_RECV) {
-    px = ld_tag(pay + 2 * (long long)ev.z);
-    py = ld_tag(pay + 2 * (long long)ev.z + 1);
-  }
   for (;;) {
-    done = p == pe || tk >= tick_end;
+    if (pend) FU_RING_COMMIT();
+    const int4 h0 = ring[rh * kBlock];
+    done = rv > 0 ? h0.w >= tick_end : !pend && fill >= pe;
     if (__all(done)) break;
     bool prog = false;
-    if (!done) {
-      while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
-      if (ev.x == FU_EV_RECV) {
-        if (px != kMsgSentinel && py != kMsgSentinel) {
+    int poll_id = scratch;  // the iteration's poll and store targets
+    int out_id = scratch;
+    double out_f = 0.0, out_a = 0.0;
+    if (!done && rv > 0) {
+      int m = 0;  // events run this iteration
+#pragma unroll
+      for (int k = 0; k < kRW; ++k) {
+        if (k >= rv) break;
+        const int4 ev = k == 0 ? h0 : ring[((rh + k) & (kRing - 1)) * kBlock];
+        const int tk = ev.w;
+        if (tk >= tick_end) break;
+        if (ev.x == FU_EV_RECV) {
+          // a receive that became the head this iteration, or whose message has not arrived:
+          // poll it at the end of the iteration, check it in the next
+          if (k > 0 || polled != ev.z || px == kMsgSentinel || py == kMsgSentinel) {
+            poll_id = ev.z;
+            break;
+          }
+        } else if (!CA && out_id != scratch) {
+          break;  // one pairwise message per iteration
+        }
+        while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
+        if (ev.x == FU_EV_RECV) {  // CA:98-99 / PW:98-99
 #pragma unroll
           for (int j = 0; j < MAXD; ++j)
             if (j == ev.y) {
               es[j] = __longlong_as_double((long long)py);
               fl[j] = -__longlong_as_double((long long)px);
             }
-          prog = true;
-        } else {  // not sent yet: poll again, checked in the next iteration
-          px = ld_tag(pay + 2 * (long long)ev.z);
-          py = ld_tag(pay + 2 * (long long)ev.z + 1);
+          px = py = kMsgSentinel;
+        } else if (CA && ev.x == FU_EV_FIRE_CA) {  // CA:105-125
+          const int kk = ev.y;
+          double S = 0.0, T = 0.0;
+#pragma unroll
+          for (int j = 0; j < MAXD; ++j)
+            if (j < kk) S = S + fl[j];
+          const double estimate = val - S;
+#pragma unroll
+          for (int j = 0; j < MAXD; ++j)
+            if (j < kk) T = T + es[j];
+          const double avg = (estimate + T) / (double)(kk + 1);
+          lst = avg;
+#pragma unroll
+          for (int j = 0; j < MAXD; ++j)
+            if (j < kk) {
+              const double nf = (fl[j] + avg) - es[j];
+              fl[j] = nf;
+              es[j] = avg;
+              send(out_uid[ev.z + j], nf, avg);
+            }
+        } else {  // FIRE_PW, PW:102-117: y = slot | k << 8
+          const int sl = ev.y & 0xFF, kk = ev.y >> 8;
+          double S = 0.0, fs = 0.0, esl = 0.0;
+#pragma unroll
+          for (int j = 0; j < MAXD; ++j) {
+            if (j < kk) S = S + fl[j];
+            if (j == sl) {
+              fs = fl[j];
+              esl = es[j];
+            }
+          }
+          const double estimate = val - S;
+          const double avg = (esl + estimate) / 2.0;
+          lst = avg;
+          const double nf = (fs + avg) - esl;
+#pragma unroll
+          for (int j = 0; j < MAXD; ++j)
+            if (j == sl) {
+              fl[j] = nf;
+              es[j] = avg;
+            }
+          if (CA) send(ev.z, nf, avg);
+          out_id = ev.z;
+          out_f = nf;
+          out_a = avg;
         }
-      } else if (CA && ev.x == FU_EV_FIRE_CA) {  // CA: the trace has collect-all fires
-        const int k = ev.y;
-        double S = 0.0, T = 0.0;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j)
-          if (j < k) S = S + fl[j];
-        const double estimate = val - S;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j)
-          if (j < k) T = T + es[j];
-        const double avg = (estimate + T) / (double)(k + 1);
-        lst = avg;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j)
-          if (j < k) {
-            const double nf = (fl[j] + avg) - es[j];
-            fl[j] = nf;
-            es[j] = avg;
-            const long long m = out_uid[ev.z + j];
-            st_tag(pay + 2 * m, nf);
-            st_tag(pay + 2 * m + 1, avg);
-          }
-        prog = true;
-      } else {  // FIRE_PW
-        const int sl = ev.y, k = ev.z;
-        double S = 0.0, fs = 0.0, esl = 0.0;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j) {
-          if (j < k) S = S + fl[j];
-          if (j == sl) {
-            fs = fl[j];
-            esl = es[j];
-          }
-        }
-        const double estimate = val - S;
-        const double avg = (esl + estimate) / 2.0;
-        lst = avg;
-        const double nf = (fs + avg) - esl;
-#pragma unroll
-        for (int j = 0; j < MAXD; ++j)
-          if (j == sl) {
-            fl[j] = nf;
-            es[j] = avg;
-          }
-        st_tag(pay + 2 * (long long)ev.w, nf);
-        st_tag(pay + 2 * (long long)ev.w + 1, avg);
-        prog = true;
+        ++m;
       }
-      if (prog) {
-        ++p;
-        tk = tk1;
-        ev = ev1;
-        tk1 = p + 1 < pe ? node_tick[p + 1] : INT_MAX;
-        ev1 = p + 1 < pe ? node_ev[p + 1] : make_int4(-1, 0, 0, 0);
-        px = py = kMsgSentinel;
-        if (ev.x == FU_EV_RECV && tk < tick_end) {
-          px = ld_tag(pay + 2 * (long long)ev.z);
-          py = ld_tag(pay + 2 * (long long)ev.z + 1);
-        }
+      if (m) {
+        p += m;
+        rh = (rh + m) & (kRing - 1);
+        rv -= m;
+        prog = true;
       }
     }
+    if (!pend && rv <= kRing - kRefill && fill < pe) FU_RING_REFILL();  // lands during the next pass
+    poll(poll_id);                          // the youngest load ...
+    if (!CA) send(out_id, out_f, out_a);    // ... and the one store after it
     if (!__any(prog)) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
@@ -1865,6 +1942,8 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   scur[node] = sc;
   last[node] = lst;
 }
+#undef FU_RING_REFILL
+#undef FU_RING_COMMIT
 
 
 template <typename T>
@@ -3459,6 +3538,7 @@ struct fu_replay {
   std::vector<int32_t> h_tasks, h_events, h_out_ids;
   long long *node_off = nullptr, *cursor = nullptr;
   int4 *node_ev = nullptr;
+  int4 *node_evt = nullptr;  // register kernel: packed {type, slot | k << 8, msg, tick}
   int *node_tick = nullptr, *out_uid = nullptr, *scur = nullptr, *status = nullptr;
   unsigned long long *pay = nullptr;
   int64_t n_uid = 0;
@@ -3473,7 +3553,7 @@ constexpr int kReplayRegDeg = 16;
 // The register variant for the trace: row registers for degree <= 8 or <= 16, the collect-all
 // fire path only when the trace has one (both cost registers, and the variant must keep
 // every node's thread resident).
-using ReplayRegKernel = void (*)(int, int, const long long *, const int4 *, const int *, const int *,
+using ReplayRegKernel = void (*)(int, int, const long long *, const int4 *, const int *, int,
                                  const long long *, const double *, double *, double *, double *,
                                  unsigned long long *, long long *, int *, int, const int *, double *, int *,
                                  long long);
@@ -3492,6 +3572,7 @@ static int replay_build_persistent(fu_replay *r) {
   std::vector<int64_t> pos(off.begin(), off.end() - 1);
   std::vector<int4> nev(ne > 0 ? ne : 1);
   std::vector<int32_t> ntick(ne > 0 ? ne : 1);
+  std::vector<int4> nevt(ne > 0 ? ne : 1);
   std::vector<int32_t> ouid(r->h_out_ids.size() > 0 ? r->h_out_ids.size() : 1);
   std::vector<int64_t> slot_uid(r->n_msgs > 0 ? r->n_msgs : 1, -1);
   int64_t U = 0;
@@ -3517,6 +3598,9 @@ static int replay_build_persistent(fu_replay *r) {
         }
         if (U >= (int64_t)INT32_MAX) return fail(FU_ERR_ALLOC, "replay: more than 2^31 messages");
         nev[pos[node]] = o;
+        nevt[pos[node]] = o.x == FU_EV_RECV      ? make_int4(o.x, o.y, o.z, t)
+                          : o.x == FU_EV_FIRE_CA ? make_int4(o.x, o.y, o.z, t)
+                                                 : make_int4(o.x, o.y | (o.z << 8), o.w, t);
         ntick[pos[node]++] = t;
       }
     }
@@ -3525,22 +3609,25 @@ static int replay_build_persistent(fu_replay *r) {
   if (int rc = dmalloc(&r->node_off, n + 1)) return rc;
   if (int rc = dmalloc(&r->node_ev, nev.size())) return rc;
   if (int rc = dmalloc(&r->node_tick, ntick.size())) return rc;
+  if (int rc = dmalloc(&r->node_evt, nevt.size())) return rc;
   if (int rc = dmalloc(&r->out_uid, ouid.size())) return rc;
-  if (int rc = dmalloc(&r->pay, 2 * (size_t)std::max<int64_t>(U, 1))) return rc;
+  // slots [U, U + n): per-node scratch slots of the register kernel's idle polls and stores
+  if (int rc = dmalloc(&r->pay, 2 * (size_t)(U + n))) return rc;
   if (int rc = dmalloc(&r->cursor, n)) return rc;
   if (int rc = dmalloc(&r->scur, n)) return rc;
   if (int rc = dmalloc(&r->status, 1)) return rc;
   HIP_TRY(hipMemcpy(r->node_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->node_ev, nev.data(), sizeof(int4) * nev.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->node_tick, ntick.data(), sizeof(int32_t) * ntick.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->node_evt, nevt.data(), sizeof(int4) * nevt.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->out_uid, ouid.data(), sizeof(int32_t) * ouid.size(), hipMemcpyHostToDevice));
   std::vector<long long> cur(off.begin(), off.end() - 1);
   HIP_TRY(hipMemcpy(r->cursor, cur.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
   HIP_TRY(hipMemset(r->scur, 0, sizeof(int) * n));
   double sentinel;
   std::memcpy(&sentinel, &kMsgSentinel, sizeof(double));
-  hipLaunchKernelGGL(k_fill, dim3(grid_for(2 * std::max<int64_t>(U, 1))), dim3(kBlock), 0, r->stream,
-                     (long long)(2 * std::max<int64_t>(U, 1)), sentinel, reinterpret_cast<double *>(r->pay));
+  hipLaunchKernelGGL(k_fill, dim3(grid_for(2 * (U + n))), dim3(kBlock), 0, r->stream,
+                     (long long)(2 * (U + n)), sentinel, reinterpret_cast<double *>(r->pay));
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipStreamSynchronize(r->stream));
   int per_cu = 0, ncu = 0;
@@ -3554,7 +3641,8 @@ static int replay_build_persistent(fu_replay *r) {
   int per_cu_reg = 0;
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, replay_reg_kernel(r), kBlock, 0));
   const long long cap_reg = (long long)std::max(0, per_cu_reg - 1) * ncu;
-  r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg;
+  // (and 16-byte payload polls at 32-bit byte offsets: below 2^27 messages)
+  r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg && U + n < (1LL << 27);
   r->pers_ready = true;
   return FU_OK;
 }
@@ -3658,7 +3746,7 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
     HIP_TRY(hipMemsetAsync(r->status, 0, sizeof(int), r->stream));
     if (r->reg_ok && r->pers_reg)
       hipLaunchKernelGGL(replay_reg_kernel(r), dim3(grid_for(r->n)), dim3(kBlock), 0, r->stream,
-                         r->n, tick_end, r->node_off, r->node_ev, r->node_tick, r->out_uid, r->rowptr, r->v,
+                         r->n, tick_end, r->node_off, r->node_evt, r->out_uid, (int)r->n_uid, r->rowptr, r->v,
                          r->flow, r->est, r->last, r->pay, r->cursor, r->scur, n_snap, d_st, snaps_dev, r->status,
                          (long long)1 << 22);
     else
@@ -3761,7 +3849,7 @@ int fu_replay_destroy(fu_replay *r) {
   hipSetDevice(r->device);
   if (r->stream) hipStreamSynchronize(r->stream);
   void *ptrs[] = {r->rowptr, r->tasks, r->events, r->out_ids, r->v, r->flow, r->est, r->last, r->msg,
-                  r->node_off, r->cursor, r->node_ev, r->node_tick, r->out_uid, r->scur, r->status, r->pay};
+                  r->node_off, r->cursor, r->node_ev, r->node_evt, r->node_tick, r->out_uid, r->scur, r->status, r->pay};
   for (void *p : ptrs)
     if (p) hipFree(p);
   if (r->ev0) hipEventDestroy(r->ev0);
