@@ -1744,22 +1744,30 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 #ifndef FU_REPLAY_SLEEP
 #define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
 #endif
-constexpr int kRW = 3;       // events per iteration at most
-constexpr int kRing = 8;     // LDS ring entries per lane
-constexpr int kRefill = 4;   // events per refill
+constexpr int kRW = 4;       // events per iteration at most
+constexpr int kScan = 4;     // ring entries searched for the next two receives
+constexpr int kRing = 16;    // LDS ring entries per lane
+constexpr int kRefill = 8;   // events per refill (64 contiguous bytes)
+// packed 8-byte event: x = type | slot << 2 | k << 7 | tick << 12 (deg <= 16, tick < 2^20),
+// y = message slot (receive, pairwise fire) or out_ids offset (collect-all fire); decoded to
+// the int4 {type, slot | k << 8 (pairwise) / slot (receive) / k (collect-all), y, tick}
+__device__ __forceinline__ int4 ev_dec(int2 e) {
+  const int ty = e.x & 3, sl = (e.x >> 2) & 31, k = (e.x >> 7) & 31, tk = (int)((unsigned)e.x >> 12);
+  return make_int4(ty, ty == FU_EV_FIRE_PW ? (sl | k << 8) : ty == FU_EV_RECV ? sl : k, e.y, tk);
+}
 template <int MAXD, bool CA>
 __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
-    int n, int tick_end, const long long *__restrict__ node_off, const int4 *__restrict__ node_evt,
+    int n, int tick_end, const long long *__restrict__ node_off, const int2 *__restrict__ node_evt,
     const int *__restrict__ out_uid, int n_uid,
     const long long *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ flow,
     double *__restrict__ est, double *__restrict__ last, unsigned long long *__restrict__ pay,
     long long *__restrict__ cursor, int *__restrict__ scur, int n_snap,
     const int *__restrict__ snap_ticks, double *__restrict__ snaps, int *__restrict__ status,
     long long max_iters) {
-  __shared__ int4 s_ring[kRing * kBlock];  // entry k of lane t at k * kBlock + t
+  __shared__ int2 s_ring[kRing * kBlock];  // entry k of lane t at k * kBlock + t
   const int node = blockIdx.x * kBlock + threadIdx.x;
   if (node >= n) return;  // (no block barrier below)
-  int4 *ring = s_ring + threadIdx.x;
+  int2 *ring = s_ring + threadIdx.x;
   long long p = cursor[node];
   const long long pe = node_off[node + 1];
   int sc = scur[node];
@@ -1776,7 +1784,7 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   // ring: events p .. p + rv - 1 at entries rh, rh + 1, ... (mod kRing); fill = next event to load
   int rh = 0, rv = 0;
   long long fill = p;
-  int4 r0, r1, r2, r3;  // the refill in flight (kRefill = 4 named registers: no private array)
+  int2 r0, r1, r2, r3, r4, r5, r6, r7;  // the refill in flight (named registers: no private array)
   bool pend = false;
   int pcnt = 0;
 #define FU_RING_REFILL()                                                    \
@@ -1786,6 +1794,10 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
     r1 = node_evt[max(0ll, min(fill + 1, lo))];                             \
     r2 = node_evt[max(0ll, min(fill + 2, lo))];                             \
     r3 = node_evt[max(0ll, min(fill + 3, lo))];                             \
+    r4 = node_evt[max(0ll, min(fill + 4, lo))];                             \
+    r5 = node_evt[max(0ll, min(fill + 5, lo))];                             \
+    r6 = node_evt[max(0ll, min(fill + 6, lo))];                             \
+    r7 = node_evt[max(0ll, min(fill + 7, lo))];                             \
     pcnt = (int)max(0ll, min((long long)kRefill, pe - fill));               \
     fill += kRefill;                                                        \
     pend = true;                                                            \
@@ -1796,10 +1808,14 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
     ring[((rh + rv + 1) & (kRing - 1)) * kBlock] = r1;                      \
     ring[((rh + rv + 2) & (kRing - 1)) * kBlock] = r2;                      \
     ring[((rh + rv + 3) & (kRing - 1)) * kBlock] = r3;                      \
+    ring[((rh + rv + 4) & (kRing - 1)) * kBlock] = r4;                      \
+    ring[((rh + rv + 5) & (kRing - 1)) * kBlock] = r5;                      \
+    ring[((rh + rv + 6) & (kRing - 1)) * kBlock] = r6;                      \
+    ring[((rh + rv + 7) & (kRing - 1)) * kBlock] = r7;                      \
     rv += pcnt;                                                             \
     pend = false;                                                           \
   } while (0)
-  static_assert(kRefill == 4, "four refill registers");
+  static_assert(kRefill == 8, "eight refill registers");
   FU_RING_REFILL();
   FU_RING_COMMIT();
   FU_RING_REFILL();
@@ -1807,13 +1823,13 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
   typedef unsigned u4 __attribute__((ext_vector_type(4)));
   const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(pay, 0, 0x7FFFFFF0, 0x00020000);
   const int scratch = n_uid + node;  // this node's scratch slot (idle polls and stores)
-  unsigned long long px = kMsgSentinel, py = kMsgSentinel;
-  int polled = -1;  // the slot px, py were loaded from
-  auto poll = [&](int msg) {  // one 16-byte sc1 load (aux 16): both tagged halves of the slot
-    polled = msg;
+  // two polls in flight: the payloads of the lane's next two receives (slots pa, pb)
+  unsigned long long ax = kMsgSentinel, ay = kMsgSentinel, bx = kMsgSentinel, by = kMsgSentinel;
+  int pa = -1, pb = -1;
+  auto ld16 = [&](int msg, unsigned long long &x, unsigned long long &y) {  // 16-byte sc1 load
     const u4 w = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(prs, msg * 16, 0, 16));
-    px = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
-    py = (unsigned long long)w.z | ((unsigned long long)w.w << 32);
+    x = (unsigned long long)w.x | ((unsigned long long)w.y << 32);
+    y = (unsigned long long)w.z | ((unsigned long long)w.w << 32);
   };
   // a message = one 16-byte sc1 store (write-through, aux 16) of {flow, avg}: one fabric write
   // instead of two 8-byte ones (narrow sc1 stores cost 2.7x per byte, MI355X_MICROARCH.md)
@@ -1823,49 +1839,74 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
     const u4 w = {(unsigned)fb, (unsigned)(fb >> 32), (unsigned)ab, (unsigned)(ab >> 32)};
     __builtin_amdgcn_raw_buffer_store_b128(w, prs, msg * 16, 0, 16);
   };
+  // the slots of the first two receives among the ring's next kScan events (scratch if fewer;
+  // scratch is never a message slot)
+#define FU_NEXT_RECVS(ida, idb)                                              \
+  do {                                                                       \
+    ida = idb = scratch;                                                     \
+    _Pragma("unroll") for (int j = 0; j < kScan; ++j) {                      \
+      const int4 e = ev_dec(ring[((rh + j) & (kRing - 1)) * kBlock]);        \
+      if (j < rv && e.w < tick_end && e.x == FU_EV_RECV) {                   \
+        if (ida == scratch) ida = e.z;                                       \
+        else if (idb == scratch) idb = e.z;                                  \
+      }                                                                      \
+    }                                                                        \
+  } while (0)
   {
-    const int4 h = ring[rh * kBlock];
-    poll(rv > 0 && h.w < tick_end && h.x == FU_EV_RECV ? h.z : scratch);
-    if (!CA) send(scratch, 0.0, 0.0);
+    int ia, ib;
+    FU_NEXT_RECVS(ia, ib);
+    pa = ia;
+    ld16(ia, ax, ay);
+    pb = ib;
+    ld16(ib, bx, by);
+    if (!CA) {
+      send(scratch, 0.0, 0.0);
+      send(scratch, 0.0, 0.0);
+    }
   }
   long long it = 0;
   bool done = false;
   for (;;) {
     if (pend) FU_RING_COMMIT();
-    const int4 h0 = ring[rh * kBlock];
+    const int4 h0 = ev_dec(ring[rh * kBlock]);
     done = rv > 0 ? h0.w >= tick_end : !pend && fill >= pe;
     if (__all(done)) break;
     bool prog = false;
-    int poll_id = scratch;  // the iteration's poll and store targets
-    int out_id = scratch;
-    double out_f = 0.0, out_a = 0.0;
+    int o1 = scratch, o2 = scratch;  // the iteration's (at most two) pairwise messages
+    double f1 = 0.0, a1 = 0.0, f2 = 0.0, a2 = 0.0;
     if (!done && rv > 0) {
-      int m = 0;  // events run this iteration
+      int m = 0;   // events run this iteration
+      int nfo = 0; // pairwise fires this iteration
 #pragma unroll
       for (int k = 0; k < kRW; ++k) {
         if (k >= rv) break;
-        const int4 ev = k == 0 ? h0 : ring[((rh + k) & (kRing - 1)) * kBlock];
+        const int4 ev = k == 0 ? h0 : ev_dec(ring[((rh + k) & (kRing - 1)) * kBlock]);
         const int tk = ev.w;
         if (tk >= tick_end) break;
-        if (ev.x == FU_EV_RECV) {
-          // a receive that became the head this iteration, or whose message has not arrived:
-          // poll it at the end of the iteration, check it in the next
-          if (k > 0 || polled != ev.z || px == kMsgSentinel || py == kMsgSentinel) {
-            poll_id = ev.z;
-            break;
+        unsigned long long mx = 0, my = 0;
+        if (ev.x == FU_EV_RECV) {  // its payload must be one of the two polls, arrived
+          if (pa == ev.z && ax != kMsgSentinel && ay != kMsgSentinel) {
+            mx = ax;
+            my = ay;
+            pa = -1;
+          } else if (pb == ev.z && bx != kMsgSentinel && by != kMsgSentinel) {
+            mx = bx;
+            my = by;
+            pb = -1;
+          } else {
+            break;  // not arrived (or not polled yet): polled again at the end
           }
-        } else if (!CA && out_id != scratch) {
-          break;  // one pairwise message per iteration
+        } else if (!CA && nfo == 2) {
+          break;  // two pairwise messages per iteration
         }
         while (sc < n_snap && snap_ticks[sc] < tk) snaps[(long long)sc++ * n + node] = lst;
         if (ev.x == FU_EV_RECV) {  // CA:98-99 / PW:98-99
 #pragma unroll
           for (int j = 0; j < MAXD; ++j)
             if (j == ev.y) {
-              es[j] = __longlong_as_double((long long)py);
-              fl[j] = -__longlong_as_double((long long)px);
+              es[j] = __longlong_as_double((long long)my);
+              fl[j] = -__longlong_as_double((long long)mx);
             }
-          px = py = kMsgSentinel;
         } else if (CA && ev.x == FU_EV_FIRE_CA) {  // CA:105-125
           const int kk = ev.y;
           double S = 0.0, T = 0.0;
@@ -1907,10 +1948,18 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
               fl[j] = nf;
               es[j] = avg;
             }
-          if (CA) send(ev.z, nf, avg);
-          out_id = ev.z;
-          out_f = nf;
-          out_a = avg;
+          if (CA) {
+            send(ev.z, nf, avg);
+          } else if (nfo == 0) {
+            o1 = ev.z;
+            f1 = nf;
+            a1 = avg;
+          } else {
+            o2 = ev.z;
+            f2 = nf;
+            a2 = avg;
+          }
+          ++nfo;
         }
         ++m;
       }
@@ -1922,8 +1971,18 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
       }
     }
     if (!pend && rv <= kRing - kRefill && fill < pe) FU_RING_REFILL();  // lands during the next pass
-    poll(poll_id);                          // the youngest load ...
-    if (!CA) send(out_id, out_f, out_a);    // ... and the one store after it
+    {  // the youngest operations, in this order every iteration: two polls, then two stores
+      int ia, ib;
+      FU_NEXT_RECVS(ia, ib);
+      pa = ia;
+      ld16(ia, ax, ay);
+      pb = ib;
+      ld16(ib, bx, by);
+      if (!CA) {
+        send(o1, f1, a1);
+        send(o2, f2, a2);
+      }
+    }
     if (!__any(prog)) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
@@ -1938,12 +1997,16 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
       flow[rb + j] = fl[j];
       est[rb + j] = es[j];
     }
+#ifdef FU_REPLAY_ITPRINT
+  if ((node & 8191) == 0) printf("replay lane %d: %lld iterations, p %lld\n", node, it, p);
+#endif
   cursor[node] = p;
   scur[node] = sc;
   last[node] = lst;
 }
 #undef FU_RING_REFILL
 #undef FU_RING_COMMIT
+#undef FU_NEXT_RECVS
 
 
 template <typename T>
@@ -3538,7 +3601,7 @@ struct fu_replay {
   std::vector<int32_t> h_tasks, h_events, h_out_ids;
   long long *node_off = nullptr, *cursor = nullptr;
   int4 *node_ev = nullptr;
-  int4 *node_evt = nullptr;  // register kernel: packed {type, slot | k << 8, msg, tick}
+  int2 *node_evt = nullptr;  // register kernel: packed 8-byte events (ev_dec)
   int *node_tick = nullptr, *out_uid = nullptr, *scur = nullptr, *status = nullptr;
   unsigned long long *pay = nullptr;
   int64_t n_uid = 0;
@@ -3553,7 +3616,7 @@ constexpr int kReplayRegDeg = 16;
 // The register variant for the trace: row registers for degree <= 8 or <= 16, the collect-all
 // fire path only when the trace has one (both cost registers, and the variant must keep
 // every node's thread resident).
-using ReplayRegKernel = void (*)(int, int, const long long *, const int4 *, const int *, int,
+using ReplayRegKernel = void (*)(int, int, const long long *, const int2 *, const int *, int,
                                  const long long *, const double *, double *, double *, double *,
                                  unsigned long long *, long long *, int *, int, const int *, double *, int *,
                                  long long);
@@ -3572,7 +3635,8 @@ static int replay_build_persistent(fu_replay *r) {
   std::vector<int64_t> pos(off.begin(), off.end() - 1);
   std::vector<int4> nev(ne > 0 ? ne : 1);
   std::vector<int32_t> ntick(ne > 0 ? ne : 1);
-  std::vector<int4> nevt(ne > 0 ? ne : 1);
+  std::vector<int2> nevt(ne > 0 ? ne : 1);
+  bool pack_ok = r->ticks < (1 << 20);  // the register kernel's 8-byte events: tick < 2^20, slot, k < 32
   std::vector<int32_t> ouid(r->h_out_ids.size() > 0 ? r->h_out_ids.size() : 1);
   std::vector<int64_t> slot_uid(r->n_msgs > 0 ? r->n_msgs : 1, -1);
   int64_t U = 0;
@@ -3598,9 +3662,14 @@ static int replay_build_persistent(fu_replay *r) {
         }
         if (U >= (int64_t)INT32_MAX) return fail(FU_ERR_ALLOC, "replay: more than 2^31 messages");
         nev[pos[node]] = o;
-        nevt[pos[node]] = o.x == FU_EV_RECV      ? make_int4(o.x, o.y, o.z, t)
-                          : o.x == FU_EV_FIRE_CA ? make_int4(o.x, o.y, o.z, t)
-                                                 : make_int4(o.x, o.y | (o.z << 8), o.w, t);
+        {
+          const int sl = o.x == FU_EV_FIRE_CA ? 0 : o.y;
+          const int kk = o.x == FU_EV_FIRE_CA ? o.y : o.x == FU_EV_FIRE_PW ? o.z : 0;
+          pack_ok &= sl < 32 && kk < 32;
+          nevt[pos[node]] = make_int2((int)((unsigned)o.x | (unsigned)(sl & 31) << 2 | (unsigned)(kk & 31) << 7 |
+                                            (unsigned)t << 12),
+                                      o.x == FU_EV_FIRE_PW ? o.w : o.z);
+        }
         ntick[pos[node]++] = t;
       }
     }
@@ -3619,7 +3688,7 @@ static int replay_build_persistent(fu_replay *r) {
   HIP_TRY(hipMemcpy(r->node_off, off.data(), sizeof(int64_t) * (n + 1), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->node_ev, nev.data(), sizeof(int4) * nev.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->node_tick, ntick.data(), sizeof(int32_t) * ntick.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(r->node_evt, nevt.data(), sizeof(int4) * nevt.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(r->node_evt, nevt.data(), sizeof(int2) * nevt.size(), hipMemcpyHostToDevice));
   HIP_TRY(hipMemcpy(r->out_uid, ouid.data(), sizeof(int32_t) * ouid.size(), hipMemcpyHostToDevice));
   std::vector<long long> cur(off.begin(), off.end() - 1);
   HIP_TRY(hipMemcpy(r->cursor, cur.data(), sizeof(long long) * n, hipMemcpyHostToDevice));
@@ -3642,7 +3711,7 @@ static int replay_build_persistent(fu_replay *r) {
   HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_reg, replay_reg_kernel(r), kBlock, 0));
   const long long cap_reg = (long long)std::max(0, per_cu_reg - 1) * ncu;
   // (and 16-byte payload polls at 32-bit byte offsets: below 2^27 messages)
-  r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg && U + n < (1LL << 27);
+  r->reg_ok = r->max_deg <= kReplayRegDeg && (long long)grid_for(r->n) <= cap_reg && U + n < (1LL << 27) && pack_ok;
   r->pers_ready = true;
   return FU_OK;
 }
