@@ -2070,6 +2070,7 @@ struct fu_handle {
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
+  int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
@@ -2725,13 +2726,17 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // the rows of the heavy tiles [nmega, m1) (4 rows each, longest first: every row of more
   // than 64 x kHeavyRL edges, and the few shorter ones sharing the last tile) as
   // k_heavy_multi blocks, many rows per chain wave
-  const int n_multi = std::min(h->multi_geo[1][1], 4 * (m1 - nmega));
+  // (multi_mid = 0: only the rows of [nmega, m0), longer than the register launch's; the rows
+  // of [m0, m1) then stay in registers, one pass)
+  const int mend = h->multi_mid ? m1 : m0;
+  const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
   const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && D == 0 && n_multi > 0;
   auto tiles = [&](auto C) {
     if (multi) {
       hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value>), dim3((n_multi + kMR - 1) / kMR), dim3(kBlock), 0,
                          h->stream, h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F, c.ap2, c.an,
                          h->target, c.err, h->code[r1], h->pctl, Gb, c.fm);
+      if (!h->multi_mid) heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     } else {
       heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
       heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
@@ -3181,6 +3186,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
     h->multi_heavy = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "multi_mid")) {  // kernel 9: rows of 257-1024 edges in k_heavy_multi (1) or in registers (0)
+    h->multi_mid = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "mid_heavy")) {  // kernel 9: register-resident launch for rows of 257-1024 edges

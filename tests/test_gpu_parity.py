@@ -582,19 +582,23 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0])
+@pytest.mark.parametrize("multi", [1, 0, "mid0"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
     block, one wave running all 32 chains) against the C oracle, with rounds 1-2 (no flow
     reads), the error check on every round (CHECK), packing every 4 rounds, rows of every
     length from the threshold to the mega hubs (ragged ends of the last chunk), and the
-    one-row-per-wave path (multi_heavy 0) for A/B."""
+    one-row-per-wave path (multi_heavy 0) and the rows of 257-1024 edges in registers
+    (multi_mid 0) for A/B."""
     g = fu.Graph.rmat(15, 16, seed=33)
     v = fu.uniform_values(g.n, seed=33)
     eng = fu.CollectAll(g, v, kernel="pregather", hub_threshold=ht, layout="degree")
     eng.set_option("mega_hub", mega)
-    eng.set_option("multi_heavy", multi)
+    if multi == "mid0":
+        eng.set_option("multi_mid", 0)
+    else:
+        eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
     tgt, _ = fu.component_means(g.rowptr, g.col, v)
     eng.set_targets(tgt)
