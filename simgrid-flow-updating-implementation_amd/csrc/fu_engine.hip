@@ -1177,6 +1177,149 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   }
 }
 
+// k_transpose software-pipelined over the block's buckets (option tr_pipe): the G_A and
+// position loads of bucket k + 1 are in flight while bucket k is scattered into LDS and
+// stored, and bucket k + 1's run table and searches are built while bucket k's loads land.
+// Every iteration issues the same loads (a missing next bucket reads element 0 and ignores
+// it), so the wait for bucket k's loads leaves bucket k + 1's in flight. Same G_B as
+// k_transpose.
+__global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, int P, long long E,
+                                                             const int *__restrict__ offT,
+                                                             const double *__restrict__ GA,
+                                                             const unsigned short *__restrict__ pos16,
+                                                             double *__restrict__ GB) {
+  __shared__ double s_v[kTrBE];
+  __shared__ unsigned short s_m[kTrMaxP + 1];
+  __shared__ int s_o[kTrMaxP];
+  __shared__ int s_c[kTrBE / 64 + 1];
+  __shared__ int s_w[kTrThreads / 64];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int per = (nbk + 7) >> 3;
+  const int nj = (int)(gridDim.x >> 3);
+  int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+  const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
+  if (bk >= bend) return;
+  constexpr int kPerT = kTrBE / kTrThreads;
+  int o[2], len[2];
+  auto load_runs = [&](int bkk) {  // clamped: a bucket past the range loads the last one's
+    const int bb = b0 + min(bkk, bend - 1);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int sl = min(2 * t + j, P - 1);
+      const int a0 = offT[(long long)bb * P + sl], a1 = offT[(long long)(bb + 1) * P + sl];
+      o[j] = 2 * t + j < P ? a0 : 0;
+      len[j] = 2 * t + j < P ? a1 - a0 : 0;
+    }
+  };
+  // run table of the bucket whose runs are in o / len: s_m (first element of each run),
+  // s_o (its G_A index), s_c (coarse table); returns the staged element count
+  auto tables = [&]() -> int {
+    int x = len[0] + len[1];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off, 64);
+      if (lane >= off) x += y;
+    }
+    __syncthreads();  // the previous bucket's searches are done with the tables
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    int base = 0;
+    for (int k = 0; k < w; ++k) base += s_w[k];
+    const int excl = base + x - (len[0] + len[1]);
+    if (2 * t < P) {
+      s_m[2 * t] = excl;
+      s_o[2 * t] = o[0];
+    }
+    if (2 * t + 1 < P) {
+      s_m[2 * t + 1] = excl + len[0];
+      s_o[2 * t + 1] = o[1];
+    }
+    if (t == 0) {
+      int tot = 0;
+      for (int k = 0; k < kTrThreads / 64; ++k) tot += s_w[k];
+      s_m[P] = tot;
+    }
+    __syncthreads();
+    const int nst = s_m[P];
+    if (t < kTrBE / 64) {
+      const int m = t * 64;
+      int lo = 1, hi = P;
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (s_m[mid] > m) hi = mid; else lo = mid + 1;
+      }
+      s_c[t] = lo;
+    }
+    if (t == 0) s_c[kTrBE / 64] = P;
+    __syncthreads();
+    return nst;
+  };
+  auto search = [&](int nst, int (&g)[kPerT]) {
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) {
+      const int m = t + k * kTrThreads;
+      g[k] = -1;
+      if (m < nst) {
+        int lo = s_c[m >> 6], hi = s_c[(m >> 6) + 1];
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (s_m[mid] > m) hi = mid; else lo = mid + 1;
+        }
+        const int run = lo - 1;
+        g[k] = s_o[run] + (m - s_m[run]);
+      }
+    }
+  };
+  auto issue = [&](const int (&g)[kPerT], double (&val)[kPerT], int (&pos)[kPerT]) {
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) {  // unconditional, from a valid index
+      const int q = max(g[k], 0);
+      val[k] = GA[q];
+      pos[k] = g[k] >= 0 ? (int)pos16[q] : -1;
+    }
+  };
+  // bucket cur: the loads in (val, pos) -> s_v by position -> G_B, coalesced
+  auto finish = [&](int cur, const double (&val)[kPerT], const int (&pos)[kPerT]) {
+    const long long e0 = (long long)(b0 + cur) * kTrBE;
+    const int ne = (int)min((long long)kTrBE, E - e0);
+    __syncthreads();  // the previous bucket's G_B stores have read s_v
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k)
+      if (pos[k] >= 0) s_v[pos[k]] = val[k];
+    __syncthreads();
+    for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
+  };
+  int gA[kPerT], gB[kPerT], pA[kPerT], pB[kPerT];
+  double vA[kPerT], vB[kPerT];
+  load_runs(bk);
+  search(tables(), gA);
+  load_runs(bk + nj);
+  issue(gA, vA, pA);
+  // one step: build + issue bucket nx's loads into N, then finish bucket cur from C
+  auto step = [&](int cur, int (&gN)[kPerT], double (&vN)[kPerT], int (&pN)[kPerT],
+                  const double (&vC)[kPerT], const int (&pC)[kPerT]) -> bool {
+    const int nx = cur + nj;
+    const bool more = nx < bend;
+    {
+      const int nst = tables();  // (runs of nx, or the clamped last bucket's: ignored)
+      search(nst, gN);
+      if (!more)
+#pragma unroll
+        for (int k = 0; k < kPerT; ++k) gN[k] = -1;
+    }
+    load_runs(nx + nj);
+    issue(gN, vN, pN);
+    finish(cur, vC, pC);
+    return more;
+  };
+  for (;;) {
+    if (!step(bk, gB, vB, pB, vA, pA)) break;
+    bk += nj;
+    if (!step(bk, gA, vA, pA, vB, pB)) break;
+    bk += nj;
+  }
+}
+
 // DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
 // 2 = no stage launch and G read as in 1 (prices the round without staging), 3 = 2 without
 // the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
@@ -1997,9 +2140,6 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
       flow[rb + j] = fl[j];
       est[rb + j] = es[j];
     }
-#ifdef FU_REPLAY_ITPRINT
-  if ((node & 8191) == 0) printf("replay lane %d: %lld iterations, p %lld\n", node, it, p);
-#endif
   cursor[node] = p;
   scur[node] = sc;
   last[node] = lst;
@@ -2069,6 +2209,7 @@ struct fu_handle {
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
+  int tr_pipe = 0;       // kernel 9: software-pipelined transpose (k_transpose_pipe; needs tr_bpx > 0)
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
@@ -2690,15 +2831,16 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   }
   plan_alone(h, c);
   const int bh = hubs ? h->tr.Bh : 0;
+  auto ktr = h->tr_pipe && h->tr_bpx > 0 ? k_transpose_pipe : k_transpose;
   if (D != 21 && D != 24 && bh)
-    hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
+    hipLaunchKernelGGL(ktr, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
                        (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
   if (hubs) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
   if (D != 21 && D != 24 && h->tr.B > bh)
-    hipLaunchKernelGGL(k_transpose, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh, h->tr.B - bh,
+    hipLaunchKernelGGL(ktr, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh, h->tr.B - bh,
                        h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
   const bool chk = c.err && !D;
   if (hubs) {
@@ -3177,6 +3319,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
     h->staged_lo = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "tr_pipe")) {  // kernel 9: software-pipelined transpose (1)
+    h->tr_pipe = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_bpx")) {  // kernel 9: transpose blocks per XCD (0 = one per bucket)

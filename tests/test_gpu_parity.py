@@ -490,14 +490,16 @@ def test_packed_gather_long_run_bitwise(kind, kernel):
     assert np.array_equal(off.estimates(), a_ref)
 
 
-@pytest.mark.parametrize("opts", [{"staged_lo": 0}, {"staged_lo": 0, "pack": 0}, {"tr_bpx": 0}])
+@pytest.mark.parametrize("opts", [{"staged_lo": 0}, {"staged_lo": 0, "pack": 0}, {"tr_bpx": 0},
+                                  {"tr_pipe": 1}, {"tr_pipe": 1, "tr_bpx": 3}])
 def test_load_order_and_transpose_options_bitwise(opts):
     """The A/B options of this round (kernel 8's interleaved load order; kernel 9's
     one-block-per-bucket transpose) give the C oracle's bits over a 300-round run with packing
     and escapes."""
     g, v = _er_with_outlier_pairs(100_000, 400_000, 64, seed=5)
     rounds = 300
-    eng = fu.CollectAll(g, v, kernel="pregather" if "tr_bpx" in opts else "stage", hub_threshold=16)
+    eng = fu.CollectAll(g, v, kernel="pregather" if {"tr_bpx", "tr_pipe"} & set(opts) else "stage",
+                        hub_threshold=16)
     eng.set_option("pack_every", 4)
     for k, val in opts.items():
         eng.set_option(k, val)
@@ -582,7 +584,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -597,6 +599,8 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     eng.set_option("mega_hub", mega)
     if multi == "mid0":
         eng.set_option("multi_mid", 0)
+    elif multi == "pipe":
+        eng.set_option("tr_pipe", 1)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)

@@ -30,6 +30,7 @@ VARIANTS = {
     "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
     "pre_multi0": ("pregather", {"layout": "degree", "pack": 0, "multi_heavy": 0}),
     "pre_multimid0": ("pregather", {"layout": "degree", "pack": 0, "multi_mid": 0}),
+    "pre_trpipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
