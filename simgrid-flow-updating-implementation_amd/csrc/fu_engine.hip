@@ -439,7 +439,9 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     unsigned long long *__restrict__ err,
     const void *__restrict__ code_prev, void *__restrict__ code_new, PackCtl *__restrict__ ctl,
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
-    const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb, int fm) {
+    const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb, int fm,
+    const unsigned short *__restrict__ col16 = nullptr, const int *__restrict__ cbase = nullptr,
+    const int *__restrict__ tnar = nullptr) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -739,14 +741,31 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     // the column indices first, then the flows (RF: round >= 3) and node words, every load
     // unconditional from a clamped index (col and F hold at least one element / 32-edge
     // block), so the gathers wait for the indices alone (in-order completion, vmcnt(N))
+    // narrow tiles (tnar: every 1024-edge block of the tile has its columns within 32K ids of
+    // the block's first row, cbase): a 2-byte offset per edge instead of the 4-byte column.
+    // The column is formed after the flow and node loads are issued (below), so those stay
+    // in flight while the gathers wait for the indices.
+    const bool narrow = tnar && tnar[blockIdx.x];
+    int cw[kPer], bs[kPer];
+    if (narrow) {
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int q = t + k * kBlock;
-      const int ci = q < ne ? e0 + q : (ne > 0 ? e0 : 0);
-      const int cv = NT ? ld_stream(col + ci) : col[ci];
-      c[k] = q < ne ? cv : 0;
-      g[k] = 0.0;
+      for (int k = 0; k < kPer; ++k) {
+        const int q = t + k * kBlock;
+        const int ci = q < ne ? e0 + q : (ne > 0 ? e0 : 0);
+        cw[k] = col16[ci];
+        bs[k] = cbase[ci >> 10];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const int q = t + k * kBlock;
+        const int ci = q < ne ? e0 + q : (ne > 0 ? e0 : 0);
+        cw[k] = NT ? ld_stream(col + ci) : col[ci];
+        bs[k] = 32768;
+      }
     }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) g[k] = 0.0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
@@ -767,6 +786,8 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     if constexpr (TN == kBlock) rp_last = (t == 0 && nn == kBlock) ? rl0 : 0;
     vv = t < nn ? v0 : 0.0;
     own2 = t < nn ? o0 : 0.0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) c[k] = t + k * kBlock < ne ? bs[k] + cw[k] - 32768 : 0;
   }
   if (PRE) {
   } else if (DIAG != 0 || pp.width == 0) {
@@ -2194,6 +2215,9 @@ struct fu_handle {
   int32_t max_deg = 0;
   int *rowptr = nullptr, *col = nullptr;
   int *blk_row = nullptr;  // round 0: row of edge b * kR0E for every block b, then of edge E - 1
+  unsigned short *col16 = nullptr;  // kernel 4 narrow tiles: col - cbase[e >> 10] + 32768 (0 where wide)
+  int *cbase = nullptr;             // per 1024-edge block: its first edge's row, or -1 (a column >= 32K ids away)
+  std::vector<int32_t> h_cbase;
   double *v = nullptr;
   double *f[2] = {nullptr, nullptr};           // F[r & 1]: f_{r-2} in, f_r out (split words)
   double *a[3] = {nullptr, nullptr, nullptr};  // A[r % 3] = a_r
@@ -2211,6 +2235,7 @@ struct fu_handle {
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
   int tr_pipe = 0;       // kernel 9: software-pipelined transpose (k_transpose_pipe; needs tr_bpx > 0)
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
+  int c16 = 1;           // kernel 4: narrow light tiles read 2-byte column offsets
   int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
@@ -2234,6 +2259,7 @@ struct fu_handle {
   // kernel 4 tiles per geometry (all four built up front so autotuning can switch between
   // rounds): mega hubs, heavy rows, then light tiles
   int4 *tiles_geo[4] = {nullptr, nullptr, nullptr, nullptr};
+  int *tnar_geo[4] = {nullptr, nullptr, nullptr, nullptr};  // per tile: narrow (col16) or not (int: a scalar load)
   int ntiles_geo[4] = {0, 0, 0, 0};
   int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
   int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
@@ -2307,7 +2333,8 @@ constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 // Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
 // block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
 // {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *nheavy, int *nbound, int *mid,
+int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *count, int *nheavy,
+                     int *nbound, int *mid,
                      int *multi) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
@@ -2377,12 +2404,25 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int *count, int *
     auto mid = std::stable_partition(light.begin(), light.end(), has_ghost);
     *nbound = (int)(mid - light.begin());
   }
+  const size_t nlead = all.size();
   all.insert(all.end(), light.begin(), light.end());
   if (*dst) hipFree(*dst);
   *dst = nullptr;
   *count = (int)all.size();
   if (int rc = dmalloc(dst, all.size())) return rc;
   HIP_TRY(hipMemcpy(*dst, all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
+  // light tiles whose 1024-edge blocks are all narrow read the 2-byte column offsets
+  std::vector<int32_t> nf(all.size(), 0);
+  for (size_t q = nlead; q < all.size(); ++q) {
+    const int64_t a0 = all[q].z, a1 = all[q].w;
+    bool ok = a1 > a0;
+    for (int64_t b = a0 / kR0E; ok && b <= (a1 - 1) / kR0E; ++b) ok = h->h_cbase[b] >= 0;
+    nf[q] = ok ? 1 : 0;
+  }
+  if (*nar) hipFree(*nar);
+  *nar = nullptr;
+  if (int rc = dmalloc(nar, nf.size())) return rc;
+  HIP_TRY(hipMemcpy(*nar, nf.data(), sizeof(int32_t) * nf.size(), hipMemcpyHostToDevice));
   return FU_OK;
 }
 
@@ -2430,7 +2470,8 @@ int build_tiles(fu_handle *h) {
   free_transpose(h);  // its hub exclusion follows the tiles
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->ntiles_geo[g], &h->nheavy_geo[g],
+    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->tnar_geo[g], &h->ntiles_geo[g],
+                                  &h->nheavy_geo[g],
                                   &h->nbound_geo[g], h->mid_geo[g], h->multi_geo[g]))
       return rc;
   if (h->hrows) hipFree(h->hrows);
@@ -2939,7 +2980,7 @@ int launch_k4_geo(fu_handle *h, RoundCtx &c) {
                                         decltype(RF)::value>),
                          dim3(cnt), dim3(kBlock), 0, h->stream, tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr,
-                         c.fm);
+                         c.fm, h->col16, h->cbase, h->c16 ? h->tnar_geo[h->geo] + t0 : nullptr);
   };
   auto light_rf = [&](auto C, auto NT, int t0, int cnt) {
     if (c.fm) light(C, NT, std::false_type{}, t0, cnt);
@@ -3170,6 +3211,27 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     if ((rc = dmalloc(&h->blk_row, br.size()))) return cleanup(rc);
     if (hipMemcpy(h->blk_row, br.data(), sizeof(int32_t) * br.size(), hipMemcpyHostToDevice) != hipSuccess)
       return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
+    // kernel 4's 2-byte column offsets: block b (edges [1024 b, 1024 b + 1024)) is narrow
+    // when every column lies within 32K ids of the block's first row (graphs with locality:
+    // RGG in cell order); a wide block keeps cbase -1 and its tiles read the 4-byte columns
+    std::vector<uint16_t> c16(std::max<int64_t>(e, 1), 0);
+    h->h_cbase.assign(std::max<int64_t>(nblk, 1), -1);
+    for (int64_t b = 0; b < nblk; ++b) {
+      const int32_t base = br[b];
+      bool ok = true;
+      const int64_t k1 = std::min<int64_t>(e, (b + 1) * kR0E);
+      for (int64_t k = b * kR0E; k < k1 && ok; ++k) {
+        const int64_t d = (int64_t)col[k] - base + 32768;
+        ok = d >= 0 && d <= 65535;
+      }
+      if (!ok) continue;
+      h->h_cbase[b] = base;
+      for (int64_t k = b * kR0E; k < k1; ++k) c16[k] = (uint16_t)((int64_t)col[k] - base + 32768);
+    }
+    if ((rc = dmalloc(&h->col16, c16.size())) || (rc = dmalloc(&h->cbase, h->h_cbase.size()))) return cleanup(rc);
+    if (hipMemcpy(h->col16, c16.data(), sizeof(uint16_t) * c16.size(), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(h->cbase, h->h_cbase.data(), sizeof(int32_t) * h->h_cbase.size(), hipMemcpyHostToDevice) != hipSuccess)
+      return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
   }
   if ((rc = build_tiles(h))) return cleanup(rc);
   if ((rc = dmalloc(&h->pctl, 3)) || (rc = dmalloc(&h->code[0], 4 * (size_t)na)) ||
@@ -3332,6 +3394,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
     h->multi_heavy = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "c16")) {  // kernel 4: 2-byte column offsets for narrow light tiles (1) or not (0)
+    h->c16 = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "multi_mid")) {  // kernel 9: rows of 257-1024 edges in k_heavy_multi (1) or in registers (0)
@@ -3715,7 +3781,8 @@ int fu_destroy(fu_handle *h) {
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
                               h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,
-                              h->psample, h->st_tiles, h->st_heavy, h->stG};
+                              h->psample, h->st_tiles, h->st_heavy, h->stG, h->col16, h->cbase,
+                              h->tnar_geo[0], h->tnar_geo[1], h->tnar_geo[2], h->tnar_geo[3]};
   free_transpose(h);
   for (const auto &L : h->st) {
     ptrs.push_back(L.brange);

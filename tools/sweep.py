@@ -16,6 +16,7 @@ import fu  # noqa: E402
 VARIANTS = {
     "recon": ("recon", {"tile_edges": 2048}),
     "recon_1024": ("recon", {"tile_edges": 1024}),
+    "recon_1024_c16off": ("recon", {"tile_edges": 1024, "c16": 0}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
     "recon_512": ("recon", {"tile_edges": 512}),
     "recon_nt": ("recon", {"nt": 1}),
