@@ -71,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target length of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-conv", action="store_true")
+    ap.add_argument("--no-unit", action="store_true",
+                    help="N = 1 default line without its weak_scaling_unit (config 5's per-GPU RGG)")
     return ap.parse_args(argv)
 
 
@@ -271,8 +273,10 @@ def run_single(args, wl):
         "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen,
     }
     out.update(conv)
-    print(json.dumps(out), flush=True)
     eng.close()
+    if args.workload == "auto" and not args.no_unit:
+        out["weak_scaling_unit"] = weak_unit(args)
+    print(json.dumps(out), flush=True)
 
 
 def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_total, per, kinfo,
@@ -319,6 +323,30 @@ def run_dist(args, world, rank, local, dist):
     """BASELINE config 5 (weak scaling): RGG with --n nodes per GPU (2^23 by default), one
     global graph cut into x-slabs (fu_part_gen_rgg: no rank builds the global graph), kernel 4
     with the estimates-only RCCL halo. value = all ranks' edge updates / max-over-ranks time."""
+    line = measure_dist(args, world, rank, local, dist)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def weak_unit(args):
+    """The N = 1 line's companion: BASELINE config 5's per-GPU unit (RGG 2^23 through the
+    partitioned path, one rank, the same steps and warmup), measured live in the same run, so
+    that the driver's N > 1 lines (which run that workload) have their one-GPU counterpart."""
+    a = argparse.Namespace(**vars(args))
+    a.n, a.kernel, a.no_conv = 0, "auto", True
+    line = measure_dist(a, 1, 0, 0, None)
+    return {"workload": line["config"]["workload"], "value": line["value"], "unit": line["unit"],
+            "ms_per_step": line["ms_per_step"], "E_directed": line["config"]["E_directed"],
+            "kernel_selected": line["config"]["kernel_selected"],
+            "tile_selected": line["config"]["tile_selected"],
+            "roofline_frac": line["roofline"]["frac"], "avg_round_us": line["roofline"]["avg_launch_us"],
+            "note": "measured in this run: compare the driver's N > 1 lines (value_per_gpu) with this"}
+
+
+def measure_dist(args, world, rank, local, dist):
+    """One rgg-dist measurement; returns rank 0's JSON line (None on other ranks)."""
     import torch
 
     import fu
@@ -381,15 +409,14 @@ def run_dist(args, world, rank, local, dist):
     elif world > 1:
         conv["conv_note"] = ("per-component targets need the global graph; see the one-rank line "
                              "of the same per-GPU unit")
+    line = None
     if rank == 0:
-        print(json.dumps(dist_line(world=world, steps=args.steps, warmup=args.warmup, wall=wall,
-                                   dev1_ms=dev1, e_tot=e_tot, n_tot=n_tot, halo=halo,
-                                   n_total=n_total, per=per, kinfo=kinfo, halo_us=halo_us,
-                                   round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
-                                   conv=conv)), flush=True)
+        line = dist_line(world=world, steps=args.steps, warmup=args.warmup, wall=wall, dev1_ms=dev1,
+                         e_tot=e_tot, n_tot=n_tot, halo=halo, n_total=n_total, per=per, kinfo=kinfo,
+                         halo_us=halo_us, round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
+                         conv=conv)
     eng.close()
-    if dist is not None:
-        dist.destroy_process_group()
+    return line
 
 
 def convergence(eng, rowptr, col, v, rounds):
