@@ -120,6 +120,11 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 the whole row in registers (default 1).
  * "tr_bpx"        kernel 9: transpose blocks per XCD, each looping over buckets (default 32;
  *                 0 = one block per bucket).
+ * "multi_heavy"   kernel 9: rows of more than 256 edges as multi-row chain blocks (default 1);
+ *                 "multi_mid" 0 keeps the rows of 257-1024 edges in the register launch.
+ * "tr_pipe"       kernel 9: software-pipelined transpose (default 0; needs tr_bpx > 0).
+ * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
+ *                 32K ids of their 1024-edge block's first row (default 1).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).
  * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster
  *                 (default 1); "pack_every" rounds between encoding plans (default 16).
