@@ -74,3 +74,10 @@ def test_dist_line_schema():
     assert line["cpu_baseline"] is None and "one_rank_reference" not in line
     json_text = __import__("json").dumps(line)
     assert "profiles/" not in json_text  # nothing read from committed files
+
+
+def test_weak_unit_flag():
+    """The default N = 1 line measures config 5's per-GPU unit beside the headline (on the
+    GPU); --no-unit skips it."""
+    assert bench.parse([]).no_unit is False
+    assert bench.parse(["--no-unit"]).no_unit is True
