@@ -529,12 +529,14 @@ def test_packed_gather_with_kernel_switches():
                                          ("recon", {"tile_edges": 1024}),
                                          ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
                                          ("recon", {"tile_edges": 512})])
-@pytest.mark.parametrize("kind", ["er", "rmat"])
+@pytest.mark.parametrize("kind", ["er", "rmat", "rgg"])
 def test_tile_geometries_bitwise(kernel, opts, kind):
     """Every kernel 4 tile geometry the autotuner may pick, with heavy rows (hub_threshold 16
     on R-MAT), against the C oracle."""
     if kind == "er":
         g = fu.Graph.erdos_renyi(200_000, 800_000, seed=6)
+    elif kind == "rgg":  # narrow tiles: 2-byte column offsets (c16)
+        g = fu.Graph.random_geometric(200_000, avg_deg=8, seed=6)
     else:
         g = fu.Graph.rmat(14, 16, seed=6)
     v = fu.uniform_values(g.n, seed=6)
@@ -821,3 +823,30 @@ def test_random_configurations_bitwise(seed):
     a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, rounds, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref), (fam, layout)
     assert np.array_equal(eng.flows(), f_ref), (fam, layout)
+
+
+@pytest.mark.parametrize("tile", [2048, 1024, 512])
+def test_c16_narrow_and_wide_tiles_bitwise(tile):
+    """Kernel 4's 2-byte column offsets: an RGG (every 1024-edge block narrow) joined to an ER
+    block with random columns (wide) and a few long-range edges inside the RGG part (one wide
+    block among narrow ones), c16 on and off, against the C oracle."""
+    import numpy as np
+    a = fu.Graph.random_geometric(60_000, avg_deg=8, seed=8)
+    b = fu.Graph.erdos_renyi(20_000, 80_000, seed=8)
+    n = a.n + b.n
+    src = [np.repeat(np.arange(a.n), np.diff(a.rowptr)), np.repeat(np.arange(b.n), np.diff(b.rowptr)) + a.n]
+    dst = [np.asarray(a.col, dtype=np.int64), np.asarray(b.col, dtype=np.int64) + a.n]
+    far = np.array([[5, 45_000], [100, 79_000], [30_000, 70_123]], dtype=np.int64)  # long-range edges
+    s_ = np.concatenate(src + [far[:, 0], far[:, 1]])
+    d_ = np.concatenate(dst + [far[:, 1], far[:, 0]])
+    g = fu.Graph.from_edges(n, s_, d_)
+    v = fu.uniform_values(g.n, seed=8)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 25, nthreads=16)
+    for c16 in (1, 0):
+        eng = fu.CollectAll(g, v, kernel="recon")
+        eng.set_option("tile_edges", tile)
+        eng.set_option("c16", c16)
+        eng.run(25)
+        assert np.array_equal(eng.estimates(), a_ref), c16
+        assert np.array_equal(eng.flows(), f_ref), c16
+        eng.close()
