@@ -1894,16 +1894,18 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 // {receive, fire} every other tick), and an iteration ends waiting for its vector-memory
 // operations, which retire in issue order: loads, and the write-through message stores.
 // So an iteration issues as few of them as it can, in a fixed order:
-//   * the lane's next events sit in an 8-entry LDS ring, refilled 4 packed descriptors
-//     (64 contiguous bytes: {type, slot | k << 8, msg, tick}) at a time; they land during
-//     one iteration and are written to the ring at the head of the next;
-//   * the pairwise path (CA = false) ends every iteration with exactly ONE 16-byte sc1 poll
-//     (the head receive's payload, both tagged halves) and then exactly ONE 16-byte sc1
-//     store (the iteration's message {flow, avg}), each aimed at the node's scratch slot
-//     when there is none: the next iteration waits for the poll and leaves the youngest
-//     store in flight (vmcnt(1)), instead of waiting for every store's write-through;
-//   * an iteration runs up to kRW events in program order: a receive only as its first
-//     event (the poll issued for it), at most one pairwise fire.
+//   * the lane's next events sit in a 16-entry LDS ring of packed 8-byte descriptors
+//     (ev_dec), refilled 8 at a time (64 contiguous bytes); they land during one iteration
+//     and are written to the ring at the head of the next;
+//   * every iteration ends with exactly TWO 16-byte sc1 polls (the payloads of the lane's
+//     next two receives, both tagged halves each) and then, on the pairwise path
+//     (CA = false), exactly TWO 16-byte sc1 stores (the iteration's messages {flow, avg}),
+//     each aimed at the node's scratch slot when there is none: the next iteration waits
+//     for the polls and leaves the stores in flight (vmcnt(2)), instead of waiting for every
+//     store's write-through;
+//   * an iteration runs up to kRW events in program order, a receive only once its payload
+//     has arrived in one of the two polls, at most two pairwise fires: RR-64K runs two
+//     {receive, fire} pairs per iteration.
 // The collect-all path (k messages per fire) stores its messages as it goes.
 #ifndef FU_REPLAY_SLEEP
 #define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
