@@ -71,6 +71,8 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=12.0,
                     help="target length of the CPU baseline sample (0 = skip)")
     ap.add_argument("--no-conv", action="store_true")
+    ap.add_argument("--strong", action="store_true",
+                    help="rgg-dist: strong scaling, --n nodes in all (2^26 by default) split over the ranks")
     ap.add_argument("--no-unit", action="store_true",
                     help="N = 1 default line without its weak_scaling_unit (config 5's per-GPU RGG)")
     return ap.parse_args(argv)
@@ -280,7 +282,7 @@ def run_single(args, wl):
 
 
 def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_total, per, kinfo,
-              halo_us, round_us, t_gen, conv):
+              halo_us, round_us, t_gen, conv, strong=False):
     """The N > 1 (rgg-dist) JSON line. Per GPU and round the algorithmic bytes are the §8(d)
     figure of the rank's rows (24 E + 28 N) plus the halo: 8 B per ghost estimate received
     (the RCCL payload written into the ghost slots; halo = ghost slots over all ranks)."""
@@ -290,9 +292,11 @@ def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_tota
     line = {
         "metric": METRIC, "value": e_tot * steps / wall, "unit": "edge-updates/s",
         "n_gpus": world, "steps": steps, "warmup": warmup,
-        "ms_per_step": wall * 1e3 / steps, "higher_is_better": True, "scaling": "weak",
+        "ms_per_step": wall * 1e3 / steps, "higher_is_better": True,
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic (seeded RGG, U[0,100) values)",
-        "config": {"workload": f"rgg-dist:n={n_total} ({per} per GPU), deg=8, x-slabs, "
+        "config": {"workload": f"rgg-dist:n={n_total} ({per} per GPU{', strong scaling' if strong else ''}), "
+                               "deg=8, x-slabs, "
                                "RCCL estimates-only halo every round",
                    "n_total": n_total, "E_directed": e_tot,
                    "rounds_timed": f"0-{steps - 1} from the zero state",
@@ -335,7 +339,7 @@ def weak_unit(args):
     partitioned path, one rank, the same steps and warmup), measured live in the same run, so
     that the driver's N > 1 lines (which run that workload) have their one-GPU counterpart."""
     a = argparse.Namespace(**vars(args))
-    a.n, a.kernel, a.no_conv = 0, "auto", True
+    a.n, a.kernel, a.no_conv, a.strong = 0, "auto", True, False
     line = measure_dist(a, 1, 0, 0, None)
     return {"workload": line["config"]["workload"], "value": line["value"], "unit": line["unit"],
             "ms_per_step": line["ms_per_step"], "E_directed": line["config"]["E_directed"],
@@ -352,8 +356,12 @@ def measure_dist(args, world, rank, local, dist):
     import fu
     from fu.dist import DistCollectAll, RggPart, unique_id
 
-    per = args.n or (1 << 23)
-    n_total = per * world
+    if args.strong:  # BASELINE config 5 as written: 2^26 nodes in all, split over the ranks
+        n_total = args.n or (1 << 26)
+        per = n_total // world
+    else:  # weak scaling: 2^23 nodes per GPU
+        per = args.n or (1 << 23)
+        n_total = per * world
     t = time.perf_counter()
     part = RggPart(n_total, avg_deg=8.0, seed=1, nparts=world, part=rank)
     v = part.values(seed=0)
@@ -414,7 +422,7 @@ def measure_dist(args, world, rank, local, dist):
         line = dist_line(world=world, steps=args.steps, warmup=args.warmup, wall=wall, dev1_ms=dev1,
                          e_tot=e_tot, n_tot=n_tot, halo=halo, n_total=n_total, per=per, kinfo=kinfo,
                          halo_us=halo_us, round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
-                         conv=conv)
+                         conv=conv, strong=args.strong)
     eng.close()
     return line
 

@@ -81,3 +81,14 @@ def test_weak_unit_flag():
     GPU); --no-unit skips it."""
     assert bench.parse([]).no_unit is False
     assert bench.parse(["--no-unit"]).no_unit is True
+
+
+def test_dist_line_strong_scaling():
+    """--strong (BASELINE config 5 as written: 2^26 nodes split over the ranks) is labelled."""
+    kinfo = {"kernel": "recon", "tile": (1024, 128)}
+    line = bench.dist_line(world=8, steps=20, warmup=5, wall=0.01, dev1_ms=6.0, e_tot=8 * 67_000_000,
+                           n_tot=1 << 26, halo=8 * 40_000, n_total=1 << 26, per=(1 << 26) // 8,
+                           kinfo=kinfo, halo_us=12.0, round_us=6.0e3 / 19, t_gen=1.0,
+                           conv={"rounds_to_1e-9": None}, strong=True)
+    assert line["scaling"] == "strong" and "strong scaling" in line["config"]["workload"]
+    assert bench.parse(["--strong"]).strong is True and bench.parse([]).strong is False
