@@ -145,7 +145,8 @@ int fu_run_collectall(fu_handle *h, int32_t rounds, int32_t err_every, double *e
  * whole region (synchronises). */
 int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms);
 /* Kernel "auto": one autotune pass now, at the current packing width, on real rounds
- * (1 warm + 8 timed per candidate, ~55 rounds; round 0 first if none ran). The rounds
+ * (1 warm + 8 timed per candidate, 2 more to confirm a slow warm round before the candidate
+ * is dropped; ~45-55 rounds; round 0 first if none ran; packing plans wait). The rounds
  * advance the state: call fu_reset before a run that must start from zero. The winner is
  * kept across fu_reset. Synchronises. Lets a caller tune outside a timed region. */
 int fu_tune(fu_handle *h);

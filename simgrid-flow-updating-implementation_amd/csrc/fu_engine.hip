@@ -2244,6 +2244,7 @@ struct fu_handle {
   int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
   bool tuned = false;
+  bool tuning = false;     // inside an autotune pass: packing plans wait until it ends
   float tune_ms[8] = {};  // per candidate (tune_cands order), ms per round of the last pass
   int tune_out[8] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
   int n_tunes = 0;        // autotune passes so far (re-run when the packing width changes)
@@ -3069,8 +3070,10 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   c.err = err_slot;
   // a packing plan due from a_{r-1}: the stage launch of kernels 8 and 9 carries it (one more
   // block); every other path runs it first as a launch of its own
-  c.plan = h->plan_pending && r > 0;
-  h->plan_pending = false;
+  // (held back during an autotune pass, so every candidate runs at the pass's width; any plan
+  // is lossless, so a late one changes nothing but the table's width)
+  c.plan = h->plan_pending && r > 0 && !h->tuning;
+  if (!h->tuning) h->plan_pending = false;
   const bool plan_done = c.plan;
   int rc;
   if (r == 0) rc = launch_round0(h, c);
@@ -3488,8 +3491,21 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   // kernel 9 stages the doubles whatever the packing: a candidate of the unpacked table only
   auto active9 = [&](int c) { return active(c) && !(kCands[c].kernel == 9 && width != 0); };
   int32_t need = 0;
-  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 1 + kTimed : 0;
+  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 3 + kTimed : 0;  // warm + a confirmation pair + timed
   if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
+  // the pass runs at the table's current width: the host's copy of it is exact once the stream
+  // is idle, and no plan runs until the pass ends (h->tuning)
+  HIP_TRY(hipStreamSynchronize(h->stream));
+  h->pw_pending = false;
+  h->seen_width = width = *h->h_pw;
+  need = 0;
+  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 3 + kTimed : 0;
+  if (*budget < need) return FU_OK;
+  h->tuning = true;
+  struct Untune {
+    fu_handle *h;
+    ~Untune() { h->tuning = false; }
+  } untune{h};
   float best = 1e30f;
   int bi = -1;
   for (int c = 0; c < kNCands; ++c) {
@@ -3506,7 +3522,10 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     }
     use_cand(h, kCands[c]);
     // the warm round is timed too: a candidate more than twice the best per-round time so far
-    // stops there (on R-MAT-24 the staged kernel would take 3x kernel 4 for 8 rounds)
+    // stops there (on R-MAT-24 the staged kernel would take 3x kernel 4 for 8 rounds). The
+    // events are recorded on an idle stream, so the warm round's time also holds the host's
+    // first launch of the candidate's kernels; a slow warm round is therefore confirmed by a
+    // second one, launched behind it, before the candidate is dropped
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     if (int rc = launch_round(h, nullptr)) return rc;
     HIP_TRY(hipEventRecord(h->ev1, h->stream));
@@ -3514,11 +3533,21 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
       HIP_TRY(hipEventSynchronize(h->ev1));
       float wms = 0.f;
       HIP_TRY(hipEventElapsedTime(&wms, h->ev0, h->ev1));
+      *budget -= 1;
       if (wms > 2.f * best / kTimed) {
-        h->tune_ms[c] = wms;
-        *budget -= 1;
-        continue;
+        HIP_TRY(hipEventRecord(h->ev0, h->stream));
+        if (int rc = launch_round(h, nullptr)) return rc;
+        if (int rc = launch_round(h, nullptr)) return rc;
+        HIP_TRY(hipEventRecord(h->ev1, h->stream));
+        HIP_TRY(hipEventSynchronize(h->ev1));
+        HIP_TRY(hipEventElapsedTime(&wms, h->ev0, h->ev1));
+        *budget -= 2;
+        if (wms > 2.f * 2.f * best / kTimed) {
+          h->tune_ms[c] = wms / 2.f;
+          continue;
+        }
       }
+      *budget += 1;  // counted below with the timed rounds
     }
     HIP_TRY(hipEventRecord(h->ev0, h->stream));
     for (int k = 0; k < kTimed; ++k)
@@ -3539,6 +3568,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     if (h->tune_ms[c] > 1.3f * h->tune_ms[bi]) h->tune_out[c]++;
   use_cand(h, kCands[bi]);
   h->tune_cache[width_class(width)] = bi;
+  h->tuned_width = width;
   h->tuned = true;
   h->n_tunes++;
   return FU_OK;
@@ -3569,7 +3599,6 @@ static int run_rounds(fu_handle *h, int32_t rounds, int32_t err_every, int nerr)
       int32_t budget = rounds - r;
       const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
       if (int rc = autotune_kernel(h, &budget, w)) return rc;
-      if (h->tuned) h->tuned_width = w;
       r = rounds - budget;
       if (r >= rounds) break;
     }
@@ -3632,7 +3661,6 @@ int fu_tune(fu_handle *h) {
   const int w = h->pw_pending ? h->tuned_width : *h->h_pw;
   int32_t budget = INT32_MAX;
   if (int rc = autotune_kernel(h, &budget, w)) return rc;
-  h->tuned_width = w;
   return FU_OK;
   FU_TRY_END
 }
