@@ -191,17 +191,18 @@ def round_kernels(kinfo):
     return k
 
 
-def pmc_traffic(n, E, kernel_selected, steps):
+def pmc_traffic(n, E, kernel_selected, steps, per_gpu=False):
     """HBM bytes per round from profiles/pmc_traffic.json (tools/pmc.sh + tools/make_pmc_traffic.py),
-    only when it was measured on this graph, kernel and timed window."""
+    only when it was measured on this graph, kernel and timed window. per_gpu: the rgg-dist
+    record of the per-GPU slab (n = nodes per GPU; E not compared: it is the slab's)."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     with open(path) as f:
         pmc = json.load(f)
     for rec in pmc if isinstance(pmc, list) else [pmc]:
-        if rec.get("n") == n and rec.get("E") == E and rec.get("kernel_selected") == kernel_selected \
-                and rec.get("rounds_timed") == steps:
+        if rec.get("n") == n and (per_gpu or rec.get("E") == E) \
+                and rec.get("kernel_selected") == kernel_selected and rec.get("rounds_timed") == steps:
             return rec.get("bytes_per_launch")
     return None
 
@@ -248,6 +249,8 @@ def run_single(args, wl):
               for k in range(len(b) - 1)]
     pack_after = eng.pack_widths()[2]
     value = g.E * args.steps / wall
+    # rounds 1..K-1 alone (round 0 writes no flows, §4.8): E (K-1) / their device time
+    value_r1 = g.E * (args.steps - 1) / (sum(dev_ms[1:]) * 1e-3) if args.steps > 1 else None
     alg_bytes = 24 * g.E + 28 * g.n
     kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
     roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, args.steps), round_kernels(kinfo))
@@ -259,6 +262,7 @@ def run_single(args, wl):
     cpu = cpu_baseline(g, v, args.cpu_seconds) if args.cpu_seconds > 0 else None
     out = {
         "metric": METRIC, "value": value, "unit": "edge-updates/s", "n_gpus": 1,
+        "value_rounds_1_on": value_r1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": f"synthetic (seeded {wl} graph, U[0,100) values)",
@@ -277,12 +281,16 @@ def run_single(args, wl):
     out.update(conv)
     eng.close()
     if args.workload == "auto" and not args.no_unit:
-        out["weak_scaling_unit"] = weak_unit(args)
+        try:  # a failure of the companion measurement must not lose the headline line
+            out["weak_scaling_unit"] = weak_unit(args)
+        except Exception as ex:  # noqa: BLE001
+            print(f"[bench] weak_scaling_unit failed: {ex!r}", file=sys.stderr, flush=True)
+            out["weak_scaling_unit"] = {"error": repr(ex)}
     print(json.dumps(out), flush=True)
 
 
 def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_total, per, kinfo,
-              halo_us, round_us, t_gen, conv, strong=False):
+              halo_us, round_us, t_gen, conv, strong=False, rccl_parity=None, traffic=None):
     """The N > 1 (rgg-dist) JSON line. Per GPU and round the algorithmic bytes are the §8(d)
     figure of the rank's rows (24 E + 28 N) plus the halo: 8 B per ghost estimate received
     (the RCCL payload written into the ghost slots; halo = ghost slots over all ranks)."""
@@ -304,16 +312,24 @@ def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_tota
                    "halo_estimates_per_round": halo, "halo_bytes_per_round": 8 * halo,
                    "parallelism": f"graph partition x{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "per_gpu": True,
+                     "frac": achieved / HBM_PEAK_GBS, "per_gpu": True,
+                     # HBM bytes per GPU and round from the PMC passes of this window on the
+                     # partitioned path (profiles/pmc_traffic.json, measured at one rank: the
+                     # same kernels on the same per-GPU slab; the halo adds 8 B per ghost)
+                     "traffic": traffic,
                      "alg_bytes_per_launch": alg, "avg_launch_us": r1 * 1e3,
                      "kernel": "k_round_recon (heavy, boundary tiles) -> k_pack + RCCL group on the "
                                "comm stream beside the interior tiles",
-                     "launch_window": f"rounds 1-{steps - 1}, max over ranks, the last halo included"},
+                     "launch_window": f"rounds 1-{steps - 1}, max over ranks, the last halo included "
+                                      "(events inside the timed region)"},
         # halo: device time on the comm stream from the start of the pack (boundary tiles
         # done) to the ghost slots written, max over ranks; it overlaps the interior tiles
         "halo": {"us_per_round": halo_us, "share_of_round": (halo_us / round_us) if round_us else None,
                  "overlapped_with": "interior tiles of the same round",
-                 "sample": "20 rounds after the timed region, one halo read per round"},
+                 "sample": "20 rounds after the timed region (outside it), one halo read per round"},
+        # the RCCL halo's correctness, checked in this run before the timed region
+        "rccl_parity": rccl_parity["status"] if rccl_parity else ("n/a (one rank: no halo)" if world == 1 else None),
+        "rccl_parity_check": rccl_parity,
         "cpu_baseline": None,
         "cpu_baseline_note": "reported on the N = 1 line only (rank 0 at N = 1)",
         "graph_gen_s": t_gen,
@@ -362,18 +378,23 @@ def measure_dist(args, world, rank, local, dist):
     else:  # weak scaling: 2^23 nodes per GPU
         per = args.n or (1 << 23)
         n_total = per * world
-    t = time.perf_counter()
-    part = RggPart(n_total, avg_deg=8.0, seed=1, nparts=world, part=rank)
-    v = part.values(seed=0)
-    t_gen = time.perf_counter() - t
-    if world > 1:
+    def shared_uid():
+        if world == 1:
+            return unique_id()
         buf = torch.zeros(128, dtype=torch.uint8)
         if rank == 0:
             buf = torch.frombuffer(bytearray(unique_id()), dtype=torch.uint8)
         dist.broadcast(buf, 0)
-        uid = bytes(buf.tolist())
-    else:
-        uid = unique_id()
+        return bytes(buf.tolist())
+
+    # correctness of the RCCL halo first (untimed, before the measured graph exists): a
+    # small RGG over the same ranks against the single-GPU engine on rank 0, bitwise
+    parity = rccl_parity(world, rank, local, dist, shared_uid) if world > 1 else None
+    t = time.perf_counter()
+    part = RggPart(n_total, avg_deg=8.0, seed=1, nparts=world, part=rank)
+    v = part.values(seed=0)
+    t_gen = time.perf_counter() - t
+    uid = shared_uid()
     eng = DistCollectAll(part.to_plan(), v, uid, device=local, kernel=args.kernel)
     if args.kernel == "auto":
         eng.tune()  # collective: the same rounds on every rank
@@ -408,23 +429,103 @@ def measure_dist(args, world, rank, local, dist):
         dev1 = sum(dev_ms[1:])
         e_tot, n_tot, halo = part.e_local, part.n_local, part.n_ghost_a
     kinfo = eng.info()
-    # rounds to 1e-9 against the per-component means (math.fsum): they need the global graph,
-    # which only the one-rank unit holds (no rank builds the global graph at N > 1)
+    # rounds to 1e-9 against the per-component means (math.fsum over each component of the
+    # global graph, joined across the ranks without any rank holding it; untimed), the
+    # error all-reduced (max) over the ranks by RCCL every round
     conv = {"rounds_to_1e-9": None, "err_after_conv_rounds": None, "conv_rounds": None,
             "components": None}
-    if world == 1 and not args.no_conv:
-        conv = convergence(eng, part.rowptr, part.col, v, args.conv_rounds)
-    elif world > 1:
-        conv["conv_note"] = ("per-component targets need the global graph; see the one-rank line "
-                             "of the same per-GPU unit")
+    if not args.no_conv:
+        conv = convergence_dist(eng, part, v, args.conv_rounds, rank, world, dist)
     line = None
     if rank == 0:
+        traffic = pmc_traffic(per, None, "rgg-dist", args.steps, per_gpu=True) if not args.strong else None
         line = dist_line(world=world, steps=args.steps, warmup=args.warmup, wall=wall, dev1_ms=dev1,
                          e_tot=e_tot, n_tot=n_tot, halo=halo, n_total=n_total, per=per, kinfo=kinfo,
                          halo_us=halo_us, round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
-                         conv=conv, strong=args.strong)
+                         conv=conv, strong=args.strong, rccl_parity=parity, traffic=traffic)
     eng.close()
     return line
+
+
+def convergence_dist(eng, part, v, rounds, rank, world, dist):
+    """convergence() for one rank of a partitioned graph: the per-component means from
+    fu.dist.component_means_dist (bitwise those of the global graph), each rank's slice as
+    its targets, one untimed run with the error check every round (RCCL max over ranks)."""
+    from fu.dist import component_means_dist
+
+    tgt, ncomp = component_means_dist(part.n_local, part.rowptr, part.col, part.send_a_off,
+                                      part.send_a_idx, part.recv_a_off, v, rank, world, dist)
+    eng.reset()
+    eng.set_targets(tgt)
+    tr = eng.run(rounds, err_every=1)
+    below = np.nonzero(tr < 1e-9)[0]
+    return {"rounds_to_1e-9": int(below[0]) + 1 if len(below) else None,
+            "err_after_conv_rounds": float(tr[-1]), "conv_rounds": rounds, "components": int(ncomp)}
+
+
+RCCL_PARITY_N = 1 << 18     # nodes of the parity graph (all ranks together)
+RCCL_PARITY_ROUNDS = 30
+
+
+def parity_verdict(a_parts, f_parts, a_ref, f_ref):
+    """Rank 0's comparison of the gathered partitioned run with the single-GPU engine:
+    (True, "bitwise") or (False, what differs)."""
+    a = np.concatenate(a_parts)
+    f = np.concatenate(f_parts)
+    if a.shape != a_ref.shape or f.shape != f_ref.shape:
+        return False, f"shape: estimates {a.shape} vs {a_ref.shape}, flows {f.shape} vs {f_ref.shape}"
+    bad_a = int(np.sum(a.view(np.uint64) != a_ref.view(np.uint64)))
+    bad_f = int(np.sum(f.view(np.uint64) != f_ref.view(np.uint64)))
+    if bad_a or bad_f:
+        return False, f"{bad_a} estimates and {bad_f} flows differ from the single-GPU engine"
+    return True, "bitwise"
+
+
+def rccl_parity_arrays(world, rank, local, dist, shared_uid, n=RCCL_PARITY_N, rounds=RCCL_PARITY_ROUNDS):
+    """Every rank runs its slab of RGG(n) through fu_dist_create + RCCL for `rounds` rounds
+    (halo exchange every round); rank 0 gathers the estimates and flows and runs the same
+    rounds on the global graph with the single-GPU engine (pinned to the C oracle by the
+    -m gpu suite). Returns (a_parts, f_parts, a_ref, f_ref) on rank 0, None elsewhere."""
+    import fu
+    from fu.dist import DistCollectAll, RggPart
+
+    part = RggPart(n, avg_deg=8.0, seed=11, nparts=world, part=rank)
+    eng = DistCollectAll(part.to_plan(), part.values(seed=12), shared_uid(), device=local)
+    eng.run(rounds)
+    mine = (eng.estimates(), eng.flows())
+    eng.close()
+    got = [None] * world if rank == 0 else None
+    if dist is not None:
+        dist.gather_object(mine, got, dst=0)
+    else:
+        got = [mine]
+    if rank != 0:
+        return None
+    g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=11)
+    ref = fu.CollectAll(g, fu.uniform_values(g.n, seed=12), device=local)
+    ref.run(rounds)
+    out = ([x[0] for x in got], [x[1] for x in got], ref.estimates(), ref.flows())
+    ref.close()
+    return out
+
+
+def rccl_parity(world, rank, local, dist, shared_uid):
+    """The N > 1 line's correctness bit for the RCCL halo (CA:74 get_async, CA:124 put_async
+    become ncclRecv/ncclSend into ghost slots): "bitwise", or every rank exits with status 5."""
+    arrs = rccl_parity_arrays(world, rank, local, dist, shared_uid)
+    verdict = [None]
+    if rank == 0:
+        verdict = [parity_verdict(*arrs)]
+    if dist is not None:
+        dist.broadcast_object_list(verdict, src=0)
+    ok, detail = verdict[0]
+    if not ok:
+        print(f"[bench] RCCL parity FAILED at {world} ranks (RGG n={RCCL_PARITY_N}, "
+              f"{RCCL_PARITY_ROUNDS} rounds): {detail}", file=sys.stderr, flush=True)
+        sys.exit(5)
+    return {"status": detail, "graph": f"rgg:n={RCCL_PARITY_N},deg=8,seed=11 over {world} ranks",
+            "rounds": RCCL_PARITY_ROUNDS,
+            "against": "single-GPU engine on the global graph (rank 0), estimates and flows"}
 
 
 def convergence(eng, rowptr, col, v, rounds):

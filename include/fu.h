@@ -123,6 +123,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "multi_heavy"   kernel 9: rows of more than 256 edges as multi-row chain blocks (default 1);
  *                 "multi_mid" 0 keeps the rows of 257-1024 edges in the register launch.
  * "tr_pipe"       kernel 9: software-pipelined transpose (default 0; needs tr_bpx > 0).
+ * "hub_multi"     kernel 9: mega hubs of <= value edges run their chains as multi-row chain
+ *                 blocks (16 hubs per chain wave) instead of one block each (default 0: none).
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).

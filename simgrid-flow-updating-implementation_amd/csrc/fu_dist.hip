@@ -99,19 +99,27 @@ int fu_dist_unique_id(uint8_t *id_out) {
     if (_e != hipSuccess) return fu::fail(FU_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-// phase 0: before a round (or a host sync / reset): the main stream waits for the last halo.
-// phase 2: mid-round, once the boundary tiles (and heavy rows) of round r are queued: pack
-//   a_r[send_a_idx] and exchange with every neighbouring part on comm_stream, concurrently with
-//   round r's interior tiles (they never read ghost slots; the receives write only ghost
-//   slots [n_local, na) of the buffer, the interior tiles only own slots). Local transport:
-//   pack only, on the main stream (fu_dist_exchange_local moves the bytes).
+// phase 0: before a round (or a host sync): the main stream waits for the last halo.
+// phase 1: fu_reset: as phase 0, then the comm stream drains and the in-process transport's
+//   round bookkeeping restarts (round 0 may be packed and exchanged again).
+// phase 2: mid-round, once the boundary tiles (and heavy rows) of round r are queued: behind
+//   ev_bnd, pack a_r[send_a_idx] on comm_stream, concurrently with round r's interior tiles
+//   (they never read ghost slots; the receives write only ghost slots [n_local, na) of the
+//   buffer, the interior tiles only own slots). RCCL: the ncclSend/ncclRecv group follows on
+//   comm_stream and records ev_halo. In-process transport: the pack records ev_packed, and
+//   fu_dist_exchange_local queues the copies into the peers' ghost slots and their ev_halo.
 // phase 100 + k: all-reduce max of k error slots (on comm_stream, joined back).
 int fu__dist_round_hook(fu_handle *h, int phase) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   hipStream_t s = fu__handle_stream(h);
-  if (phase == 0) {
+  if (phase == 0 || phase == 1) {
     if (d->halo_pending) HIPD_TRY(hipStreamWaitEvent(s, d->ev_halo, 0));
     d->halo_pending = false;
+    if (phase == 1) {
+      HIPD_TRY(hipStreamSynchronize(d->comm_stream));
+      d->packed_round = d->exchanged_round = -1;
+      d->timed_once = false;
+    }
     return FU_OK;
   }
   if (phase >= 100) {
@@ -327,6 +335,11 @@ int fu_dist_halo_time(fu_handle *h, float *ms) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   if (!d) return fail(FU_ERR_ARG, "fu_dist_halo_time: not a multi-GPU handle");
   if (!d->timed_once) return fail(FU_ERR_STATE, "fu_dist_halo_time: no halo exchanged yet");
+  // in-process transport: ev_h0 is re-recorded by every round's pack, ev_h1 only by the
+  // exchange, so the pair is one halo only when the last packed round was exchanged
+  if (!d->comm && d->packed_round != d->exchanged_round)
+    return fail(FU_ERR_STATE, "fu_dist_halo_time: round " + std::to_string(d->packed_round) +
+                                  "'s halo is packed but not exchanged yet");
   HIPD_TRY(hipSetDevice(fu__handle_device(h)));
   HIPD_TRY(hipEventSynchronize(d->ev_h1));
   HIPD_TRY(hipEventElapsedTime(ms, d->ev_h0, d->ev_h1));

@@ -1524,7 +1524,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // ------------------------------------------------------------------------------------
 constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
-template <bool CHECK>
+template <bool CHECK, bool FLOWS = true>
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
@@ -1586,6 +1586,25 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       const int len = min(kMCH, max(0, s_d[cr] - c * kMCH));
       const double *src = sh[buf][lane];
       int q = 0;
+      if (len == kMCH) {  // a full chunk: the next 8 LDS reads in flight beside the 8 dependent adds
+        double x[8], y[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = src[u];
+#pragma unroll
+        for (int b = 0; b < kMCH; b += 16) {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) y[u] = src[b + 8 + u];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc = acc + x[u];
+          if (b + 16 < kMCH) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) x[u] = src[b + 16 + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc = acc + y[u];
+        }
+        q = len;
+      }
       for (; q + 8 <= len; q += 8) {
         double x[8];
 #pragma unroll
@@ -1629,6 +1648,10 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
+  }
+  if (!FLOWS) {  // the mega hubs: k_hub_flows writes their flows with the whole grid
+    if (CHECK) block_max_to(eb, err);
+    return;
   }
   __syncthreads();
   // flows (CA:117-118): wave w, its rows, 8 elements per lane in flight
@@ -2276,6 +2299,10 @@ struct fu_handle {
   int64_t hub_total = 0;
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
   int *hub_blk = nullptr;    // per 256-edge block of the hub edges: the hub of its first edge
+  int *hub_sorted = nullptr;  // the mega hubs' node ids, longest first (option hub_multi)
+  int4 *hub_tiles_sorted = nullptr;  // their -3 tiles in the same order
+  std::vector<int64_t> h_hub_len;    // their lengths (host)
+  int hub_multi = 0;          // kernel 9: mega hubs of <= hub_multi edges as k_heavy_multi blocks (0: none)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2431,9 +2458,12 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *c
 
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
-  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk})
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk, (void *)h->hub_sorted,
+                  (void *)h->hub_tiles_sorted})
     if (p) hipFree(p);
   h->hub_blk = nullptr;
+  h->hub_sorted = nullptr;
+  h->hub_tiles_sorted = nullptr;
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
@@ -2464,6 +2494,19 @@ int build_hubs(fu_handle *h) {
   }
   if (int rc = dmalloc(&h->hub_blk, blk.size())) return rc;
   HIP_TRY(hipMemcpy(h->hub_blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
+  std::vector<int32_t> srt;
+  for (const int4 &hr : rows) srt.push_back(hr.x);
+  std::stable_sort(srt.begin(), srt.end(), [&](int32_t x, int32_t y) {
+    return h->h_rowptr[x + 1] - h->h_rowptr[x] > h->h_rowptr[y + 1] - h->h_rowptr[y];
+  });
+  std::vector<int4> stl;
+  for (int32_t x : srt) stl.push_back(make_int4(x, -3, (int)h->h_rowptr[x], (int)h->h_rowptr[x + 1]));
+  if (int rc = dmalloc(&h->hub_sorted, srt.size())) return rc;
+  HIP_TRY(hipMemcpy(h->hub_sorted, srt.data(), sizeof(int32_t) * srt.size(), hipMemcpyHostToDevice));
+  if (int rc = dmalloc(&h->hub_tiles_sorted, stl.size())) return rc;
+  HIP_TRY(hipMemcpy(h->hub_tiles_sorted, stl.data(), sizeof(int4) * stl.size(), hipMemcpyHostToDevice));
+  h->h_hub_len.clear();
+  for (int32_t x : srt) h->h_hub_len.push_back(h->h_rowptr[x + 1] - h->h_rowptr[x]);
   return FU_OK;
 }
 
@@ -2889,9 +2932,23 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const bool chk = c.err && !D;
   if (hubs) {
     auto chains = [&](auto C) {
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
-                         0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
-                         h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm);
+      // hub_multi: the hubs of <= hub_multi edges as k_heavy_multi blocks (kMR hubs of similar
+      // length per block, one chain wave: few blocks hold LDS beside the transposes); the
+      // longer ones keep a block each (deeper prefetch on their long chains)
+      int nbig = nmega;
+      if (h->hub_multi) {
+        nbig = 0;
+        while (nbig < nmega && h->h_hub_len[nbig] > h->hub_multi) ++nbig;
+        if (nmega > nbig)
+          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, false>), dim3((nmega - nbig + kMR - 1) / kMR),
+                             dim3(kBlock), 0, h->stream2, h->hub_sorted + nbig, nmega - nbig, h->rowptr, h->v, c.F,
+                             c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm);
+      }
+      if (nbig)
+        hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
+                           0, h->stream2, h->hub_multi ? h->hub_tiles_sorted : tl, h->rowptr, h->col, h->v, c.F, c.ap,
+                           c.ap2, c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1,
+                           Gb, c.fm);
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
@@ -3397,6 +3454,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->tr_bpx = (int)value;
     return FU_OK;
   }
+  if (!std::strcmp(key, "hub_multi")) {  // kernel 9: mega hubs of <= value edges many per chain wave (0: one per block)
+    if (value < 0 || value > INT32_MAX) return fail(FU_ERR_ARG, "fu_set_option: hub_multi must be in [0, 2^31)");
+    h->hub_multi = (int)value;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
     h->multi_heavy = value != 0;
     return FU_OK;
@@ -3434,8 +3496,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
 int fu_reset(fu_handle *h) {
   if (!h) return fail(FU_ERR_ARG, "fu_reset: NULL handle");
   if (int rc = set_device(h)) return rc;
-  if (h->dist) {
-    if (int rc = fu__dist_round_hook(h, 0)) return rc;
+  if (h->dist) {  // phase 1: wait for the last halo, drain the comm stream, forget its rounds
+    if (int rc = fu__dist_round_hook(h, 1)) return rc;
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
@@ -3810,7 +3872,7 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
-                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,
+                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->hub_sorted, h->hub_tiles_sorted, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG, h->col16, h->cbase,
                               h->tnar_geo[0], h->tnar_geo[1], h->tnar_geo[2], h->tnar_geo[3]};
   free_transpose(h);

@@ -189,6 +189,110 @@ class RggPart:
                     self.recv_a_off)
 
 
+def _exact_expansion(vals) -> list:
+    """Non-overlapping doubles whose exact sum is the exact sum of `vals`: math.fsum's
+    correctly rounded sum, then the correctly rounded residual of the rest, until nothing is
+    left (each step takes 53 more bits; 3-4 steps for millions of values)."""
+    import math
+
+    vals = list(vals)
+    out = []
+    while True:
+        s = math.fsum(vals + [-x for x in out])
+        if s == 0.0 or len(out) > 40:
+            return out
+        out.append(s)
+
+
+def component_means_dist(n_local, rowptr, col, send_a_off, send_a_idx, recv_a_off, values,
+                         rank, nranks, dist=None):
+    """fu.component_means for a partitioned graph, without any rank holding the global graph:
+    the per-node exact mean of its connected component (math.fsum over the component, divided
+    by its size; the convergence target of SURVEY.md §8(d)). Bitwise equal to
+    fu.component_means on the global graph.
+
+    Every rank labels the components of its own rows (edges to ghost slots left out) and
+    the exact sum of each as a double expansion; rank 0 joins the labels across the cut edges
+    (a ghost slot of this rank from peer p is p's node send_a_idx[send_a_off[me] + k], the
+    slot order of the halo plan) with a union-find and fsums the expansions of each global
+    component; the means go back to the ranks. `dist` is torch.distributed (any backend
+    with object collectives) or None at one rank."""
+    import math
+
+    from scipy.sparse import csr_matrix
+    from scipy.sparse.csgraph import connected_components
+
+    rowptr = np.asarray(rowptr, dtype=np.int64)
+    col = np.asarray(col, dtype=np.int64)
+    values = np.asarray(values, dtype=np.float64)
+    send_a_off = np.asarray(send_a_off, dtype=np.int64)
+    recv_a_off = np.asarray(recv_a_off, dtype=np.int64)
+    src = np.repeat(np.arange(n_local, dtype=np.int64), np.diff(rowptr))
+    own = col < n_local
+    m = csr_matrix((np.ones(int(own.sum()), dtype=np.int8), (src[own], col[own])), shape=(n_local, n_local))
+    nc, lab = connected_components(m, directed=False)
+    # exact sums per local component (sizes 1 and 2 without a Python loop, as fu.component_means)
+    order = np.argsort(lab, kind="stable")
+    bounds = np.searchsorted(lab[order], np.arange(nc + 1))
+    vs = values[order]
+    size = np.diff(bounds)
+    exp = [None] * nc
+    for k in np.nonzero(size == 1)[0]:
+        exp[k] = [float(vs[bounds[k]])]
+    for k in np.nonzero(size >= 2)[0]:
+        exp[k] = _exact_expansion(vs[bounds[k]:bounds[k + 1]].tolist())
+    # cut edges: (my label, peer, index into the peer's send list)
+    ghost = ~own
+    slot = col[ghost] - n_local
+    peer = np.searchsorted(recv_a_off, slot, side="right") - 1
+    cut = np.unique(np.stack([lab[src[ghost]], peer, slot - recv_a_off[peer]]), axis=1) \
+        if ghost.any() else np.zeros((3, 0), dtype=np.int64)
+    send_lab = lab[np.asarray(send_a_idx, dtype=np.int64)] if len(send_a_idx) else np.zeros(0, dtype=np.int64)
+    mine = {"nc": nc, "size": size, "exp": exp, "cut": cut, "send_lab": send_lab, "send_a_off": send_a_off}
+    if dist is not None and nranks > 1:
+        allr = [None] * nranks if rank == 0 else None
+        dist.gather_object(mine, allr, dst=0)
+    else:
+        allr = [mine]
+    result = [None]
+    if rank == 0:
+        base = np.cumsum([0] + [r["nc"] for r in allr])
+        parent = np.arange(base[-1])
+
+        def find(x):
+            while parent[x] != x:
+                parent[x] = parent[parent[x]]
+                x = parent[x]
+            return x
+
+        for q, r in enumerate(allr):
+            for mylab, p, k in r["cut"].T:
+                pr = allr[int(p)]
+                other = base[int(p)] + pr["send_lab"][pr["send_a_off"][q] + int(k)]
+                x, y = find(base[q] + int(mylab)), find(int(other))
+                if x != y:
+                    parent[max(x, y)] = min(x, y)
+        roots = np.array([find(x) for x in range(base[-1])], dtype=np.int64)
+        sizes = np.concatenate([r["size"] for r in allr]).astype(np.int64)
+        exps = [e for r in allr for e in r["exp"]]
+        groups = {}
+        for x, rt in enumerate(roots):
+            groups.setdefault(int(rt), []).append(x)
+        mean = np.empty(base[-1])
+        for rt, members in groups.items():
+            tot = int(sizes[members].sum())
+            if len(members) == 1 and len(exps[members[0]]) == 1:
+                mean[members] = exps[members[0]][0] / tot if tot > 1 else exps[members[0]][0]
+            else:
+                mean[members] = math.fsum([x for mbr in members for x in exps[mbr]]) / tot
+        ncomp = len(groups)
+        result = [[(mean[base[q]:base[q + 1]], ncomp) for q in range(len(allr))]]
+    if dist is not None and nranks > 1:
+        dist.broadcast_object_list(result, src=0)
+    lmean, ncomp = result[0][rank]
+    return lmean[lab], ncomp
+
+
 def unique_id() -> bytes:
     buf = (ctypes.c_uint8 * 128)()
     L.call("fu_dist_unique_id", buf)

@@ -92,3 +92,63 @@ def test_dist_line_strong_scaling():
                            conv={"rounds_to_1e-9": None}, strong=True)
     assert line["scaling"] == "strong" and "strong scaling" in line["config"]["workload"]
     assert bench.parse(["--strong"]).strong is True and bench.parse([]).strong is False
+
+
+def test_dist_line_rccl_parity_and_traffic_fields():
+    """N > 1 lines carry the RCCL halo's correctness bit and the per-GPU PMC traffic."""
+    kinfo = {"kernel": "recon", "tile": (1024, 128)}
+    chk = {"status": "bitwise", "graph": "rgg", "rounds": 30, "against": "x"}
+    line = bench.dist_line(world=2, steps=20, warmup=5, wall=0.01, dev1_ms=6.0, e_tot=2 * 67_000_000,
+                           n_tot=2 * 8_388_608, halo=2 * 40_000, n_total=2 * 8_388_608, per=8_388_608,
+                           kinfo=kinfo, halo_us=12.0, round_us=6.0e3 / 19, t_gen=1.0,
+                           conv={"rounds_to_1e-9": None, "err_after_conv_rounds": 0.6}, rccl_parity=chk,
+                           traffic=1.7e9)
+    assert line["rccl_parity"] == "bitwise" and line["rccl_parity_check"] == chk
+    assert line["roofline"]["traffic"] == 1.7e9
+    assert line["err_after_conv_rounds"] == 0.6
+    one = bench.dist_line(world=1, steps=20, warmup=5, wall=0.01, dev1_ms=6.0, e_tot=67_000_000,
+                          n_tot=8_388_608, halo=0, n_total=8_388_608, per=8_388_608, kinfo=kinfo,
+                          halo_us=1.0, round_us=300.0, t_gen=1.0, conv={})
+    assert one["rccl_parity"].startswith("n/a")
+
+
+def test_parity_verdict():
+    a = np.arange(10, dtype=np.float64)
+    f = np.linspace(-1, 1, 40)
+    assert bench.parity_verdict([a[:4], a[4:]], [f[:15], f[15:]], a, f) == (True, "bitwise")
+    a2 = a.copy()
+    a2[3] = np.nextafter(a2[3], 10.0)  # one ulp
+    ok, why = bench.parity_verdict([a2[:4], a2[4:]], [f], a, f)
+    assert not ok and "1 estimates and 0 flows" in why
+    z = np.array([0.0])
+    assert not bench.parity_verdict([np.array([-0.0])], [f], z, f)[0]  # signed zero counts
+    assert not bench.parity_verdict([a[:4]], [f], a, f)[0]
+
+
+def test_rccl_parity_mismatch_exits_nonzero(monkeypatch, capsys):
+    """A wrong halo must not produce a fast, plausible line: rank 0's mismatch ends the run
+    with status 5 (every rank, through the broadcast verdict)."""
+    a = np.arange(6, dtype=np.float64)
+    f = np.arange(12, dtype=np.float64)
+    bad = a.copy()
+    bad[5] += 1.0
+    monkeypatch.setattr(bench, "rccl_parity_arrays", lambda *x, **k: ([bad[:3], bad[3:]], [f], a, f))
+    with pytest.raises(SystemExit) as ex:
+        bench.rccl_parity(2, 0, 0, None, lambda: b"")
+    assert ex.value.code == 5
+    assert "RCCL parity FAILED" in capsys.readouterr().err
+    monkeypatch.setattr(bench, "rccl_parity_arrays", lambda *x, **k: ([a[:3], a[3:]], [f], a, f))
+    assert bench.rccl_parity(2, 0, 0, None, lambda: b"")["status"] == "bitwise"
+
+
+def test_pmc_traffic_per_gpu_record(tmp_path, monkeypatch):
+    import json
+
+    rec = [{"n": 8388608, "E": 67000000, "kernel_selected": "rgg-dist", "rounds_timed": 20,
+            "bytes_per_launch": 1.8e9}]
+    (tmp_path / "profiles").mkdir()
+    (tmp_path / "profiles" / "pmc_traffic.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    assert bench.pmc_traffic(8388608, None, "rgg-dist", 20, per_gpu=True) == 1.8e9
+    assert bench.pmc_traffic(8388608, None, "rgg-dist", 21, per_gpu=True) is None
+    assert bench.pmc_traffic(8388608, 5, "rgg-dist", 20) is None

@@ -185,3 +185,59 @@ def test_rgg_slab_generator_matches_global_and_partition(nparts):
         assert np.array_equal(p.send_a_idx, ref.send_a_idx)
         assert np.array_equal(p.recv_a_off, ref.recv_a_off)
         assert np.array_equal(p.values(seed=3), fu.uniform_values(n, seed=3)[p.lo:p.hi])
+
+
+def _cm_worker(rank, world, port, kind, n, out_q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import fu
+    from fu.dist import RggPart, component_means_dist
+
+    if kind == "rgg":
+        p = RggPart(n, avg_deg=3.0, seed=5, nparts=world, part=rank)
+        v = p.values(seed=6)
+        args = (p.n_local, p.rowptr, p.col, p.send_a_off, p.send_a_idx, p.recv_a_off)
+        lo = p.lo
+    else:
+        g = fu.Graph.erdos_renyi(n, n, seed=5)  # average degree 2: many small components
+        v = fu.uniform_values(g.n, seed=6)
+        p = partition(g.rowptr, g.col, g.rev, world, rank)
+        args = (p.n_local, p.rowptr, p.col, p.send_a_off, p.send_a_idx, p.recv_a_off)
+        v, lo = v[p.lo:p.hi], p.lo
+    mean, nc = component_means_dist(*args, v, rank, world, dist)
+    out_q.put((rank, lo, mean, nc))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("kind", ["rgg", "er"])
+def test_component_means_dist_bitwise(world, kind):
+    """The N > 1 line's convergence targets: per-component exact means of a partitioned graph
+    (each rank's own components + expansions, joined on rank 0 across the cut edges) equal
+    fu.component_means on the global graph bitwise, with components that span several ranks
+    (sparse RGG at average degree 3, ER at average degree 2)."""
+    import fu
+
+    n = 6000
+    g = (fu.Graph.random_geometric(n, avg_deg=3.0, seed=5) if kind == "rgg"
+         else fu.Graph.erdos_renyi(n, n, seed=5))
+    v = fu.uniform_values(g.n, seed=6)
+    ref, comp = fu.component_means(g.rowptr, g.col, v)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cm_worker, args=(r, world, port, kind, n, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = np.empty(g.n)
+    for rank, lo, mean, nc in res:
+        got[lo:lo + len(mean)] = mean
+        assert nc == int(comp.max()) + 1
+    assert np.array_equal(got, ref)
+    assert len(np.unique(comp)) > 50  # many components, several across the cuts

@@ -4,6 +4,7 @@ fixtures. Bit-exact everywhere: the kernels keep the reference's left-to-right f
 properties (convergence to the component means, flow antisymmetry) and a bitwise
 comparison against the C oracle on a prefix of the rounds."""
 import io
+import os
 
 import numpy as np
 import pytest
@@ -340,10 +341,32 @@ def test_dist_exchange_local_checks_round_counts():
     engs[0].run(1)
     with pytest.raises(fu.FuError, match="different numbers of rounds"):
         fu._lib.call("fu_dist_exchange_local", arr, 2)
+    with pytest.raises(fu.FuError, match="no halo exchanged yet"):
+        engs[0].halo_ms()  # packed, never exchanged
     engs[1].run(1)
     fu._lib.call("fu_dist_exchange_local", arr, 2)
     with pytest.raises(fu.FuError, match="no packed halo pending"):
         fu._lib.call("fu_dist_exchange_local", arr, 2)
+    assert engs[0].halo_ms() > 0 and engs[1].halo_ms() > 0
+    # a reset restarts the round bookkeeping: exactly one round, reset, one round again
+    for e in engs:
+        e.reset()
+    with pytest.raises(fu.FuError, match="no halo exchanged yet"):
+        engs[0].halo_ms()
+    from fu.dist import run_local
+
+    run_local(engs, 1)
+    engs[0].run(1)  # round 1 launched on rank 0 only: its halo is packed, not exchanged
+    with pytest.raises(fu.FuError, match="packed but not exchanged"):
+        engs[0].halo_ms()
+    engs[1].run(1)
+    fu._lib.call("fu_dist_exchange_local", arr, 2)
+    assert engs[0].halo_ms() > 0
+    run_local(engs, 3)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 5, nthreads=16)
+    for p, e in zip(plans, engs):
+        assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), p.rank
+        assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), p.rank
     for e in engs:
         e.close()
 
@@ -586,7 +609,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -603,6 +626,10 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("multi_mid", 0)
     elif multi == "pipe":
         eng.set_option("tr_pipe", 1)
+    elif multi == "hubm":  # mega hubs up to 2 * mega as multi-row chain blocks, longer ones alone
+        eng.set_option("hub_multi", 2 * mega)
+    elif multi == "hubm_all":
+        eng.set_option("hub_multi", 1 << 30)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -850,3 +877,25 @@ def test_c16_narrow_and_wide_tiles_bitwise(tile):
         assert np.array_equal(eng.estimates(), a_ref), c16
         assert np.array_equal(eng.flows(), f_ref), c16
         eng.close()
+
+
+def test_bench_rccl_two_ranks_parity_and_convergence():
+    """bench.py --gpus 2 (rgg-dist, small slabs): the RCCL halo's parity check against the
+    single-GPU engine reports "bitwise", and the line carries the error reached against the
+    per-component means. Two RCCL ranks need two GPUs (RCCL refuses two ranks on one)."""
+    import json
+    import subprocess
+    import sys
+
+    if fu.device_count() < 2:
+        pytest.skip("two RCCL ranks need two GPUs (this box has one)")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--workload", "rgg-dist",
+                        "--n", "262144", "--steps", "5", "--warmup", "2", "--conv-rounds", "60"],
+                       capture_output=True, text=True, timeout=110, env=env, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["rccl_parity"] == "bitwise"
+    assert line["err_after_conv_rounds"] is not None and line["components"] >= 1

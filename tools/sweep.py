@@ -32,6 +32,9 @@ VARIANTS = {
     "pre_multi0": ("pregather", {"layout": "degree", "pack": 0, "multi_heavy": 0}),
     "pre_multimid0": ("pregather", {"layout": "degree", "pack": 0, "multi_mid": 0}),
     "pre_trpipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
+    "pre_hubm16k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 16384}),
+    "pre_hubm64k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 65536}),
+    "pre_hubmall": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 1 << 30}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
