@@ -254,6 +254,10 @@ def run_single(args, wl):
     alg_bytes = 24 * g.E + 28 * g.n
     kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
     roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, args.steps), round_kernels(kinfo))
+    # the box's own streaming rate, measured in this run (untimed, after the timed region):
+    # a float4 copy of 1 GB, so a slow box shows as a slow copy as well as a slow round
+    roof["copy_GBs"] = fu.copy_bandwidth(0, 1 << 30, 5)
+    roof["frac_of_copy"] = roof["achieved"] / roof["copy_GBs"]
 
     conv = {"rounds_to_1e-9": None, "err_after_conv_rounds": None, "conv_rounds": None,
             "components": None}

@@ -179,6 +179,11 @@ int fu_get_info(fu_handle *h, int64_t info[32]);  /* ABI 2: 32 entries */
 int fu_get_pack(fu_handle *h, int32_t width[3]);
 int fu_synchronize(fu_handle *h);
 int fu_destroy(fu_handle *h);
+/* Measurement helper (no reference counterpart): the device's streaming rate, a float4
+ * copy of `bytes` bytes (read + write counted) repeated `iters` times on `device`, best of
+ * the repetitions in GB/s. bench.py reports it beside the roofline (roofline.copy_GBs) so a
+ * slow box reads as a slow copy too. */
+int fu_copy_bandwidth(int32_t device, int64_t bytes, int32_t iters, double *gbs);
 
 /* ======================================================================================
  * Tick-level replay (pairwise mode, and faithful collect-all on small platforms).

@@ -1077,6 +1077,12 @@ constexpr int kTrBE = FU_TR_BE;  // edges per bucket (8K: 76 KB of LDS, two bloc
 static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 positions, coarse table");
 constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
 constexpr int kTrThreads = 1024;
+// Hot estimates (option tr_hot): the neighbours of id < H (H <= kTrHot; under the degree
+// layout the H highest-degree nodes: R-MAT-24's first 10K take 23 % of all gathers) never
+// pass through the staging launch. Each transpose block keeps a_{r-1}[0, H) in LDS beside
+// its bucket and serves a bucket's hot edges from a per-bucket list {column, position} in
+// edge order: 4 B per hot edge read instead of 2 + 8 staged, 8 + 2 transposed.
+constexpr int kTrHot = 10240;  // 80 KB of LDS; with the 76 KB bucket tables: 156 KB of 160
 
 // Persistent over its buckets: grid = 8 x (blocks per XCD); XCD x owns the contiguous
 // bucket range [x per, (x + 1) per) and its blocks take every nj-th bucket of it. The next
@@ -1086,12 +1092,17 @@ constexpr int kTrThreads = 1024;
 #ifndef FU_TR_WAVES
 #define FU_TR_WAVES 1
 #endif
+template <bool HOT>
 __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
-                                                        double *__restrict__ GB) {
+                                                        double *__restrict__ GB,
+                                                        const double *__restrict__ a_prev, int H,
+                                                        const int *__restrict__ hoff,
+                                                        const unsigned *__restrict__ hlist) {
   __shared__ double s_v[kTrBE];
+  __shared__ double s_hot[HOT ? kTrHot : 1];
   __shared__ unsigned short s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
   __shared__ int s_o[kTrMaxP];      // G_A index of each run
   __shared__ int s_c[kTrBE / 64 + 1];
@@ -1104,6 +1115,8 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
   if (bk >= bend) return;
+  if (HOT)  // a_{r-1} of the hot nodes, once per block (visible after the first table barrier)
+    for (int q = t; q < H; q += kTrThreads) s_hot[q] = a_prev[q];
   // runs: thread t owns slices 2t, 2t + 1
   int o[2], len[2];
   auto load_runs = [&](int bkk, int (&oo)[2], int (&ll)[2]) {
@@ -1185,11 +1198,31 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
     val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
+  unsigned hx[HOT ? 2 : 1];  // the bucket's hot edges: at most 2 per thread in one pass
+  int h0 = 0, h1 = 0;
+  if (HOT) {
+    h0 = hoff[bb];
+    h1 = hoff[bb + 1];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int q = h0 + t + k * kTrThreads;
+      hx[k] = q < h1 ? hlist[q] : 0u;
+    }
+  }
   const int next = bk + nj;
   if (next < bend) load_runs(next, o, len);  // in flight beside this bucket's loads
 #pragma unroll
   for (int k = 0; k < kPerT; ++k)
     if (g[k] >= 0) s_v[pos[k]] = val[k];
+  if (HOT) {
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (h0 + t + k * kTrThreads < h1) s_v[hx[k] & 0xFFFFu] = s_hot[hx[k] >> 16];
+    for (int q = h0 + t + 2 * kTrThreads; q < h1; q += kTrThreads) {  // buckets of > 2048 hot edges
+      const unsigned x = hlist[q];
+      s_v[x & 0xFFFFu] = s_hot[x >> 16];
+    }
+  }
   __syncthreads();
   for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
   if (next >= bend) break;
@@ -1346,7 +1379,7 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
 // the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
 template <bool CHECK, int TE, int TN, int DIAG = 0, bool RF = true, bool LO = true>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
-    const int4 *__restrict__ tiles, int ntl,
+    const int4 *__restrict__ tiles, int t0, int ntl,
     const int *__restrict__ rowptr, const int *__restrict__ col,
     const StageArgs sa, const void *__restrict__ G, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev, const double *__restrict__ a_prev2,
@@ -1369,7 +1402,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   // XCD-aware order: block b runs on XCD b % 8; consecutive tiles go to the same XCD, so
   // the G runs that neighbouring tiles share in every slice region meet in one L2
   const int xcd = blockIdx.x & 7, per = ntl >> 3, rem = ntl & 7;
-  const int tile = DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3);
+  const int tile = t0 + (DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3));
   const int4 tl = tiles[tile];
   const int nb = tl.x, nn = tl.y - tl.x;
   const int e0 = tl.z, ne = tl.w - tl.z;
@@ -1522,19 +1555,32 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // pre-gathered estimates (CA:117-118). Same operations in the same order as every other
 // path: the results are bitwise equal.
 // ------------------------------------------------------------------------------------
+//
+// LAG (option "lag", kernel 9): no flow pass. Round r leaves f_r unwritten and instead
+// materialises f_{r-2} while it stages the row: F holds f_{r-4} and f_{r-2} = (recon(f_{r-4}, er_{r-2}, a_{r-4}) +
+// a_{r-2}) - er_{r-2} is exactly what round r - 2's flow pass would have written (CA:117-118,
+// same operations, same operands: er_{r-2} from the G_B ring, a_{r-4} from the per-row
+// history `hist`). So a lagged row costs 32 B per edge (f and G_B of two rounds, one flow
+// store) instead of 40 (both re-read for the flow pass). LAGM = 1: F holds f_{r-2}
+// already (fm = 1, 2: computed, and stored as the base of round r + 2); LAGM = 2: F holds
+// f_{r-4} (the previous round of this parity was lagged). lag_finalize
+// writes f_r when another kernel, fu_get_flows or a tile rebuild needs it.
 constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
-template <bool CHECK, bool FLOWS = true>
+template <bool CHECK, bool FLOWS = true, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
     const double *__restrict__ target, unsigned long long *__restrict__ err, void *__restrict__ code_new,
-    PackCtl *__restrict__ ctl, const double *__restrict__ Gb, int fm) {
+    PackCtl *__restrict__ ctl, const double *__restrict__ Gb, int fm,
+    const double *__restrict__ Gb_old = nullptr, double *__restrict__ hist = nullptr) {
+  constexpr bool LAG = LAGM > 0;
+  constexpr bool mat = LAGM == 2;
   // sh[buf][2 r + {0: fr, 1: er}][q]; a row stride of kMCH + 1 doubles puts the 32 chain lanes'
   // reads of one step on 32 different bank pairs
   __shared__ double sh[2][2 * kMR][kMCH + 1];
   __shared__ int s_b[kMR], s_d[kMR];
-  __shared__ double s_o2[kMR], s_a[kMR];
+  __shared__ double s_o2[kMR], s_a[kMR], s_o4[kMR];
   const PackCtl pc = ctl[2];  // packing of a_r (the table written here)
   const int t = threadIdx.x, w = t >> 6, lane = t & 63;
   const int r0 = blockIdx.x * kMR;
@@ -1544,37 +1590,56 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int b = ok ? rowptr[i] : 0;
     s_b[t] = b;
     s_d[t] = ok ? rowptr[i + 1] - b : 0;
-    s_o2[t] = ok ? a_prev2[i] : 0.0;
+    const double o2 = ok ? a_prev2[i] : 0.0;
+    s_o2[t] = o2;
+    if (LAG) {  // a_{r-4} of the row (written by round r - 2), then a_{r-2} for round r + 2
+      s_o4[t] = ok && mat ? hist[r0 + t] : 0.0;
+      if (ok) hist[r0 + t] = o2;
+    }
   }
   __syncthreads();
   // wave w stages rows 4 w .. 4 w + 3; element c kMCH + lane of each
   int rb[4], rd[4];
-  double ro2[4];
+  double ro2[4], ro4[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     rb[j] = s_b[4 * w + j];
     rd[j] = s_d[4 * w + j];
     ro2[j] = s_o2[4 * w + j];
+    ro4[j] = LAG ? s_o4[4 * w + j] : 0.0;
   }
   const int nch = (s_d[0] + kMCH - 1) / kMCH;  // rows sorted longest first
   // two register sets, each one chunk of the wave's 4 rows: the loads run two chunks ahead of
   // the chain. Loads are unconditional from clamped indices (the compiler then waits for a
   // set by count, vmcnt(N), not for everything)
   double fo0[4], er0[4], fo1[4], er1[4];
-  auto load = [&](double (&fo)[4], double (&er)[4], int c) {
+  double eo0[4], eo1[4];  // LAGM 2: er_{r-2} (G_B of round r - 2)
+  auto load = [&](double (&fo)[4], double (&er)[4], double (&eo)[4], int c) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = min(c * kMCH + lane, max(rd[j] - 1, 0));
       er[j] = Gb[rb[j] + k];
-      fo[j] = ld_fo(F, rb[j] + k, fm, ro2[j]);
+      if constexpr (mat) eo[j] = Gb_old[rb[j] + k];
+      if constexpr (mat) fo[j] = ld_f(F, rb[j] + k);
+      else fo[j] = ld_fo(F, rb[j] + k, fm, ro2[j]);
     }
   };
-  auto put = [&](const double (&fo)[4], const double (&er)[4], int c, int buf) {
+  auto put = [&](const double (&fo)[4], const double (&er)[4], const double (&eo)[4], int c, int buf) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int r = 4 * w + j;
       const bool in = c * kMCH + lane < rd[j];
-      sh[buf][2 * r][lane] = in ? recon_fr(fo[j], er[j], ro2[j]) : 0.0;
+      double f2 = fo[j];  // f_{r-2}
+      if (LAG && in) {
+        const int e = rb[j] + c * kMCH + lane;
+        if constexpr (mat) {  // round r - 2's flow (CA:117-118), from f_{r-4}
+          f2 = (recon_fr(fo[j], eo[j], ro4[j]) + ro2[j]) - eo[j];
+          st_f(F, e, f2, fo[j]);
+        } else if (fm) {  // f_{-1} / f_0, the base round r + 2 materialises from
+          st_f_full(F, e, f2);
+        }
+      }
+      sh[buf][2 * r][lane] = in ? recon_fr(f2, er[j], ro2[j]) : 0.0;
       sh[buf][2 * r + 1][lane] = in ? er[j] : 0.0;
     }
   };
@@ -1616,25 +1681,25 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     }
   };
   if (nch > 0) {
-    load(fo0, er0, 0);
-    load(fo1, er1, 1);
-    put(fo0, er0, 0, 0);
+    load(fo0, er0, eo0, 0);
+    load(fo1, er1, eo1, 1);
+    put(fo0, er0, eo0, 0, 0);
   }
   __syncthreads();
   for (int c = 0; c < nch; c += 2) {
     // chunk c in buffer 0, chunk c + 1 in flight in set 1
-    if (c + 2 < nch) load(fo0, er0, c + 2);
+    if (c + 2 < nch) load(fo0, er0, eo0, c + 2);
     chain(c, 0);
     __syncthreads();
     if (c + 1 >= nch) break;
-    put(fo1, er1, c + 1, 1);
+    put(fo1, er1, eo1, c + 1, 1);
     __syncthreads();
     // chunk c + 1 in buffer 1, chunk c + 2 in flight in set 0
-    if (c + 3 < nch) load(fo1, er1, c + 3);
+    if (c + 3 < nch) load(fo1, er1, eo1, c + 3);
     chain(c + 1, 1);
     __syncthreads();
     if (c + 2 >= nch) break;
-    put(fo0, er0, c + 2, 0);
+    put(fo0, er0, eo0, c + 2, 0);
     __syncthreads();
   }
   unsigned long long eb = 0;
@@ -1649,7 +1714,7 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       if (CHECK) eb = err_bits(a, target[i]);
     }
   }
-  if (!FLOWS) {  // the mega hubs: k_hub_flows writes their flows with the whole grid
+  if (!FLOWS || LAG) {  // mega hubs: k_hub_flows writes their flows; LAG: round r + 2 does
     if (CHECK) block_max_to(eb, err);
     return;
   }
@@ -1675,6 +1740,32 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     }
   }
   if (CHECK) block_max_to(eb, err);
+}
+
+// Lagged rows (k_heavy_multi<LAG>): write the flows f_{r'} their last round r' of this
+// parity left unwritten: F holds f_{r'-2}, Gb = er_{r'} (G_B of round r'), hist = a_{r'-2},
+// a = a_{r'} (CA:117-118, the flow pass k_heavy_multi would have run). One block per row.
+__global__ __launch_bounds__(kBlock) void k_lag_final(const int *__restrict__ rows, const int *__restrict__ rowptr,
+                                                      double *__restrict__ F, const double *__restrict__ Gb,
+                                                      const double *__restrict__ hist,
+                                                      const double *__restrict__ a) {
+  const int i = rows[blockIdx.x];
+  const int b = rowptr[i], d = rowptr[i + 1] - b;
+  const double own2 = hist[blockIdx.x], an = a[i];
+  for (int k0 = 0; k0 < d; k0 += 8 * kBlock) {
+    double f8[8], e8[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + (int)threadIdx.x + kBlock * u;
+      e8[u] = k < d ? Gb[b + k] : 0.0;
+      f8[u] = k < d ? ld_f(F, b + k) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int k = k0 + (int)threadIdx.x + kBlock * u;
+      if (k < d) st_f(F, b + k, (recon_fr(f8[u], e8[u], own2) + an) - e8[u], f8[u]);
+    }
+  }
 }
 
 // Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
@@ -1736,6 +1827,13 @@ __global__ void k_unsplit(long long cnt, const double *__restrict__ src, double 
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) dst[q] = ld_f(src, (int)q);
 }
+// fu_copy_bandwidth: a plain float4 copy, grid-stride (the part's streaming rate)
+__global__ __launch_bounds__(kBlock) void k_copy4(long long cnt, const float4 *__restrict__ src,
+                                                  float4 *__restrict__ dst) {
+  const long long stride = (long long)gridDim.x * kBlock;
+  for (long long q = (long long)blockIdx.x * kBlock + threadIdx.x; q < cnt; q += stride) dst[q] = src[q];
+}
+
 __global__ void k_fill(long long cnt, double val, double *__restrict__ p) {
   long long q = (long long)blockIdx.x * kBlock + threadIdx.x;
   if (q < cnt) p[q] = val;
@@ -2259,6 +2357,7 @@ struct fu_handle {
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
   int tr_pipe = 0;       // kernel 9: software-pipelined transpose (k_transpose_pipe; needs tr_bpx > 0)
+  int tr_hot = 0;        // kernel 9: neighbours of id < tr_hot (<= kTrHot) served from the transpose's LDS
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int c16 = 1;           // kernel 4: narrow light tiles read 2-byte column offsets
   int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
@@ -2329,6 +2428,7 @@ struct fu_handle {
   std::string st_why;                     // why no layout could be built (kernel 8 unavailable)
   int4 *st_tiles = nullptr;               // light tiles
   int st_ntiles = 0;
+  int st_nbound = 0;                      // multi-GPU: leading light tiles with ghost neighbours
   int4 *st_heavy = nullptr;               // rows above the tile limit ({i, -1, b, e})
   int st_nheavy = 0;
   void *stG = nullptr;                    // staged estimates, 8 B per G element
@@ -2343,10 +2443,24 @@ struct fu_handle {
     unsigned short *colS = nullptr;       // per G_A element: column offset in its slice
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
     int *offT = nullptr;                  // (B + 1) x P: G_A index where bucket b's run of slice s starts
-    double *GA = nullptr, *GB = nullptr;
+    double *GA = nullptr;
+    int H = 0;                            // hot neighbours: id < H (tr_hot), served from LDS
+    int *hoff = nullptr;                  // B + 1: per bucket, its range of hlist
+    unsigned *hlist = nullptr;            // per hot edge: column << 16 | position in its bucket
+    double *GBr[3] = {nullptr, nullptr, nullptr};  // G_B of round r in GBr[r % 3] (one buffer without lag)
+    double *hist[2] = {nullptr, nullptr};          // lag: per parity, a_{r-2} of every lagged row
+    int hist_hub = 0;                              // lag: hist slot of the first mega hub
   };
   TransLayout tr;
   bool tr_ready = false;
+  // kernel 9 option "lag" (k_heavy_multi<LAG>): per parity p, lagf[p] = F[p] holds f_{r'-2}
+  // (not f_{r'}) on the lagged rows, r' = lag_round[p] the last round of that parity; the
+  // lagged rows: lag_nmulti[p] heavy rows and, if lag_hubs[p], every mega hub
+  int lag = 0;
+  int lagf[2] = {0, 0};
+  int64_t lag_round[2] = {0, 0};
+  int lag_nmulti[2] = {0, 0};
+  int lag_hubs[2] = {0, 0};
   std::string tr_why;
   int n_cu = 256;
   void *dist = nullptr;  // multi-GPU (fu_dist.hip)
@@ -2511,8 +2625,10 @@ int build_hubs(fu_handle *h) {
 }
 
 void free_transpose(fu_handle *h);
+int lag_finalize_all(fu_handle *h);
 
 int build_tiles(fu_handle *h) {
+  if (int rc = lag_finalize_all(h)) return rc;  // the lagged rows' flows, before their lists change
   free_transpose(h);  // its hub exclusion follows the tiles
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
@@ -2557,6 +2673,17 @@ int ensure_light(fu_handle *h) {
     }
     light.push_back(make_int4(b, i, (int)rp[b], (int)rp[i]));
   }
+  // multi-GPU (ghost estimate slots exist): light tiles that read a ghost go first, so the
+  // halo exchange can start once they are done, beside the interior tiles (as kernel 4)
+  h->st_nbound = 0;
+  if (h->na > h->n) {
+    auto has_ghost = [&](const int4 &tl) {
+      for (int32_t e = tl.z; e < tl.w; ++e)
+        if (h->h_col[e] >= n) return true;
+      return false;
+    };
+    h->st_nbound = (int)(std::stable_partition(light.begin(), light.end(), has_ghost) - light.begin());
+  }
   h->h_light = light;
   if (int rc = dmalloc(&h->st_tiles, std::max<size_t>(1, light.size()))) return rc;
   if (int rc = dmalloc(&h->st_heavy, std::max<size_t>(1, heavy.size()))) return rc;
@@ -2579,7 +2706,6 @@ int ensure_stage(fu_handle *h) {
   if (h->st_ready) return FU_OK;
   if (!h->st_why.empty()) return fail(FU_ERR_GRAPH, h->st_why);
   if (int rc = ensure_light(h)) return rc;
-  const int32_t n = h->n;
   const std::vector<int4> &light = h->h_light;
   const int T = (int)light.size();
   auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
@@ -2592,7 +2718,7 @@ int ensure_stage(fu_handle *h) {
   for (int li = 0; li < 4 && T > 0; ++li) {
     auto &L = h->st[li];
     const int64_t SN = std::min<int64_t>(kStageLds >> li, 65536);  // column offsets are u16
-    const int64_t P = (n + SN - 1) / SN;
+    const int64_t P = ((int64_t)h->na + SN - 1) / SN;  // multi-GPU: the ghost slots are slices too
     if (P > kStageMaxP) {
       why = "kernel 8 (staged slices): more than " + std::to_string(kStageMaxP) + " slices";
       continue;
@@ -2729,8 +2855,11 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
 // slice's region into Q pieces.
 void free_transpose(fu_handle *h) {
   auto &T = h->tr;
-  for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA, (void *)T.GB})
+  for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA,
+                  (void *)T.GBr[0], (void *)T.hist[0], (void *)T.hist[1], (void *)T.hoff, (void *)T.hlist})
     if (p) hipFree(p);
+  if (T.GBr[1] != T.GBr[0]) hipFree(T.GBr[1]);
+  if (T.GBr[2] != T.GBr[0]) hipFree(T.GBr[2]);
   T = fu_handle::TransLayout{};
   h->tr_ready = false;
 }
@@ -2750,8 +2879,11 @@ int ensure_transpose(fu_handle *h) {
   int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
     if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
+  // hot neighbours (id < H) bypass the staging launch (k_transpose<true>; not k_transpose_pipe)
+  const int32_t H = h->tr_pipe ? 0 : (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
   std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < E; ++e) cnt[h->h_col[e] / SN]++;
+  for (int64_t e = 0; e < E; ++e)
+    if (h->h_col[e] >= H) cnt[h->h_col[e] / SN]++;
   std::vector<int64_t> reg(P + 1, 0);
   for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
   const int64_t total = reg[P];
@@ -2762,16 +2894,24 @@ int ensure_transpose(fu_handle *h) {
   std::vector<uint16_t> colS(total, 0), pos(total, 0);
   std::vector<int32_t> offT((size_t)(B + 1) * P);
   std::vector<int64_t> cur(reg.begin(), reg.end() - 1);
+  std::vector<int32_t> hoff(B + 1, 0);
+  std::vector<uint32_t> hlist;
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
+    hoff[b] = (int32_t)hlist.size();
     const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
     for (int64_t e = b * kTrBE; e < e1; ++e) {
       const int32_t c = h->h_col[e];
+      if (c < H) {  // {column, position in the bucket}, edge order
+        hlist.push_back(((uint32_t)c << 16) | (uint32_t)(e - b * kTrBE));
+        continue;
+      }
       const int64_t g = cur[c / SN]++;
       colS[g] = (uint16_t)(c % SN);
       pos[g] = (uint16_t)(e - b * kTrBE);
     }
   }
+  hoff[B] = (int32_t)hlist.size();
   for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)B * P + s2] = (int32_t)cur[s2];
   // stage pieces by element count, not per slice: under the degree layout the hottest slice
   // holds ~40% of all elements (R-MAT-24), so a slice gets as many blocks as its share
@@ -2792,8 +2932,21 @@ int ensure_transpose(fu_handle *h) {
   if (int rc = up(&T.colS, colS.data(), colS.size())) return rc;
   if (int rc = up(&T.pos16, pos.data(), pos.size())) return rc;
   if (int rc = up(&T.offT, offT.data(), offT.size())) return rc;
+  if (int rc = up(&T.hoff, hoff.data(), hoff.size())) return rc;
+  if (int rc = up(&T.hlist, hlist.data(), hlist.size())) return rc;
+  T.H = H;
   if (int rc = dmalloc(&T.GA, (size_t)total)) return rc;
-  if (int rc = dmalloc(&T.GB, (size_t)E)) return rc;
+  // G_B: a ring of three with lag (round r reads G_B of round r - 2 for the lagged rows)
+  for (int k = 0; k < 3; ++k) {
+    if (k && !h->lag) {
+      T.GBr[k] = T.GBr[0];
+      continue;
+    }
+    if (int rc = dmalloc(&T.GBr[k], (size_t)E)) return rc;
+  }
+  T.hist_hub = h->multi_geo[1][1];
+  for (int p = 0; p < 2; ++p)
+    if (int rc = dmalloc(&T.hist[p], (size_t)(T.hist_hub + h->n_hub + 1))) return rc;
   T.P = (int)P;
   T.Q = (int)Q;
   T.NB = (int)br.size();
@@ -2804,6 +2957,32 @@ int ensure_transpose(fu_handle *h) {
 }
 
 inline unsigned grid_for(long long work) { return (unsigned)((work + kBlock - 1) / kBlock); }
+
+// Kernel 9 "lag": write the flows parity p's last round r' left unwritten on its lagged rows
+// (k_lag_final: F[p] holds f_{r'-2}; G_B of r' is GBr[r' % 3], a_{r'} is A[r' % 3]). Valid
+// while r' is one of the last two rounds (the A ring holds a_{r'}; no kernel-9 round has
+// reused r''s G_B slot), which holds at every call site: before a round of another kernel,
+// fu_get_flows, a tile rebuild, the option's change.
+int lag_finalize(fu_handle *h, int p) {
+  if (!h->lagf[p]) return FU_OK;
+  const int64_t rr = h->lag_round[p];
+  const double *Gb = h->tr.GBr[rr % 3];
+  const double *a = h->a[rr % 3];
+  if (h->lag_nmulti[p])
+    hipLaunchKernelGGL(k_lag_final, dim3(h->lag_nmulti[p]), dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0],
+                       h->rowptr, h->f[p], Gb, h->tr.hist[p], a);
+  if (h->lag_hubs[p] && h->n_hub)
+    hipLaunchKernelGGL(k_lag_final, dim3(h->n_hub), dim3(kBlock), 0, h->stream, h->hub_sorted, h->rowptr, h->f[p], Gb,
+                       h->tr.hist[p] + h->tr.hist_hub, a);
+  HIP_TRY(hipGetLastError());
+  h->lagf[p] = 0;
+  return FU_OK;
+}
+int lag_finalize_all(fu_handle *h) {
+  for (int p = 0; p < 2; ++p)
+    if (int rc = lag_finalize(h, p)) return rc;
+  return FU_OK;
+}
 
 // k_transpose grid for nbk buckets: 8 XCDs x min(buckets per XCD, tr_bpx blocks per XCD)
 // (tr_bpx 0: one block per bucket)
@@ -2824,6 +3003,7 @@ void plan_alone(fu_handle *h, RoundCtx &c) {
 // flows are written (rounds 1 and 2 compute f_{-1} and f_0 themselves: fm).
 int launch_round0(fu_handle *h, RoundCtx &c) {
   static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
+  h->lagf[0] = h->lagf[1] = 0;  // zero state: no lagged flows
   hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
                      h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
   if (c.err)
@@ -2848,7 +3028,7 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   const StageArgs sa = stage_args(h, &sgrid);
   const void *cp = h->code[(c.r - 1) & 1];
   if (h->st_ntiles && D < 2) {
-    hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap, cp,
+    hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap, cp,
                        h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
@@ -2863,23 +3043,33 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
     else heavy(std::false_type{});
   }
   // light tiles: rounds 1 and 2 (fm) read no flows (RF = false); LO = staged indices first
-  auto light = [&](auto chk, auto rf, auto lo) {
-    hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, D, decltype(rf)::value,
-                                       decltype(lo)::value>),
-                       dim3(h->st_ntiles), dim3(kBlock), 0, h->stream, h->st_tiles, h->st_ntiles, h->rowptr, h->col,
-                       sa, h->stG, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
+  // multi-GPU: the boundary tiles [0, st_nbound), then the halo goes out on the comm stream
+  // beside the interior tiles
+  auto light = [&](auto chk, auto rf, auto lo) -> int {
+    const int nb = h->dist ? h->st_nbound : 0;
+    for (int part = 0; part < 2; ++part) {
+      const int t0 = part ? nb : 0, cnt = part ? h->st_ntiles - nb : nb;
+      if (cnt)
+        hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, D, decltype(rf)::value,
+                                           decltype(lo)::value>),
+                           dim3(cnt), dim3(kBlock), 0, h->stream, h->st_tiles, t0, cnt, h->rowptr, h->col, sa,
+                           h->stG, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
+      if (!part && h->dist) {  // boundary rows (and the heavy rows) done
+        h->halo_a = c.an;
+        if (int rc = fu__dist_round_hook(h, 2)) return rc;
+      }
+    }
+    return FU_OK;
   };
   auto light_lo = [&](auto chk, auto rf) {
-    if (h->staged_lo) light(chk, rf, std::true_type{});
-    else light(chk, rf, std::false_type{});
+    return h->staged_lo ? light(chk, rf, std::true_type{}) : light(chk, rf, std::false_type{});
   };
   auto light_rf = [&](auto chk) {
-    if (c.fm) light_lo(chk, std::false_type{});
-    else light_lo(chk, std::true_type{});
+    return c.fm ? light_lo(chk, std::false_type{}) : light_lo(chk, std::true_type{});
   };
-  if (h->st_ntiles) {
-    if (c.err && !D) light_rf(std::true_type{});
-    else light_rf(std::integral_constant<bool, C0>{});
+  if (h->st_ntiles || h->dist) {
+    if (c.err && !D) return light_rf(std::true_type{});
+    return light_rf(std::integral_constant<bool, C0>{});
   }
   return FU_OK;
 }
@@ -2892,7 +3082,8 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
 template <int D>
 int launch_k9(fu_handle *h, RoundCtx &c) {
   if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
-  const double *Gb = h->tr.GB;
+  double *Gb = h->tr.GBr[c.r % 3];
+  const double *Gb_old = h->tr.GBr[(c.r + 1) % 3];  // G_B of round r - 2 (lag)
   if (!Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
   const int r1 = (int)(c.r & 1);
   const void *cp = h->code[(c.r - 1) & 1];
@@ -2918,31 +3109,58 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   }
   plan_alone(h, c);
   const int bh = hubs ? h->tr.Bh : 0;
-  auto ktr = h->tr_pipe && h->tr_bpx > 0 ? k_transpose_pipe : k_transpose;
-  if (D != 21 && D != 24 && bh)
-    hipLaunchKernelGGL(ktr, dim3(tr_grid(h, bh)), dim3(kTrThreads), 0, h->stream, 0, bh, h->tr.P,
-                       (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+  // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
+  // multi-row heavy rows, and the mega hubs when all of them run as multi-row blocks
+  int nbig = nmega;  // hub_multi: hubs longer than it keep a block each
+  if (h->hub_multi) {
+    nbig = 0;
+    while (nbig < nmega && h->h_hub_len[nbig] > h->hub_multi) ++nbig;
+  }
+  const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
+  const int mend = h->multi_mid ? m1 : m0_;
+  const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
+  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && D == 0 && n_multi > 0;
+  const bool lag_multi = h->lag && multi;
+  const bool lag_hub = h->lag && hubs && h->hub_multi && nbig == 0 && D == 0;
+  const int p = r1;
+  if (h->lagf[p] && (h->lag_nmulti[p] != (lag_multi ? n_multi : 0) || h->lag_hubs[p] != (int)lag_hub)) {
+    if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
+  }
+  const int lagm = (lag_multi || lag_hub) ? (h->lagf[p] ? 2 : 1) : 0;
+  const bool pipe = h->tr_pipe && h->tr_bpx > 0 && h->tr.H == 0;
+  auto tr_launch = [&](int b0, int nb) {
+    if (pipe)
+      hipLaunchKernelGGL(k_transpose_pipe, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb);
+    else if (h->tr.H)
+      hipLaunchKernelGGL(k_transpose<true>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
+    else
+      hipLaunchKernelGGL(k_transpose<false>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
+  };
+  if (D != 21 && D != 24 && bh) tr_launch(0, bh);
   if (hubs) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
-  if (D != 21 && D != 24 && h->tr.B > bh)
-    hipLaunchKernelGGL(ktr, dim3(tr_grid(h, h->tr.B - bh)), dim3(kTrThreads), 0, h->stream, bh, h->tr.B - bh,
-                       h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, h->tr.GB);
+  if (D != 21 && D != 24 && h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
   const bool chk = c.err && !D;
   if (hubs) {
     auto chains = [&](auto C) {
       // hub_multi: the hubs of <= hub_multi edges as k_heavy_multi blocks (kMR hubs of similar
       // length per block, one chain wave: few blocks hold LDS beside the transposes); the
       // longer ones keep a block each (deeper prefetch on their long chains)
-      int nbig = nmega;
-      if (h->hub_multi) {
-        nbig = 0;
-        while (nbig < nmega && h->h_hub_len[nbig] > h->hub_multi) ++nbig;
-        if (nmega > nbig)
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, false>), dim3((nmega - nbig + kMR - 1) / kMR),
-                             dim3(kBlock), 0, h->stream2, h->hub_sorted + nbig, nmega - nbig, h->rowptr, h->v, c.F,
-                             c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm);
+      if (h->hub_multi && nmega > nbig) {
+        auto hm = [&](auto L) {
+          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, false, decltype(L)::value>),
+                             dim3((nmega - nbig + kMR - 1) / kMR), dim3(kBlock), 0, h->stream2, h->hub_sorted + nbig,
+                             nmega - nbig, h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl,
+                             Gb, c.fm, Gb_old, h->tr.hist[p] + h->tr.hist_hub);
+        };
+        if (!lag_hub) hm(std::integral_constant<int, 0>{});
+        else if (lagm == 1) hm(std::integral_constant<int, 1>{});
+        else hm(std::integral_constant<int, 2>{});
       }
       if (nbig)
         hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
@@ -2952,8 +3170,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
-    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
-                       (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
+    if (!lag_hub)
+      hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
+                         (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
   }
@@ -2971,14 +3190,16 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // k_heavy_multi blocks, many rows per chain wave
   // (multi_mid = 0: only the rows of [nmega, m0), longer than the register launch's; the rows
   // of [m0, m1) then stay in registers, one pass)
-  const int mend = h->multi_mid ? m1 : m0;
-  const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
-  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && D == 0 && n_multi > 0;
   auto tiles = [&](auto C) {
     if (multi) {
-      hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value>), dim3((n_multi + kMR - 1) / kMR), dim3(kBlock), 0,
-                         h->stream, h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F, c.ap2, c.an,
-                         h->target, c.err, h->code[r1], h->pctl, Gb, c.fm);
+      auto hm = [&](auto L) {
+        hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, true, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
+                           dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F,
+                           c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old, h->tr.hist[p]);
+      };
+      if (!lag_multi) hm(std::integral_constant<int, 0>{});
+      else if (lagm == 1) hm(std::integral_constant<int, 1>{});
+      else hm(std::integral_constant<int, 2>{});
       if (!h->multi_mid) heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     } else {
       heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
@@ -2996,6 +3217,12 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   }
   HIP_TRY(hipGetLastError());
   if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
+    h->lagf[p] = 1;
+    h->lag_round[p] = c.r;
+    h->lag_nmulti[p] = lag_multi ? n_multi : 0;
+    h->lag_hubs[p] = (int)lag_hub;
+  }
   return FU_OK;
 }
 
@@ -3133,6 +3360,11 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
   if (!h->tuning) h->plan_pending = false;
   const bool plan_done = c.plan;
   int rc;
+  // kernel 9's lag: another kernel reads F[r & 1] as f_{r-2}, so the lagged rows' flows of
+  // round r - 2 are written first
+  if (r > 0 && h->kernel != 9 && h->lagf[r & 1]) {
+    if (int rc2 = lag_finalize(h, (int)(r & 1))) return rc2;
+  }
   if (r == 0) rc = launch_round0(h, c);
   else if (h->diag_body) rc = h->diag_body(h, c);
   else rc = launch_body<0>(h, c);
@@ -3375,7 +3607,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!std::strcmp(key, "kernel")) {
     if (value != 0 && value != 4 && value != 8 && value != 9)
       return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon), 8 (stage) or 9 (pregather)");
-    if (h->dist && value >= 8) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernel 4 (recon)");
+    if (h->dist && value == 9) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 4 (recon) and 8 (stage)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     if (value == 8) {
       if (int rc = ensure_stage(h)) return rc;
@@ -3446,12 +3678,34 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_pipe")) {  // kernel 9: software-pipelined transpose (1)
+    if ((value != 0) != (h->tr_pipe != 0)) {
+      if (int rc = lag_finalize_all(h)) return rc;
+      free_transpose(h);  // the layout's hot lists follow it (k_transpose_pipe has none)
+    }
     h->tr_pipe = value != 0;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "tr_hot")) {  // kernel 9: neighbours of id < value served from LDS (0: none)
+    if (value < 0 || value > kTrHot) return fail(FU_ERR_ARG, "fu_set_option: tr_hot must be in [0, 10240]");
+    if (value != h->tr_hot) {
+      if (int rc = lag_finalize_all(h)) return rc;
+      free_transpose(h);  // the staging layout leaves the hot neighbours out
+    }
+    h->tr_hot = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_bpx")) {  // kernel 9: transpose blocks per XCD (0 = one per bucket)
     if (value < 0 || value > 1 << 20) return fail(FU_ERR_ARG, "fu_set_option: tr_bpx must be in [0, 2^20]");
     h->tr_bpx = (int)value;
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "lag")) {  // kernel 9: the multi-row heavy rows (and hubs) write f_r in round r + 2
+    const int lv = value != 0;
+    if (lv != h->lag) {
+      if (int rc = lag_finalize_all(h)) return rc;  // flows first, with the current G_B ring
+      free_transpose(h);                            // the ring's size follows the option
+      h->lag = lv;
+    }
     return FU_OK;
   }
   if (!std::strcmp(key, "hub_multi")) {  // kernel 9: mega hubs of <= value edges many per chain wave (0: one per block)
@@ -3501,6 +3755,7 @@ int fu_reset(fu_handle *h) {
   }
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->rounds = 0;
+  h->lagf[0] = h->lagf[1] = 0;  // zero state: nothing lagged
   h->pw_pending = false;  // the stream is idle: no plan in flight
   h->plan_pending = false;  // round 0 clears the plan
   *h->h_pw = 0;           // round 0 clears the packing plan
@@ -3549,7 +3804,7 @@ constexpr int kTimed = 8;
 static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
   // candidate is dropped and none stops early on rank-local timings
-  auto active = [&](int c) { return (h->dist || h->tune_out[c] < 2) && !(h->dist && kCands[c].kernel != 4); };
+  auto active = [&](int c) { return (h->dist || h->tune_out[c] < 2) && !(h->dist && kCands[c].kernel == 9); };
   // kernel 9 stages the doubles whatever the packing: a candidate of the unpacked table only
   auto active9 = [&](int c) { return active(c) && !(kCands[c].kernel == 9 && width != 0); };
   int32_t need = 0;
@@ -3576,6 +3831,14 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     if (!active9(c)) continue;
     if (kCands[c].kernel == 8 && ensure_stage(h) != FU_OK) {  // no slice layout fits this graph
       set_error("");
+      if (!h->dist) continue;
+      // multi-GPU: this rank still runs the candidate's rounds (kernel 4), so that every
+      // rank runs the same rounds (each is a halo exchange); its time is never the best
+      use_cand(h, kCands[0]);
+      for (int k = 0; k < 1 + kTimed; ++k)
+        if (int rc = launch_round(h, nullptr)) return rc;
+      *budget -= 1 + kTimed;
+      h->tune_ms[c] = 1e30f;
       continue;
     }
     if (kCands[c].kernel == 9 && ensure_transpose(h) != FU_OK) {  // too many nodes for the slices
@@ -3791,6 +4054,9 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   if (!h->ftmp) {
     if (int rc = dmalloc(&h->ftmp, (size_t)h->E)) return rc;
   }
+  if (h->rounds >= 2) {  // kernel 9's lag: the last round's flows of its lagged rows
+    if (int rc = lag_finalize(h, (int)((h->rounds - 1) & 1))) return rc;
+  }
   if (h->rounds == 1)  // round 0 writes no flows (fm): f_0 = (0.0 + a_0[i]) - 0.0 on demand
     hipLaunchKernelGGL(k_round0_flows, dim3((unsigned)((h->E + kR0E - 1) / kR0E)), dim3(kBlock), 0, h->stream,
                        (long long)h->E, h->rowptr, h->blk_row, h->a[0], h->f[0], nullptr);
@@ -3852,6 +4118,47 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done) {
   if (!h || !rounds_done) return fail(FU_ERR_ARG, "fu_get_round: NULL argument");
   *rounds_done = h->rounds;
   return FU_OK;
+}
+
+int fu_copy_bandwidth(int32_t device, int64_t bytes, int32_t iters, double *gbs) {
+  FU_TRY_BEGIN
+  if (!gbs || bytes < 16 * 1024 || iters < 1) return fail(FU_ERR_ARG, "fu_copy_bandwidth: bad arguments");
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return fail(FU_ERR_HIP, "fu_copy_bandwidth: no HIP device visible");
+  if (device < 0 || device >= nd) return fail(FU_ERR_ARG, "fu_copy_bandwidth: bad device");
+  HIP_TRY(hipSetDevice(device));
+  const long long cnt = bytes / 2 / 16;  // half read, half written
+  float4 *a = nullptr, *b = nullptr;
+  if (int rc = dmalloc(&a, (size_t)cnt)) return rc;
+  if (int rc = dmalloc(&b, (size_t)cnt)) {
+    hipFree(a);
+    return rc;
+  }
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int rc = FU_OK;
+  float best = 1e30f;
+  const unsigned grid = 8u * 256u * 8u;  // 8 blocks per CU, grid-stride
+  if (hipMemset(a, 0, sizeof(float4) * cnt) != hipSuccess || hipEventCreate(&e0) != hipSuccess ||
+      hipEventCreate(&e1) != hipSuccess)
+    rc = fail(FU_ERR_HIP, "fu_copy_bandwidth: setup");
+  for (int k = 0; rc == FU_OK && k <= iters; ++k) {  // the first copy warms up, untimed
+    hipEventRecord(e0, nullptr);
+    hipLaunchKernelGGL(k_copy4, dim3(grid), dim3(kBlock), 0, nullptr, cnt, a, b);
+    hipEventRecord(e1, nullptr);
+    float ms = 0.f;
+    if (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess)
+      rc = fail(FU_ERR_HIP, "fu_copy_bandwidth: copy");
+    else if (k > 0)
+      best = std::min(best, ms);
+  }
+  if (e0) hipEventDestroy(e0);
+  if (e1) hipEventDestroy(e1);
+  hipFree(a);
+  hipFree(b);
+  if (rc) return rc;
+  *gbs = 2.0 * 16.0 * (double)cnt / (best * 1e-3) / 1e9;
+  return FU_OK;
+  FU_TRY_END
 }
 
 int fu_synchronize(fu_handle *h) {

@@ -75,6 +75,7 @@ _SIGS = {
     "fu_get_pack": ([vp, vp], ctypes.c_int),
     "fu_synchronize": ([vp], ctypes.c_int),
     "fu_destroy": ([vp], ctypes.c_int),
+    "fu_copy_bandwidth": ([i32, i64, i32, P(f64)], ctypes.c_int),
     "fu_trace_build": ([i32, vp, vp, i32, i32, cp, P(vp)], ctypes.c_int),
     "fu_trace_build_ex": ([i32, vp, vp, i32, i32, cp, cp, P(vp)], ctypes.c_int),
     "fu_trace_build_routes": ([i32, vp, vp, i32, i32, cp, cp, vp, P(vp)], ctypes.c_int),
@@ -134,6 +135,13 @@ def ptr(a: np.ndarray | None):
     if not a.flags["C_CONTIGUOUS"]:
         raise ValueError("array must be C-contiguous")
     return a.ctypes.data_as(vp)
+
+
+def copy_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5) -> float:
+    """The device's float4 copy rate in GB/s (read + write), best of `iters` copies."""
+    g = f64(0.0)
+    call("fu_copy_bandwidth", int(device), int(nbytes), int(iters), ctypes.byref(g))
+    return float(g.value)
 
 
 def device_count() -> int:

@@ -259,19 +259,25 @@ def test_dist_single_rank_rccl_matches_engine():
     d.set_targets(tgt)
     tr = d.run(10, err_every=5)
     assert len(tr) == 2 and np.isfinite(tr).all()
-    with pytest.raises(fu.FuError, match="multi-GPU supports kernel 4"):
-        DistCollectAll(plan, v, unique_id(), kernel="stage")
     d.close()
+    d8 = DistCollectAll(plan, v, unique_id(), kernel="stage")  # kernel 8 at one RCCL rank
+    d8.run(30)
+    assert np.array_equal(d8.estimates(), eng.estimates())
+    assert np.array_equal(d8.flows(), eng.flows())
+    d8.close()
 
 
+@pytest.mark.parametrize("kernel", ["recon", "stage"])
 @pytest.mark.parametrize("world", [2, 3])
 @pytest.mark.parametrize("kind", ["rgg", "er"])
-def test_dist_ghost_slots_local_transport_bitwise(world, kind):
+def test_dist_ghost_slots_local_transport_bitwise(world, kind, kernel):
     """Every rank of a partitioned graph as its own handle on GPU 0, the halo moved by the
     in-process transport through the RCCL path's comm-stream / event chain (pack on the comm
     stream behind the boundary tiles, copies into the peers' ghost slots beside the interior
     tiles, the next round behind ev_halo), 100 rounds queued with no host sync. Estimates and
-    flows equal the C oracle bitwise. ER cuts most edges (every rank talks to every rank)."""
+    flows equal the C oracle bitwise. ER cuts most edges (every rank talks to every rank).
+    kernel "stage": kernel 8, the ghost slots staged as slices of their own (boundary light
+    tiles first, then the halo beside the interior tiles)."""
     from fu.dist import DistCollectAll, partition, run_local
 
     if kind == "rgg":
@@ -281,7 +287,8 @@ def test_dist_ghost_slots_local_transport_bitwise(world, kind):
     v = fu.uniform_values(g.n, seed=21)
     plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
     assert all(p.n_ghost_a > 0 and len(p.send_a_idx) > 0 for p in plans)
-    engs = [DistCollectAll(p, v[p.lo:p.hi], None) for p in plans]
+    engs = [DistCollectAll(p, v[p.lo:p.hi], None, kernel=kernel) for p in plans]
+    assert all(e.info()["kernel"] == kernel for e in engs)
     rounds = 100
     run_local(engs, rounds)
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
@@ -290,6 +297,16 @@ def test_dist_ghost_slots_local_transport_bitwise(world, kind):
         assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), p.rank
     for e in engs:
         e.close()
+
+
+def test_dist_refuses_kernel_9():
+    from fu.dist import DistCollectAll, partition
+
+    g = fu.Graph.erdos_renyi(20_000, 80_000, seed=2)
+    v = fu.uniform_values(g.n, seed=2)
+    p = partition(g.rowptr, g.col, g.rev, 2, 0)
+    with pytest.raises(fu.FuError, match="kernels 4 .recon. and 8 .stage."):
+        DistCollectAll(p, v[p.lo:p.hi], None, kernel="pregather")
 
 
 @pytest.mark.parametrize("world", [2, 3])
@@ -609,7 +626,8 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all", "lag", "lag_hubm_all", "lag_hubm",
+                                   "hot", "hot_lag", "hot_pipe"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -630,6 +648,23 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("hub_multi", 2 * mega)
     elif multi == "hubm_all":
         eng.set_option("hub_multi", 1 << 30)
+    elif multi == "lag":  # the multi-row heavy rows write f_r in round r + 2
+        eng.set_option("lag", 1)
+    elif multi == "lag_hubm_all":  # ... and every mega hub (all as multi-row blocks: no k_hub_flows)
+        eng.set_option("lag", 1)
+        eng.set_option("hub_multi", 1 << 30)
+    elif multi == "lag_hubm":  # hubs split: the longer ones keep k_hub_flows, none lagged
+        eng.set_option("lag", 1)
+        eng.set_option("hub_multi", 2 * mega)
+    elif multi == "hot":  # neighbours of id < 10240 served from the transpose's LDS
+        eng.set_option("tr_hot", 10240)
+    elif multi == "hot_lag":
+        eng.set_option("tr_hot", 3000)
+        eng.set_option("lag", 1)
+        eng.set_option("hub_multi", 1 << 30)
+    elif multi == "hot_pipe":  # tr_pipe has no hot lists: the layout keeps every neighbour staged
+        eng.set_option("tr_hot", 10240)
+        eng.set_option("tr_pipe", 1)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -899,3 +934,61 @@ def test_bench_rccl_two_ranks_parity_and_convergence():
     line = json.loads(p.stdout.strip().splitlines()[-1])
     assert line["n_gpus"] == 2 and line["rccl_parity"] == "bitwise"
     assert line["err_after_conv_rounds"] is not None and line["components"] >= 1
+
+
+def test_copy_bandwidth_plausible():
+    """bench.py's roofline.copy_GBs: a float4 copy of 256 MB reads as an HBM-class rate."""
+    gbs = fu.copy_bandwidth(0, 256 << 20, 3)
+    assert 1000.0 < gbs < 20000.0, gbs
+    with pytest.raises(fu.FuError, match="bad arguments"):
+        fu.copy_bandwidth(0, 8, 1)
+
+
+def test_lag_flows_every_round_and_switches():
+    """Kernel 9's lag (the multi-row heavy rows and the mega hubs leave f_r to round r + 2):
+    the flows read after every round (fu_get_flows writes the lagged ones first) and the
+    rounds that continue after each read, the option switched off and on mid-run, hub_multi
+    changed mid-run (the lagged set changes: its flows are written first), and fu_reset, all
+    bitwise against the C oracle."""
+    g = fu.Graph.rmat(14, 16, seed=8)
+    v = fu.uniform_values(g.n, seed=8)
+    eng = fu.CollectAll(g, v, kernel="pregather", hub_threshold=16, layout="given")
+    eng.set_option("mega_hub", 600)
+    eng.set_option("lag", 1)
+    eng.set_option("hub_multi", 1 << 30)
+    for r in range(1, 12):  # rounds 0 .. r-1 run: compare after each
+        eng.run(1)
+        a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, r, nthreads=16)
+        assert np.array_equal(eng.estimates(), a_ref), r
+        assert np.array_equal(eng.flows(), f_ref), r
+    eng.run(5)
+    eng.set_option("hub_multi", 2 * 600)  # hubs no longer lagged (some keep a block each)
+    eng.run(4)
+    eng.set_option("lag", 0)
+    eng.run(3)
+    eng.set_option("lag", 1)
+    eng.set_option("hub_multi", 1 << 30)
+    eng.run(7)
+    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 11 + 5 + 4 + 3 + 7, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    eng.reset()
+    eng.run(9)
+    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 9, nthreads=16)
+    assert np.array_equal(eng.flows(), f_ref) and np.array_equal(eng.estimates(), a_ref)
+
+
+def test_lag_with_autotune_kernel_switches():
+    """kernel "auto" with lag on: the autotune passes run kernel 9 (lagged) and then other
+    kernels, which read F as f_{r-2}: the lagged rows' flows are written before each switch.
+    200 rounds with packing every 4 rounds (re-tunes at every width), bitwise."""
+    g = fu.Graph.rmat(15, 16, seed=9)
+    v = fu.uniform_values(g.n, seed=9)
+    eng = fu.CollectAll(g, v, kernel="auto", hub_threshold=16, layout="degree")
+    eng.set_option("mega_hub", 2000)
+    eng.set_option("lag", 1)
+    eng.set_option("pack_every", 4)
+    eng.run(200)
+    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 200, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)

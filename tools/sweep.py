@@ -35,6 +35,10 @@ VARIANTS = {
     "pre_hubm16k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 16384}),
     "pre_hubm64k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 65536}),
     "pre_hubmall": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 1 << 30}),
+    "pre_lag": ("pregather", {"layout": "degree", "pack": 0, "lag": 1}),
+    "pre_hot": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240}),
+    "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1, "hub_multi": 1 << 30}),
+    "pre_lag_hubmall": ("pregather", {"layout": "degree", "pack": 0, "lag": 1, "hub_multi": 1 << 30}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
