@@ -216,12 +216,25 @@ int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl
                       fu_trace **out);
 /* Same, with route transfer times: route_s[src * n + dst] = seconds
  * a message from src to dst takes (SimGrid's LV08 model: 13.01 * sum(latency) +
- * size / (0.97 * min bandwidth), fu/platform.py; link sharing is not modelled). A message
+ * size / (0.97 * min bandwidth), fu/platform.py; no link sharing: fu_trace_build_links). A message
  * matched at tick t is consumed from tick t + floor(T) + 1 (t + 1 for T < 1 s, the only
  * case on the reference platform, CA:76). route_s NULL = every route under one tick. */
 int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                           int32_t mode, int32_t ticks, const char *order, const char *faults,
                           const double *route_s, fu_trace **out);
+/* Same, with link sharing (parity-unpinned against SimGrid): the
+ * platform's links (bandwidth B/s, latency s, shared = 0 for FATPIPE) and every route
+ * (route_links[route_off[src * n + dst] .. route_off[src * n + dst + 1]), n * n + 1 offsets;
+ * an empty route = same host). A message matched at tick t starts a transfer at time t:
+ * lat_factor * sum(latency) with no bandwidth, then msg_bytes at the max-min fair share of
+ * bw_factor * bandwidth on every shared link it crosses (capped by its FATPIPE links); it
+ * is consumed at the first tick after its end. Alone, a transfer takes the per-route time
+ * above (SimGrid LV08: lat_factor 13.01, bw_factor 0.97, 154-byte messages). */
+int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                         int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                         const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                         const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                         double lat_factor, double bw_factor, fu_trace **out);
 int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed);
 /* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
  * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */

@@ -192,6 +192,109 @@ class _Node:
         self.last_avg = 0.0
 
 
+class LinkNet:
+    """Link-sharing transfer model (fu_trace.cpp LinkNet), restated
+    operation for operation so both give the same doubles: a transfer matched at tick t has
+    a latency phase of lat_factor * sum(latency), then `bytes` at its max-min fair share of
+    bw_factor * bandwidth on the shared links it crosses, capped by its FATPIPE links.
+    Parity-unpinned against SimGrid (not installable offline)."""
+
+    def __init__(self, net):
+        self.n = int(net["n"])
+        self.bw = [float(x) for x in net["bw"]]
+        self.lat = [float(x) for x in net["lat"]]
+        self.shared = [int(x) for x in net["shared"]]
+        self.roff = [int(x) for x in net["route_off"]]
+        self.rl = [int(x) for x in net["route_links"]]
+        self.bytes = float(net.get("bytes", 154.0))
+        self.lat_factor = float(net.get("lat_factor", 13.01))
+        self.bw_factor = float(net.get("bw_factor", 0.97))
+        self.active = []  # flows (dicts) not done, in start order
+        self.now = 0.0
+
+    def links(self, f):
+        return self.rl[self.roff[f["r"]]:self.roff[f["r"] + 1]]
+
+    def start(self, src, dst, t):
+        r = src * self.n + dst
+        f = {"r": r, "rate": 0.0, "end": math.inf, "phase": 0, "rem": self.bytes}
+        lsum, cap = 0.0, math.inf
+        for k in self.links(f):
+            lsum = lsum + self.lat[k]
+            if not self.shared[k]:
+                cap = min(cap, self.bw_factor * self.bw[k])
+        f["lat_end"] = t + self.lat_factor * lsum
+        f["cap"] = cap
+        if self.roff[r] == self.roff[r + 1]:  # same host: no transfer
+            f["phase"], f["end"] = 2, t
+            return f
+        self.active.append(f)
+        return f
+
+    def _rates(self):
+        nl = len(self.bw)
+        crem = [self.bw_factor * self.bw[k] for k in range(nl)]
+        cnt = [0] * nl
+        un = [f for f in self.active if f["phase"] == 1]
+        for f in un:
+            for k in self.links(f):
+                if self.shared[k]:
+                    cnt[k] += 1
+        while un:
+            best = math.inf
+            for k in range(nl):
+                if cnt[k] > 0:
+                    best = min(best, max(0.0, crem[k] / cnt[k]))
+            for f in un:
+                best = min(best, f["cap"])
+            keep, fix = [], []
+            for f in un:
+                b = f["cap"] == best
+                for k in self.links(f):
+                    if b:
+                        break
+                    b = bool(self.shared[k]) and cnt[k] > 0 and max(0.0, crem[k] / cnt[k]) == best
+                (fix if b else keep).append(f)
+            for f in fix:
+                f["rate"] = best
+                for k in self.links(f):
+                    if self.shared[k]:
+                        crem[k] = crem[k] - best
+                        cnt[k] -= 1
+            un = keep
+
+    def advance_to(self, T):
+        while True:
+            self._rates()
+            nx = T
+            for f in self.active:
+                if f["phase"] == 0:
+                    nx = min(nx, f["lat_end"])
+                elif f["rate"] > 0.0:
+                    nx = min(nx, self.now + f["rem"] / f["rate"])
+            dt = nx - self.now
+            ev = False
+            keep = []
+            for f in self.active:
+                if f["phase"] == 1:
+                    if f["rate"] > 0.0 and self.now + f["rem"] / f["rate"] <= nx:
+                        f["phase"], f["end"] = 2, nx
+                        ev = True
+                        continue
+                    f["rem"] = f["rem"] - f["rate"] * dt
+                elif f["lat_end"] <= nx:
+                    f["phase"] = 1
+                    ev = True
+                    if not f["rem"] > 0.0:
+                        f["phase"], f["end"] = 2, nx
+                        continue
+                keep.append(f)
+            self.active = keep
+            self.now = nx
+            if not ev:
+                return
+
+
 class TickEmulator:
     """Pure-Python model of the reference run for small graphs.
 
@@ -199,7 +302,7 @@ class TickEmulator:
     mode: "ca" (collect-all) or "pw" (pairwise).
     """
 
-    def __init__(self, actors, mode: str, faults: str | None = None, route_s=None):
+    def __init__(self, actors, mode: str, faults: str | None = None, route_s=None, net=None):
         """faults: "drop=P,delay=D:Q,seed=S" (extension, not in the reference; same spec and
         draw order as fu_trace.cpp: one U[0,1) draw per put, in put order).
         route_s: optional n x n transfer times in seconds (sender row): a message matched at
@@ -207,6 +310,8 @@ class TickEmulator:
         every route, CA:76; the rule for longer routes is the extension fu_trace_build_routes
         implements, parity unpinned against SimGrid itself)."""
         self.route_s = route_s
+        # net: the link model (fu.platform.Platform.link_net; fu_trace_build_links) instead
+        self.net = LinkNet(net) if net is not None else None
         if mode not in ("ca", "pw"):
             raise ValueError(mode)
         self.p_drop, self.p_delay, self.d_ticks, self.fstate = 0.0, 0.0, 0, 0
@@ -256,6 +361,8 @@ class TickEmulator:
         c = self.comm[d]
         if c is not None and not c[0]:
             c[0], c[1], c[2] = True, msg, self.t
+            if self.net is not None:
+                c.append(self.net.start(self.idx[msg[0]], d, float(self.t)))
         else:
             self.fifo[d].append(msg)
 
@@ -349,6 +456,8 @@ class TickEmulator:
         tick = self._ca_tick if self.mode == "ca" else self._pw_tick
         n = len(self.nodes)
         for perm in tick_orders(n, order, ticks):
+            if self.net is not None:  # transfers ending before this tick are consumable
+                self.net.advance_to(float(self.t))
             for d, msg in self.delayed.pop(self.t, []):
                 self._arrive(d, msg)
             for i in perm:
@@ -356,10 +465,16 @@ class TickEmulator:
                 if c is None:  # CA:73-74
                     if self.fifo[i]:
                         c = [True, self.fifo[i].popleft(), self.t]
+                        if self.net is not None:
+                            c.append(self.net.start(self.idx[c[1][0]], i, float(self.t)))
                     else:
                         c = [False, None, -1]
                     self.comm[i] = c
-                if c[0] and c[2] + self._extra(c[1][0], i) < self.t:  # CA:76
+                if self.net is not None:
+                    arrived = c[0] and c[3]["phase"] == 2 and c[3]["end"] < self.t
+                else:
+                    arrived = c[0] and c[2] + self._extra(c[1][0], i) < self.t
+                if arrived:  # CA:76
                     msg = c[1]
                     self.comm[i] = None
                     self.events.append((self.t, i, 0, self.idx[msg[0]]))

@@ -33,6 +33,7 @@
 // same code.
 #include <cmath>
 #include <cstring>
+#include <limits>
 #include <unordered_map>
 
 #include "fu_common.h"
@@ -54,6 +55,138 @@ struct fu_trace {
 namespace {
 
 using namespace fu;
+
+// Transfers with link sharing (parity-unpinned against SimGrid, which
+// cannot run offline). A message matched at tick t (the rendez-vous, CA:74 / CA:124)
+// starts its transfer at time t: a latency phase of lat_factor * sum(route latencies) with
+// no bandwidth, then `bytes` at the rate max-min fair sharing gives it. A shared link l
+// offers bw_factor * bw_l to the transfers in their data phase that cross it, split by
+// progressive filling; a FATPIPE link caps each transfer at bw_factor * bw_l without
+// sharing. Rates change only when a transfer enters or leaves its data phase. Alone, a
+// transfer takes lat_factor * sum(lat) + bytes / (bw_factor * min bw), the fixed per-route
+// time of fu_trace_build_routes. The message is consumed at the first tick > its end
+// (CA:76: the actor tests the receive once per tick). oracle/oracle.py (LinkNet) mirrors
+// every operation in the same order, so both produce the same doubles.
+struct LinkNet {
+  int32_t n = 0, n_links = 0;
+  const double *bw = nullptr, *lat = nullptr;
+  const int32_t *shared = nullptr;
+  const int64_t *roff = nullptr;
+  const int32_t *rl = nullptr;
+  double bytes = 154.0, lat_factor = 13.01, bw_factor = 0.97;
+  struct Flow {
+    int64_t r;         // route index src * n + dst
+    double lat_end;    // end of the latency phase
+    double rem;        // bytes left (data phase)
+    double cap;        // FATPIPE cap (inf: none)
+    double rate;
+    double end;        // completion time (inf while running)
+    int phase;         // 0 latency, 1 data, 2 done
+  };
+  std::vector<Flow> fl;           // one per message id
+  std::vector<int32_t> active;    // message ids not done, in start order
+  double now = 0.0;
+
+  void start(int32_t id, int32_t src, int32_t dst, double t) {
+    if ((int32_t)fl.size() <= id) fl.resize(id + 1);
+    Flow &f = fl[id];
+    f.r = (int64_t)src * n + dst;
+    double l = 0.0, cap = std::numeric_limits<double>::infinity();
+    for (int64_t k = roff[f.r]; k < roff[f.r + 1]; ++k) {
+      l = l + lat[rl[k]];
+      if (!shared[rl[k]]) cap = std::min(cap, bw_factor * bw[rl[k]]);
+    }
+    f.lat_end = t + lat_factor * l;
+    f.rem = bytes;
+    f.cap = cap;
+    f.rate = 0.0;
+    f.end = std::numeric_limits<double>::infinity();
+    f.phase = 0;
+    if (roff[f.r] == roff[f.r + 1]) {  // same host: no transfer
+      f.phase = 2;
+      f.end = t;
+      return;
+    }
+    active.push_back(id);
+  }
+  // progressive filling over the data-phase transfers
+  void rates() {
+    std::vector<double> crem(n_links, 0.0);
+    std::vector<int32_t> cnt(n_links, 0);
+    std::vector<int32_t> un;
+    for (int32_t id : active) {
+      if (fl[id].phase != 1) continue;
+      un.push_back(id);
+      for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1]; ++k)
+        if (shared[rl[k]]) cnt[rl[k]]++;
+    }
+    for (int32_t l = 0; l < n_links; ++l) crem[l] = bw_factor * bw[l];
+    while (!un.empty()) {
+      double best = std::numeric_limits<double>::infinity();
+      for (int32_t l = 0; l < n_links; ++l)
+        if (cnt[l] > 0) best = std::min(best, std::max(0.0, crem[l] / cnt[l]));
+      for (int32_t id : un) best = std::min(best, fl[id].cap);
+      std::vector<int32_t> keep, fix;
+      for (int32_t id : un) {
+        bool b = fl[id].cap == best;
+        for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1] && !b; ++k) {
+          const int32_t l = rl[k];
+          b = shared[l] && cnt[l] > 0 && std::max(0.0, crem[l] / cnt[l]) == best;
+        }
+        (b ? fix : keep).push_back(id);
+      }
+      for (int32_t id : fix) {
+        fl[id].rate = best;
+        for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1]; ++k)
+          if (shared[rl[k]]) {
+            crem[rl[k]] = crem[rl[k]] - best;
+            cnt[rl[k]]--;
+          }
+      }
+      un.swap(keep);
+    }
+  }
+  // run the fluid model up to time T (every event at a time <= T is processed)
+  void advance_to(double T) {
+    for (;;) {
+      rates();
+      double nx = T;
+      for (int32_t id : active) {
+        const Flow &f = fl[id];
+        if (f.phase == 0) nx = std::min(nx, f.lat_end);
+        else if (f.rate > 0.0) nx = std::min(nx, now + f.rem / f.rate);
+      }
+      const double dt = nx - now;
+      bool ev = false;
+      std::vector<int32_t> keep;
+      for (int32_t id : active) {
+        Flow &f = fl[id];
+        if (f.phase == 1) {
+          if (f.rate > 0.0 && now + f.rem / f.rate <= nx) {
+            f.phase = 2;
+            f.end = nx;
+            ev = true;
+            continue;
+          }
+          f.rem = f.rem - f.rate * dt;
+        } else if (f.lat_end <= nx) {
+          f.phase = 1;
+          ev = true;
+          if (!(f.rem > 0.0)) {
+            f.phase = 2;
+            f.end = nx;
+            continue;
+          }
+        }
+        keep.push_back(id);
+      }
+      active.swap(keep);
+      now = nx;
+      if (!ev) return;  // nx == T with nothing due
+    }
+  }
+  bool done_before(int32_t id, double t) const { return fl[id].phase == 2 && fl[id].end < t; }
+};
 
 struct Builder {
   int32_t n;
@@ -82,6 +215,7 @@ struct Builder {
   std::vector<std::vector<std::pair<int32_t, int32_t>>> delayed;  // due tick -> (dst, id)
   // route transfer times (seconds, n x n, sender row), NULL = every route under one tick
   const double *route = nullptr;
+  LinkNet *net = nullptr;  // link sharing (fu_trace_build_links), else per-route times
 
   // whole ticks a transfer on src -> dst takes beyond the first: a message matched at tick t
   // completes at t + T and is consumed from tick t + floor(T) + 1 (t + 1 when T < 1, CA:76)
@@ -134,6 +268,7 @@ struct Builder {
       cstate[dst] = 2;
       cmsg[dst] = id;
       ctick[dst] = t;
+      if (net) net->start(id, msg_sender[id], dst, (double)t);
     } else {
       if (qtail[dst] < 0) qhead[dst] = id;
       else qnext[qtail[dst]] = id;
@@ -198,11 +333,13 @@ struct Builder {
         cstate[i] = 2;
         cmsg[i] = id;
         ctick[i] = t;
+        if (net) net->start(id, msg_sender[id], i, (double)t);
       } else {
         cstate[i] = 1;
       }
     }
-    if (cstate[i] == 2 && ctick[i] + extra(msg_sender[cmsg[i]], i) < t) {  // CA:76-82
+    if (cstate[i] == 2 && (net ? net->done_before(cmsg[i], (double)t)
+                               : ctick[i] + extra(msg_sender[cmsg[i]], i) < t)) {  // CA:76-82
       int32_t id = cmsg[i];
       cstate[i] = 0;
       int32_t s = slot_for(i, msg_sender[id]);
@@ -298,9 +435,54 @@ int fu_trace_build_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl
   return fu_trace_build_routes(n, decl_rowptr, decl_col, mode, ticks, order, faults, nullptr, out);
 }
 
+static int build_trace(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                       int32_t ticks, const char *order, const char *faults, const double *route_s, LinkNet *net,
+                       fu_trace **out);
+
 int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col,
                           int32_t mode, int32_t ticks, const char *order, const char *faults,
                           const double *route_s, fu_trace **out) {
+  return build_trace(n, decl_rowptr, decl_col, mode, ticks, order, faults, route_s, nullptr, out);
+}
+
+int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                         int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                         const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                         const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                         double lat_factor, double bw_factor, fu_trace **out) {
+  FU_TRY_BEGIN
+  if (n <= 0 || n_links < 0 || !route_off || (n_links > 0 && (!link_bw || !link_lat || !link_shared)) ||
+      !(msg_bytes >= 0.0) || !(lat_factor >= 0.0) || !(bw_factor > 0.0))
+    return fail(FU_ERR_ARG, "fu_trace_build_links: bad arguments");
+  const int64_t nr = (int64_t)n * n;
+  if (route_off[0] != 0) return fail(FU_ERR_ARG, "fu_trace_build_links: route_off[0] must be 0");
+  for (int64_t r = 0; r < nr; ++r) {
+    if (route_off[r + 1] < route_off[r]) return fail(FU_ERR_ARG, "fu_trace_build_links: route_off not ascending");
+    for (int64_t k = route_off[r]; k < route_off[r + 1]; ++k)
+      if (!route_links || route_links[k] < 0 || route_links[k] >= n_links)
+        return fail(FU_ERR_ARG, "fu_trace_build_links: route link out of range");
+  }
+  for (int32_t l = 0; l < n_links; ++l)
+    if (!(link_bw[l] > 0.0) || !(link_lat[l] >= 0.0))
+      return fail(FU_ERR_ARG, "fu_trace_build_links: link bandwidths must be > 0, latencies >= 0");
+  LinkNet net;
+  net.n = n;
+  net.n_links = n_links;
+  net.bw = link_bw;
+  net.lat = link_lat;
+  net.shared = link_shared;
+  net.roff = route_off;
+  net.rl = route_links;
+  net.bytes = msg_bytes;
+  net.lat_factor = lat_factor;
+  net.bw_factor = bw_factor;
+  return build_trace(n, decl_rowptr, decl_col, mode, ticks, order, faults, nullptr, &net, out);
+  FU_TRY_END
+}
+
+static int build_trace(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                       int32_t ticks, const char *order, const char *faults, const double *route_s, LinkNet *net,
+                       fu_trace **out) {
   FU_TRY_BEGIN
   if (!out || n <= 0 || !decl_rowptr || ticks < 0 || (mode != FU_MODE_COLLECTALL && mode != FU_MODE_PAIRWISE))
     return fail(FU_ERR_ARG, "fu_trace_build: bad arguments");
@@ -324,6 +506,7 @@ int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *
   B.delay_ticks = dticks;
   B.fstate = fseed;
   B.route = route_s;
+  B.net = net;
   B.nbrs.resize(n);
   for (int32_t i = 0; i < n; ++i) {
     for (int64_t k = decl_rowptr[i]; k < decl_rowptr[i + 1]; ++k) {
@@ -355,6 +538,7 @@ int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *
   tr->tick_task_off.push_back(0);
   for (int32_t t = 0; t < ticks; ++t) {
     B.t = t;
+    if (net) net->advance_to((double)t);  // transfers that end before tick t are consumable
     if (t < (int32_t)B.delayed.size()) {  // held-back messages reach their mailbox now
       for (auto &m : B.delayed[t]) B.arrive(m.first, m.second);
       B.delayed[t].clear();

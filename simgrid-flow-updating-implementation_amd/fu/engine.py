@@ -189,9 +189,11 @@ class Trace:
     """
 
     def __init__(self, decl_rowptr, decl_col, mode: str, ticks: int, order: str = "fwd",
-                 faults: str | None = None, route_s=None):
+                 faults: str | None = None, route_s=None, net=None):
         """route_s: optional n x n transfer times in seconds (sender row); a message matched at
-        tick t is consumed from tick t + floor(T) + 1 (fu_trace_build_routes)."""
+        tick t is consumed from tick t + floor(T) + 1 (fu_trace_build_routes).
+        net: optional link model (fu.platform.Platform.link_net): transfers share the
+        links' bandwidth (max-min fair, fu_trace_build_links); exclusive with route_s."""
         rp = np.ascontiguousarray(decl_rowptr, dtype=np.int64)
         c = np.ascontiguousarray(decl_col, dtype=np.int32)
         self.n = len(rp) - 1
@@ -205,9 +207,25 @@ class Trace:
             self._route = np.ascontiguousarray(route_s, dtype=np.float64)
             if self._route.shape != (self.n, self.n):
                 raise ValueError("route_s must be n x n")
-        L.call("fu_trace_build_routes", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
-               self.ticks, order.encode(), faults.encode() if faults else None,
-               None if self._route is None else L.ptr(self._route), ctypes.byref(out))
+        if net is not None:
+            if route_s is not None:
+                raise ValueError("route_s and net are exclusive")
+            self._net = {k: np.ascontiguousarray(net[k], dtype=dt) for k, dt in (
+                ("bw", np.float64), ("lat", np.float64), ("shared", np.int32),
+                ("route_off", np.int64), ("route_links", np.int32))}
+            if len(self._net["route_off"]) != self.n * self.n + 1:
+                raise ValueError("net['route_off'] must have n * n + 1 entries")
+            nl = len(self._net["bw"])
+            z = lambda a: L.ptr(a) if len(a) else None  # noqa: E731
+            L.call("fu_trace_build_links", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
+                   self.ticks, order.encode(), faults.encode() if faults else None, nl, z(self._net["bw"]),
+                   z(self._net["lat"]), z(self._net["shared"]), L.ptr(self._net["route_off"]),
+                   z(self._net["route_links"]), float(net.get("bytes", 154.0)),
+                   float(net.get("lat_factor", 13.01)), float(net.get("bw_factor", 0.97)), ctypes.byref(out))
+        else:
+            L.call("fu_trace_build_routes", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
+                   self.ticks, order.encode(), faults.encode() if faults else None,
+                   None if self._route is None else L.ptr(self._route), ctypes.byref(out))
         self._h = out
         self.faults = faults
         dr, dl = L.i64(), L.i64()

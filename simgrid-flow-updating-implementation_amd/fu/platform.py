@@ -54,6 +54,7 @@ class Platform:
     links: dict = field(default_factory=dict)   # id -> (bandwidth B/s, latency s)
     routes: dict = field(default_factory=dict)  # (src, dst) -> [link ids]
     routing: str = "Full"
+    fatpipe: set = field(default_factory=set)   # ids of sharing_policy="FATPIPE" links
 
     def add_host(self, name: str, speed="0f"):
         """Mirror of e.netzone_root.add_host (CA:159): hosts without routes, e.g. the observer."""
@@ -70,6 +71,31 @@ class Platform:
         bw = min(self.links[k][0] for k in links)
         return LV08_LATENCY_FACTOR * lat + size_bytes / (LV08_BANDWIDTH_FACTOR * bw)
 
+    def link_net(self, hosts, size_bytes: float = 154.0, pairs=None) -> dict:
+        """The link model of fu_trace_build_links for the actors on `hosts` (in actor order):
+        every link (bandwidth, latency, shared unless FATPIPE) and the route of every host
+        pair (empty for a host to itself). Concurrent transfers share the links' bandwidth
+        (max-min fair); alone, a transfer takes route_time. pairs: the (i, j) actor pairs
+        that exchange messages (None = all): only they need a route; the others stay empty."""
+        ids = sorted(self.links)
+        at = {k: q for q, k in enumerate(ids)}
+        n = len(hosts)
+        need = None if pairs is None else {(int(i), int(j)) for i, j in pairs}
+        off, lst = [0], []
+        for i, a in enumerate(hosts):
+            for j, b in enumerate(hosts):
+                if a != b and (need is None or (i, j) in need):
+                    if (a, b) not in self.routes:
+                        raise KeyError(f"no route {a} -> {b}")
+                    lst.extend(at[k] for k in self.routes[(a, b)])
+                off.append(len(lst))
+        return {"bw": np.array([self.links[k][0] for k in ids], dtype=np.float64),
+                "lat": np.array([self.links[k][1] for k in ids], dtype=np.float64),
+                "shared": np.array([0 if k in self.fatpipe else 1 for k in ids], dtype=np.int32),
+                "route_off": np.array(off, dtype=np.int64), "route_links": np.array(lst, dtype=np.int32),
+                "bytes": float(size_bytes), "lat_factor": LV08_LATENCY_FACTOR,
+                "bw_factor": LV08_BANDWIDTH_FACTOR, "n": n}
+
 
 def load_platform(path: str) -> Platform:
     root = ET.parse(path).getroot()
@@ -82,6 +108,8 @@ def load_platform(path: str) -> Platform:
     for ln in root.iter("link"):
         p.links[ln.get("id")] = (parse_bandwidth(ln.get("bandwidth", "0")),
                                  parse_time(ln.get("latency", "0")))
+        if ln.get("sharing_policy", "SHARED").upper() == "FATPIPE":
+            p.fatpipe.add(ln.get("id"))
     for r in root.iter("route"):
         src, dst = r.get("src"), r.get("dst")
         ids = [c.get("id") for c in r.findall("link_ctn")]

@@ -138,9 +138,9 @@ class Engine:
             return self._run_sync(cls, names, values, nbrs, t_end)
         n = len(names)
         decl_rp, decl_col = declared_csr(names, nbrs)
-        route_s = None
+        net = None
         if self.platform is not None and self.platform.routes:
-            route_s = self._route_matrix(names)
+            net = self._link_net(names, decl_rp, decl_col)
         if self.watcher is not None:
             w_end, w_int, w_host = self.watcher
             last_tick = int(min(w_end, t_end))
@@ -154,7 +154,7 @@ class Engine:
             ticks = int(np.ceil(t_end))
             snap_times = []
             w_host = None
-        trace = Trace(decl_rp, decl_col, cls.mode, ticks, self.order, route_s=route_s)
+        trace = Trace(decl_rp, decl_col, cls.mode, ticks, self.order, net=net)
         snap_ticks = sorted({int(t) for t in snap_times if int(t) < ticks})
         rep = Replay(trace, values, device=self.device)
         snaps = rep.run(ticks, snapshot_ticks=snap_ticks)
@@ -225,6 +225,17 @@ class Engine:
         return self.result
 
     # -- helpers ----------------------------------------------------------------------------
+    def _link_net(self, names, decl_rp, decl_col):
+        """The platform's links and the routes of every pair of actors that exchange messages
+        (declared neighbours, both directions: replies go back to the sender), for
+        fu_trace_build_links: concurrent transfers share link bandwidth (SimGrid LV08 factors,
+        fu/platform.py). On the reference platform every transfer ends within a tick, so the
+        schedule is the plain one (CA:76)."""
+        src = np.repeat(np.arange(len(names)), np.diff(decl_rp))
+        pairs = set(zip(src.tolist(), np.asarray(decl_col).tolist()))
+        pairs |= {(j, i) for i, j in pairs}
+        return self.platform.link_net(names, pairs=pairs)
+
     def _route_matrix(self, names):
         """Transfer time (s) of every host pair's route under SimGrid's LV08 model
         (fu/platform.py), or None when every route takes under one tick: then the schedule

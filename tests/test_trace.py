@@ -183,11 +183,137 @@ def test_route_times_match_emulator(mode, order):
         fu.Trace(rp, col, mode, 10, order, route_s=np.zeros((n, n + 1)))
 
 
+def _random_net(n, seed, slow):
+    """A random platform for the link model: 6-9 links (some FATPIPE), a route of 1-4
+    links for every ordered host pair. slow: bandwidths low enough (200 B/s - 2 kB/s) that
+    sharing moves deliveries by whole ticks."""
+    rng = np.random.default_rng(seed)
+    nl = int(rng.integers(6, 10))
+    bw = rng.uniform(60.0, 400.0, nl) if slow else rng.uniform(1e6, 1e9, nl)
+    lat = rng.uniform(0.0, 0.06 if slow else 0.015, nl)  # fast: 13.01 x 4 x 15 ms < 1 s
+    shared = (rng.uniform(size=nl) > 0.25).astype(np.int32)
+    off, lst = [0], []
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                lst.extend(rng.choice(nl, size=int(rng.integers(1, 5)), replace=False).tolist())
+            off.append(len(lst))
+    return {"n": n, "bw": bw, "lat": lat, "shared": shared, "route_off": np.array(off, dtype=np.int64),
+            "route_links": np.array(lst, dtype=np.int32), "bytes": 154.0, "lat_factor": 13.01,
+            "bw_factor": 0.97}
+
+
+@pytest.mark.parametrize("mode", ["collectall", "pairwise"])
+@pytest.mark.parametrize("order", ["fwd", "rand:5"])
+@pytest.mark.parametrize("seed", [1, 2])
+def test_link_sharing_matches_emulator(mode, order, seed):
+    """Link sharing (§8(f) row 3, fu_trace_build_links): concurrent transfers split the
+    shared links' bandwidth max-min fairly (FATPIPE links cap each transfer alone), so a
+    message's delivery tick depends on the traffic beside it. The native builder and the
+    oracle emulator (LinkNet, the same operations in the same order) agree event for event
+    and snapshot for snapshot over 2000 ticks, with fault injection on the asymmetric
+    12-node fixture. Parity-unpinned against SimGrid itself (not installable offline)."""
+    d = load_json("tick_asym12_ca_fwd.json") if seed == 2 else load_json("tick_small_platform_ca_fwd.json")
+    names, vals, rp, col = fixture_decl_csr(d)
+    n = len(names)
+    net = _random_net(n, seed, slow=True)
+    faults = "drop=0.05,delay=3:0.05,seed=4" if seed == 2 else None
+    em = oracle.TickEmulator(d["actors"], "ca" if mode == "collectall" else "pw", faults=faults, net=net)
+    snaps = {}
+
+    def cb(t, e):
+        if t % 100 == 0 or t == 1999:
+            snaps[t] = dict(e.last_avg_items())
+
+    em.run(2000, order, on_tick=cb)
+    tr = fu.Trace(rp, col, mode, 2000, order, faults=faults, net=net)
+    a = tr.arrays()
+    assert trace_events_as_log(a) == [list(x) for x in em.events]
+    ticks = sorted(snaps)
+    _, _, _, s2 = coracle.replay(a["rowptr"], vals, a["tick_task_off"], a["tasks"], a["events"], a["out_ids"],
+                                 tr.n_msgs, ticks)
+    for t in ticks:
+        for i, v in snaps[t].items():
+            assert s2[t][i] == v
+    # sharing matters here: the same links without it (each transfer alone, its route time)
+    # give another schedule
+    rt = np.zeros((n, n))
+    for i in range(n):
+        for j in range(n):
+            if i != j:
+                ks = net["route_links"][net["route_off"][i * n + j]:net["route_off"][i * n + j + 1]]
+                rt[i, j] = 13.01 * sum(net["lat"][k] for k in ks) + 154.0 / (0.97 * min(net["bw"][k] for k in ks))
+    alone = fu.Trace(rp, col, mode, 2000, order, faults=faults, route_s=rt).arrays()
+    assert not (np.array_equal(alone["tick_task_off"], a["tick_task_off"])
+                and np.array_equal(alone["events"], a["events"]))
+
+
+@pytest.mark.parametrize("mode", ["collectall", "pairwise"])
+def test_link_model_fast_links_give_the_plain_schedule(mode, tmp_path):
+    """Links fast enough that every transfer ends within a tick (the reference platform:
+    PLAT:13-36) give exactly the plain schedule, and the reference platform itself does too."""
+    from conftest import write_platform_xml
+
+    d = load_json("tick_small_platform_ca_fwd.json")
+    names, vals, rp, col = fixture_decl_csr(d)
+    n = len(names)
+    plain = fu.Trace(rp, col, mode, 800, "rand:2").arrays()
+    for net in (_random_net(n, 9, slow=False), None):
+        if net is None:
+            plat = tmp_path / "small_platform.xml"
+            write_platform_xml(plat)
+            net = fu.platform.load_platform(str(plat)).link_net(names)
+        got = fu.Trace(rp, col, mode, 800, "rand:2", net=net).arrays()
+        for k in ("tick_task_off", "tasks", "events", "out_ids"):
+            assert np.array_equal(got[k], plain[k])
+
+
+def test_link_model_single_transfer_time_and_sharing():
+    """One transfer alone takes the per-route LV08 time; two at once on one shared link take
+    longer each, a FATPIPE link does not slow them down. Checked on the emulator's LinkNet
+    (the native builder equals it event for event, test above)."""
+    net = {"n": 3, "bw": np.array([100.0, 100.0]), "lat": np.array([0.01, 0.0]), "shared": np.array([1, 0]),
+           "route_off": np.array([0, 0, 1, 2, 3, 3, 4, 5, 6, 6]), "route_links": np.array([0, 0, 0, 1, 1, 1]),
+           "bytes": 154.0, "lat_factor": 13.01, "bw_factor": 0.97}
+    ln = oracle.LinkNet(net)
+    f = ln.start(0, 1, 0.0)
+    ln.advance_to(10.0)
+    assert f["end"] == pytest.approx(13.01 * 0.01 + 154.0 / 97.0)
+    ln = oracle.LinkNet(net)
+    f1, f2 = ln.start(0, 1, 0.0), ln.start(1, 0, 0.0)  # both on shared link 0
+    ln.advance_to(10.0)
+    assert f1["end"] == f2["end"] == pytest.approx(13.01 * 0.01 + 2 * 154.0 / 97.0)
+    ln = oracle.LinkNet(net)
+    f1, f2 = ln.start(1, 2, 0.0), ln.start(2, 1, 0.0)  # both on FATPIPE link 1
+    ln.advance_to(10.0)
+    assert f1["end"] == f2["end"] == pytest.approx(154.0 / 97.0)
+
+
+def test_link_model_argument_checks():
+    d = load_json("tick_small_platform_ca_fwd.json")
+    names, vals, rp, col = fixture_decl_csr(d)
+    n = len(names)
+    net = _random_net(n, 3, slow=True)
+    bad = dict(net, route_off=net["route_off"][:-1])
+    with pytest.raises(ValueError):
+        fu.Trace(rp, col, "pairwise", 10, net=bad)
+    bad = dict(net, route_links=np.full_like(net["route_links"], 99))
+    with pytest.raises(fu.FuError, match="out of range"):
+        fu.Trace(rp, col, "pairwise", 10, net=bad)
+    bad = dict(net, bw=np.zeros_like(net["bw"]))
+    with pytest.raises(fu.FuError, match="bandwidths"):
+        fu.Trace(rp, col, "pairwise", 10, net=bad)
+    with pytest.raises(ValueError, match="exclusive"):
+        fu.Trace(rp, col, "pairwise", 10, net=net, route_s=np.zeros((n, n)))
+
+
 @pytest.mark.gpu
 def test_engine_runs_a_slow_platform(tmp_path):
     """A platform whose routes need more than one tick (LV08: 13.01 x 100 ms + 154 B / (0.97
-    x 1 kB/s) = 1.46 s) is simulated with route times instead of being rejected: the drop-in
-    Engine's replay equals the oracle emulator with the same route matrix, and converges."""
+    x 1 kB/s) = 1.46 s alone) is simulated instead of being rejected: every route crosses the
+    one shared link, so concurrent transfers split its bandwidth (link model,
+    fu_trace_build_links). The drop-in Engine's replay equals the oracle emulator with the
+    same link model bit for bit, and converges."""
     import io
 
     from conftest import write_deployment_xml
@@ -209,13 +335,11 @@ def test_engine_runs_a_slow_platform(tmp_path):
     p = fu.platform.load_platform(str(plat))
     T = p.route_time(hosts[0], hosts[1])
     assert 1.0 < T < 2.0
-    n = len(hosts)
-    route = np.full((n, n), T)
-    np.fill_diagonal(route, 0.0)
+    net = p.link_net(hosts)  # one shared link: concurrent transfers split its 1 kB/s
     for mode, m in (("collectall", "ca"), ("pairwise", "pw")):
         e, res = fu.run_reference_main(mode, str(plat), str(dep), 1000.0, 10.0, order="fwd",
                                        out=io.StringIO())
-        em = oracle.TickEmulator(d["actors"], m, route_s=route)
+        em = oracle.TickEmulator(d["actors"], m, net=net)
         em.run(1001, "fwd")
         want = dict(em.last_avg_items())
         for i, v in want.items():
