@@ -418,18 +418,9 @@ constexpr int kHeavyRL = FU_HEAVY_RL;
 // other heavy rows can afford (R-MAT-24: 19 % of the edges sit in rows of 641-1024)
 constexpr int kMidRL = 16;
 
-// DIAG (timing-only builds selected by fu_set_option("diag", k); results are WRONG):
-//   1 = the a_{r-1}[col e] gather replaced by a coalesced read (prices the gather);
-//   2 = no flow load/store (prices the flow stream);
-//   3 / 4 = the gather folded into the first n/2 / n/4 estimates (prices a smaller table);
-//   5 = hub chains skipped (prices the exact sequential hub sums);
-//   6 = the flow pass of multi-chunk heavy rows skips its estimate gathers;
-//   12 = 1 and 2 together (prices col + the per-node arrays alone);
-//   kernel 9 only: 20 = staging passes alone, 21 = round tiles alone, 22 = no hub path,
-//   23 = no k_stage, 24 = no k_transpose.
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
-template <bool CHECK, bool NT, int DIAG = 0, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
+template <bool CHECK, bool NT, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
           bool PRE = false, int HRL = kHeavyRL, bool RF = true>
 __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
@@ -502,7 +493,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
             }
             wave_sync();
             // the register-resident mid launch: 8-element batches (its rows hold 64 VGPRs)
-            if (DIAG != 5) chain_sum<(HRL > kHeavyRL ? 8 : FU_CHAIN_B)>(xs, es, min(CH, d - c * CH), S, T);
+            chain_sum<(HRL > kHeavyRL ? 8 : FU_CHAIN_B)>(xs, es, min(CH, d - c * CH), S, T);
           }
         }
         const double a = ((v[i] - S) + T) / (double)(d + 1);
@@ -546,7 +537,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
           es[lane + 64 * u] = er[u];
         }
         wave_sync();
-        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+        chain_sum(xs, es, min(CH, d - c0), S, T);
       }
       const double a = ((v[i] - S) + T) / (double)(d + 1);
       if (lane == 0) {
@@ -567,7 +558,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
         if constexpr (!PRE) {
 #pragma unroll
           for (int u = 0; u < 8; ++u)
-            er[u] = k0 + lane + 64 * u < d ? (DIAG == 6 ? 0.0 : ld_est(pp, code_prev, a_prev, cc[u])) : 0.0;
+            er[u] = k0 + lane + 64 * u < d ? ld_est(pp, code_prev, a_prev, cc[u]) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
@@ -618,7 +609,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
           ng[u] = k < d ? Gb[b + k] : 0.0;
         }
         wave_sync();
-        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+        chain_sum(xs, es, min(CH, d - c0), S, T);
         wave_sync();
       }
     } else if (!PRE && t < 64) {
@@ -639,7 +630,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
           nx[u] = k < d ? xy[k] : make_double2(0.0, 0.0);
         }
         wave_sync();
-        if (DIAG != 5) chain_sum(xs, es, min(CH, d - c0), S, T);
+        chain_sum(xs, es, min(CH, d - c0), S, T);
         wave_sync();
       }
     }
@@ -686,7 +677,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     for (int c = 0; c < nch; ++c) {
       if (t >= 64) {
         if (c + 1 < nch) stage(c + 1, t - 64, kBlock - 64);
-      } else if (DIAG != 5) {
+      } else {
         chain_sum(s_x + (c & 1) * CH, s_er + (c & 1) * CH, min(CH, e - (b + c * CH)), S, T);
       }
       __syncthreads();
@@ -769,7 +760,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
-      if constexpr (RF && DIAG != 2 && DIAG != 12) {
+      if constexpr (RF) {
         const double f = ld_f(F, q < ne ? e0 + q : 0);
         x[k] = q < ne ? f : 0.0;
       } else {
@@ -790,15 +781,11 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     for (int k = 0; k < kPer; ++k) c[k] = t + k * kBlock < ne ? bs[k] + cw[k] - 32768 : 0;
   }
   if (PRE) {
-  } else if (DIAG != 0 || pp.width == 0) {
+  } else if (pp.width == 0) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
-      g[k] = 0.0;
-      if (q < ne) {
-        const int gi = (DIAG == 1 || DIAG == 12) ? nb + (q % (nn + 1)) : DIAG == 3 ? (c[k] >> 1) : DIAG == 4 ? (c[k] >> 2) : c[k];
-        g[k] = a_prev[gi];
-      }
+      g[k] = q < ne ? a_prev[c[k]] : 0.0;
     }
   } else if (pp.width == 8) {
     gather_packed<8>(c, g, t, ne, code_prev, pp.base, a_prev);
@@ -845,12 +832,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
   for (int k = 0; k < kPer; ++k) {
     const int q = t + k * kBlock;
     if (q < ne) {
-      const double fnew = (s_x[q] + s_a[s_own[q]]) - s_er[q];
-      if (DIAG == 2 || DIAG == 12) {
-        if (fnew == 12345.678) st_f_full(F, e0 + q, fnew);  // keep the value live, store ~never
-      } else {
-        st_fo(F, e0 + q, fnew, x[k], fm);
-      }
+      st_fo(F, e0 + q, (s_x[q] + s_a[s_own[q]]) - s_er[q], x[k], fm);
     }
   }
   if (CHECK) block_max_to(eb, err);
@@ -1374,10 +1356,7 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   }
 }
 
-// DIAG (timing only, wrong results): 1 = G read at the edge's own index (prices the runs),
-// 2 = no stage launch and G read as in 1 (prices the round without staging), 3 = 2 without
-// the XCD tile order; 4 = no stage launch, G read as usual (prices the round launch alone).
-template <bool CHECK, int TE, int TN, int DIAG = 0, bool RF = true, bool LO = true>
+template <bool CHECK, int TE, int TN, bool RF = true, bool LO = true>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
     const int4 *__restrict__ tiles, int t0, int ntl,
     const int *__restrict__ rowptr, const int *__restrict__ col,
@@ -1402,7 +1381,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   // XCD-aware order: block b runs on XCD b % 8; consecutive tiles go to the same XCD, so
   // the G runs that neighbouring tiles share in every slice region meet in one L2
   const int xcd = blockIdx.x & 7, per = ntl >> 3, rem = ntl & 7;
-  const int tile = t0 + (DIAG == 3 ? (int)blockIdx.x : xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3));
+  const int tile = t0 + xcd * per + min(xcd, rem) + (int)(blockIdx.x >> 3);
   const int4 tl = tiles[tile];
   const int nb = tl.x, nn = tl.y - tl.x;
   const int e0 = tl.z, ne = tl.w - tl.z;
@@ -1452,7 +1431,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
       const int q = t + k * kBlock;
       const int dd = __shfl(dl, (int)(c16[k] >> 10));
       si[k] = c16[k] & 1023u;
-      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : q + dd) : -1;
+      gi[k] = q < ne ? q + dd : -1;
     }
   }
   } else {  // the round-1 order: indices and flows interleaved (measured against LO)
@@ -1470,7 +1449,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
       const int q = t + k * kBlock;
       const int dd = __shfl(dl, (int)(c16[k] >> 10));
       si[k] = c16[k] & 1023u;
-      gi[k] = q < ne ? ((DIAG >= 1 && DIAG <= 3) ? e0 + q : q + dd) : -1;
+      gi[k] = q < ne ? q + dd : -1;
     }
   }
   rp = t <= nn ? rowptr[nb + t] : 0;
@@ -2376,9 +2355,6 @@ struct fu_handle {
   bool pw_pending = false;
   int *pw_dev = nullptr;      // h_pw as the device sees it (the plan kernels write the width there)
   bool plan_pending = false;  // a packing plan is due before the next round (from its table)
-  // timing-only ablations (-DFU_DIAG builds: fu_set_option("diag", k); wrong results): the
-  // round body launch_body<k>; null = the product path
-  int (*diag_body)(fu_handle *, RoundCtx &) = nullptr;
   std::vector<int64_t> h_rowptr;
   std::vector<int32_t> h_col;
   // kernel 4 tiles per geometry (all four built up front so autotuning can switch between
@@ -3017,29 +2993,26 @@ int launch_round0(fu_handle *h, RoundCtx &c) {
 }
 
 // Kernel 8: k_stage (carrying the packing plan), heavy rows as kernel 4 tiles, then the light
-// tiles reading the staged estimates. D: timing-only ablations (FU_DIAG builds; 0 = product):
-// 1 = G read at the edge's own index, 2 = 1 without k_stage, 3 = 2 without the XCD tile
-// order, 4 = no k_stage, G read as usual.
-template <int D>
+// tiles reading the staged estimates.
 int launch_k8(fu_handle *h, RoundCtx &c) {
   constexpr bool C0 = false;
   const int r1 = (int)(c.r & 1);
   unsigned sgrid = 1;
   const StageArgs sa = stage_args(h, &sgrid);
   const void *cp = h->code[(c.r - 1) & 1];
-  if (h->st_ntiles && D < 2) {
+  if (h->st_ntiles) {
     hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap, cp,
                        h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
   plan_alone(h, c);
   auto heavy = [&](auto chk) {
-    hipLaunchKernelGGL((k_round_recon<decltype(chk)::value, false, 0, kStageTE, kStageTN>), dim3(h->st_nheavy),
+    hipLaunchKernelGGL((k_round_recon<decltype(chk)::value, false, kStageTE, kStageTN>), dim3(h->st_nheavy),
                        dim3(kBlock), 0, h->stream, h->st_heavy, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
                        h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr, c.fm);
   };
   if (h->st_nheavy) {
-    if (c.err && !D) heavy(std::true_type{});
+    if (c.err) heavy(std::true_type{});
     else heavy(std::false_type{});
   }
   // light tiles: rounds 1 and 2 (fm) read no flows (RF = false); LO = staged indices first
@@ -3050,7 +3023,7 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
     for (int part = 0; part < 2; ++part) {
       const int t0 = part ? nb : 0, cnt = part ? h->st_ntiles - nb : nb;
       if (cnt)
-        hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, D, decltype(rf)::value,
+        hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, decltype(rf)::value,
                                            decltype(lo)::value>),
                            dim3(cnt), dim3(kBlock), 0, h->stream, h->st_tiles, t0, cnt, h->rowptr, h->col, sa,
                            h->stG, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
@@ -3068,7 +3041,7 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
     return c.fm ? light_lo(chk, std::false_type{}) : light_lo(chk, std::true_type{});
   };
   if (h->st_ntiles || h->dist) {
-    if (c.err && !D) return light_rf(std::true_type{});
+    if (c.err) return light_rf(std::true_type{});
     return light_rf(std::integral_constant<bool, C0>{});
   }
   return FU_OK;
@@ -3076,10 +3049,7 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
 
 // Kernel 9: k_stage -> k_transpose (the mega-hub buckets first) -> kernel 4's tiles reading
 // the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
-// the remaining buckets and tiles. D (FU_DIAG builds): 5 = hub chains skipped, 6 = the flow
-// pass of multi-chunk heavy rows skips its estimate reads, 20 = the staging passes alone,
-// 21 = the round tiles alone, 22 = no hub path, 23 = no k_stage, 24 = no k_transpose.
-template <int D>
+// the remaining buckets and tiles.
 int launch_k9(fu_handle *h, RoundCtx &c) {
   if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
   double *Gb = h->tr.GBr[c.r % 3];
@@ -3092,7 +3062,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
   const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
   const int4 *tl = h->tiles_geo[1];
-  const bool hubs = nmega && D != 22;
+  const bool hubs = nmega > 0;
   StageArgs sa{};
   for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
   sa.P[3] = h->tr.P;
@@ -3102,7 +3072,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   sa.brange[3] = h->tr.brange;
   sa.colS[3] = h->tr.colS;
   sa.f64 = 1;
-  if (D != 21 && D != 23) {
+  {
     hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap,
                        cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
@@ -3119,9 +3089,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
   const int mend = h->multi_mid ? m1 : m0_;
   const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
-  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && D == 0 && n_multi > 0;
+  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
   const bool lag_multi = h->lag && multi;
-  const bool lag_hub = h->lag && hubs && h->hub_multi && nbig == 0 && D == 0;
+  const bool lag_hub = h->lag && hubs && h->hub_multi && nbig == 0;
   const int p = r1;
   if (h->lagf[p] && (h->lag_nmulti[p] != (lag_multi ? n_multi : 0) || h->lag_hubs[p] != (int)lag_hub)) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
@@ -3139,13 +3109,13 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       hipLaunchKernelGGL(k_transpose<false>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
   };
-  if (D != 21 && D != 24 && bh) tr_launch(0, bh);
+  if (bh) tr_launch(0, bh);
   if (hubs) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
-  if (D != 21 && D != 24 && h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
-  const bool chk = c.err && !D;
+  if (h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
+  const bool chk = c.err != nullptr;
   if (hubs) {
     auto chains = [&](auto C) {
       // hub_multi: the hubs of <= hub_multi edges as k_heavy_multi blocks (kMR hubs of similar
@@ -3163,7 +3133,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
         else hm(std::integral_constant<int, 2>{});
       }
       if (nbig)
-        hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
+        hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
                            0, h->stream2, h->hub_multi ? h->hub_tiles_sorted : tl, h->rowptr, h->col, h->v, c.F, c.ap,
                            c.ap2, c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1,
                            Gb, c.fm);
@@ -3176,11 +3146,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
   }
-  // heavy tiles [t0, t1) with RL register elements per lane; DH = the heavy-row ablation
-  constexpr int DH = (D == 5 || D == 6) ? D : 0;
+  // heavy tiles [t0, t1) with RL register elements per lane
   auto heavy = [&](auto C, auto RL, int t0, int t1) {
     if (t1 > t0)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, DH, 1024, 128, 2, true, decltype(RL)::value>),
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, decltype(RL)::value>),
                          dim3(t1 - t0), dim3(kBlock), 0, h->stream, tl + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                          c.fm);
@@ -3207,14 +3176,12 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     }
     heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
     if (nl)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 0, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
   };
-  if (D != 20) {
-    if (chk) tiles(std::true_type{});
-    else tiles(std::false_type{});
-  }
+  if (chk) tiles(std::true_type{});
+  else tiles(std::false_type{});
   HIP_TRY(hipGetLastError());
   if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
@@ -3229,11 +3196,8 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
 // Kernel 4: heavy tiles (mega hubs, heavy rows) lead the tile list; with fork_heavy they run
 // on the side stream beside the light tiles' launch (which keeps kernel 4's light-path
 // register budget). Multi-GPU: the heavy tiles stay on the main stream, then the boundary
-// light tiles, then the halo goes out beside the interior light tiles. D (FU_DIAG builds):
-// 1 = the gather replaced by a coalesced read, 2 = no flow load/store, 3 / 4 = the gather
-// folded into n/2 / n/4 estimates, 5 = hub chains skipped, 6 = the heavy flow pass without
-// its gathers, 12 = 1 and 2.
-template <int TE, int TN, int D>
+// light tiles, then the halo goes out beside the interior light tiles.
+template <int TE, int TN>
 int launch_k4_geo(fu_handle *h, RoundCtx &c) {
   const int r1 = (int)(c.r & 1);
   const void *cp = h->code[(c.r - 1) & 1];
@@ -3253,17 +3217,16 @@ int launch_k4_geo(fu_handle *h, RoundCtx &c) {
   if (h->n_hub)
     hipLaunchKernelGGL(k_hub_stage, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
                        (long long)h->hub_total, h->col, c.F, c.ap, c.ap2, cp, h->pctl, r1, h->hubxy, c.fm, h->hub_blk);
-  constexpr int DH = (D == 5 || D == 6) ? D : 0;
   auto heavy = [&](auto C, hipStream_t st, int t0, int cnt) {
     if (cnt)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, DH, TE, TN, 2>), dim3(cnt), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, TE, TN, 2>), dim3(cnt), dim3(kBlock), 0, st,
                          tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp, h->code[r1],
                          h->pctl, r1, h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, c.fm);
   };
   // light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
   auto light = [&](auto C, auto NT, auto RF, int t0, int cnt) {
     if (cnt)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, decltype(NT)::value, D, TE, TN, 1, false, kHeavyRL,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, decltype(NT)::value, TE, TN, 1, false, kHeavyRL,
                                         decltype(RF)::value>),
                          dim3(cnt), dim3(kBlock), 0, h->stream, tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr,
@@ -3285,8 +3248,7 @@ int launch_k4_geo(fu_handle *h, RoundCtx &c) {
     return FU_OK;
   };
   int rc;
-  if (D) rc = body(std::false_type{}, std::false_type{});
-  else if (c.err) rc = h->nt ? body(std::true_type{}, std::true_type{}) : body(std::true_type{}, std::false_type{});
+  if (c.err) rc = h->nt ? body(std::true_type{}, std::true_type{}) : body(std::true_type{}, std::false_type{});
   else rc = h->nt ? body(std::false_type{}, std::true_type{}) : body(std::false_type{}, std::false_type{});
   if (rc) return rc;
   if (hub_sep)
@@ -3300,43 +3262,20 @@ int launch_k4_geo(fu_handle *h, RoundCtx &c) {
   return FU_OK;
 }
 
-template <int D>
 int launch_k4(fu_handle *h, RoundCtx &c) {
   plan_alone(h, c);
-  if (h->geo == 0) return launch_k4_geo<2048, 256, D>(h, c);
-  if (h->geo == 2) return launch_k4_geo<1024, 256, D>(h, c);
-  if (h->geo == 1) return launch_k4_geo<1024, 128, D>(h, c);
-  return launch_k4_geo<512, 64, D>(h, c);
+  if (h->geo == 0) return launch_k4_geo<2048, 256>(h, c);
+  if (h->geo == 2) return launch_k4_geo<1024, 256>(h, c);
+  if (h->geo == 1) return launch_k4_geo<1024, 128>(h, c);
+  return launch_k4_geo<512, 64>(h, c);
 }
 
-// The round body of rounds >= 1 for the handle's kernel (D = 0: the product path).
-template <int D>
+// The round body of rounds >= 1 for the handle's kernel.
 int launch_body(fu_handle *h, RoundCtx &c) {
-  if (h->kernel == 8) return launch_k8<D>(h, c);
-  if (h->kernel == 9) return launch_k9<D>(h, c);
-  return launch_k4<D>(h, c);
+  if (h->kernel == 8) return launch_k8(h, c);
+  if (h->kernel == 9) return launch_k9(h, c);
+  return launch_k4(h, c);
 }
-
-#ifdef FU_DIAG
-// -DFU_DIAG builds: fu_set_option("diag", k) selects launch_body<k> (timing only, WRONG results)
-int (*diag_body(int k))(fu_handle *, RoundCtx &) {
-  switch (k) {
-    case 1: return launch_body<1>;
-    case 2: return launch_body<2>;
-    case 3: return launch_body<3>;
-    case 4: return launch_body<4>;
-    case 5: return launch_body<5>;
-    case 6: return launch_body<6>;
-    case 12: return launch_body<12>;
-    case 20: return launch_body<20>;
-    case 21: return launch_body<21>;
-    case 22: return launch_body<22>;
-    case 23: return launch_body<23>;
-    case 24: return launch_body<24>;
-    default: return nullptr;
-  }
-}
-#endif
 
 // One round: state of round r-1 -> round r. err_slot: nullptr = no check.
 int launch_round(fu_handle *h, unsigned long long *err_slot) {
@@ -3366,8 +3305,7 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
     if (int rc2 = lag_finalize(h, (int)(r & 1))) return rc2;
   }
   if (r == 0) rc = launch_round0(h, c);
-  else if (h->diag_body) rc = h->diag_body(h, c);
-  else rc = launch_body<0>(h, c);
+  else rc = launch_body(h, c);
   if (rc) return rc;
   HIP_TRY(hipGetLastError());
   if (plan_done && !h->pw_pending) {  // the autotuner watches the width (poll_pack_width)
@@ -3625,16 +3563,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     if (value < -1 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: stage_layout must be -1..3");
     h->st_force = (int)value;
     return FU_OK;
-  }
-  if (!std::strcmp(key, "diag")) {  // timing-only ablations (wrong results): tools builds only
-#ifdef FU_DIAG
-    if (value && !diag_body((int)value)) return fail(FU_ERR_ARG, "fu_set_option: unknown diag");
-    h->diag_body = value ? diag_body((int)value) : nullptr;
-    return FU_OK;
-#else
-    (void)value;
-    return fail(FU_ERR_ARG, "fu_set_option: 'diag' exists only in a -DFU_DIAG build (make DIAG=1)");
-#endif
   }
   if (!std::strcmp(key, "nt")) {
     h->nt = value != 0;

@@ -30,7 +30,6 @@ for s in $STEPS; do
                  i=$((i+1))
                  step "sweep_${i}_$lib" 600 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so python tools/sweep.py ${SWEEP_ARGS:-}
                done ;;
-    sweepdiag) step sweepdiag 900 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/libfu_diag.so python tools/sweep.py ${SWEEP_ARGS:-} ;;
     replay) step replay 400 python tools/bench_replay.py ;;
     replaylibs) for lib in ${REPLAY_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...)
                   step "replay_$lib" 400 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so TICKS=1000 python tools/bench_replay.py

@@ -18,12 +18,27 @@ ap.add_argument("--rounds", type=int, default=1000)
 ap.add_argument("--nt", type=int, default=-1)
 ap.add_argument("--pack", type=int, default=1)
 ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1024/512); 0 = default")
-ap.add_argument("--diag", type=int, default=0)
 ap.add_argument("--layout", default="given")
 ap.add_argument("--opt", action="append", default=[], help="extra engine option key=value (repeatable)")
 ap.add_argument("--pairwise", default="", help="WARMUP:STEPS: bench.py's pairwise window instead (RR-64K "
                 "tick replay: ticks 0..51+WARMUP in one launch, then the STEPS timed ticks in a second)")
+ap.add_argument("--dist-rgg", type=int, default=0, help="N: bench.py's rgg-dist window instead (RGG of N "
+                "nodes through the partitioned path at one RCCL rank, kernel auto: tune, --warm rounds, "
+                "reset, --rounds rounds)")
 a = ap.parse_args()
+if a.dist_rgg:
+    from fu.dist import DistCollectAll, RggPart, unique_id
+
+    part = RggPart(a.dist_rgg, avg_deg=8.0, seed=1, nparts=1, part=0)
+    eng = DistCollectAll(part.to_plan(), part.values(seed=0), unique_id(), kernel=a.kernel)
+    if a.kernel == "auto":
+        eng.tune()
+    eng.run(a.warm)
+    eng.reset()
+    eng.run(a.rounds)
+    eng.synchronize()
+    print("rgg-dist", part.n_local, part.e_local, "info", eng.info())
+    sys.exit(0)
 if a.pairwise:
     warm, steps = (int(x) for x in a.pairwise.split(":"))
     g = fu.Graph.random_regular(65536, 8, seed=1)
@@ -50,8 +65,6 @@ if a.kernel == "auto":
     eng.tune()  # as bench.py: one untimed autotune pass
 eng.run(a.warm)
 eng.reset()
-if a.diag:
-    eng.set_option("diag", a.diag)  # needs FU_LIBRARY=.../libfu_diag.so
 eng.run(a.rounds)
 eng.synchronize()
 print("n", g.n, "E", g.E, "alg_bytes", 24 * g.E + 28 * g.n, "info", eng.info(), "pack", eng.pack_widths())

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Kernel-variant sweep: device time per round for each round-kernel variant, interleaved
-in one process (cdna guide §5.4 rule 24). Variants named diag* are timing-only ablations
-with WRONG results (they price one memory stream each).
+in one process (cdna guide §5.4 rule 24).
 
     python tools/sweep.py [spec ...] [--variants a,b,c]
 """
@@ -52,13 +51,6 @@ VARIANTS = {
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
     "pre_mega64k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 65536}),
-    "pre_d20": ("pregather", {"layout": "degree", "pack": 0, "diag": 20}),
-    "pre_d21": ("pregather", {"layout": "degree", "pack": 0, "diag": 21}),
-    "pre_d22": ("pregather", {"layout": "degree", "pack": 0, "diag": 22}),
-    "pre_d23": ("pregather", {"layout": "degree", "pack": 0, "diag": 23}),
-    "pre_d24": ("pregather", {"layout": "degree", "pack": 0, "diag": 24}),
-    "pre_d5": ("pregather", {"layout": "degree", "pack": 0, "diag": 5}),
-    "pre_d6": ("pregather", {"layout": "degree", "pack": 0, "diag": 6}),
     "pre_ht128": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
     "pre_ht256": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
     "pre_ht512": ("pregather", {"layout": "degree", "pack": 0, "hub_threshold": 512}),
@@ -69,17 +61,6 @@ VARIANTS = {
     "stage_nopack": ("stage", {"pack": 0}),
     "stage_lo0": ("stage", {"staged_lo": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
-    # timing-only ablations (WRONG results): need the -DFU_DIAG library (make DIAG=1,
-    # FU_LIBRARY=.../libfu_diag.so)
-    "diag1_1024": ("recon", {"tile_edges": 1024, "diag": 1}),
-    "diag2_1024": ("recon", {"tile_edges": 1024, "diag": 2}),
-    "diag12_1024": ("recon", {"tile_edges": 1024, "diag": 12}),
-    "diag5_deg": ("recon", {"diag": 5, "layout": "degree"}),
-    "diag6_deg": ("recon", {"diag": 6, "layout": "degree"}),
-    "diag1_stage_nopack": ("stage", {"pack": 0, "diag": 1}),
-    "diag2_stage_nopack": ("stage", {"pack": 0, "diag": 2}),
-    "diag4_stage_nopack": ("stage", {"pack": 0, "diag": 4}),
-    "diag4_stage": ("stage", {"diag": 4}),
 }
 
 args = [a for a in sys.argv[1:] if not a.startswith("--")]
@@ -100,11 +81,9 @@ for spec in specs:
         kern, o = VARIANTS[nm]
         e = fu.CollectAll(g, v, kernel=kern, layout=o.get("layout", "given"))
         for k, val in o.items():
-            if k not in ("diag", "layout"):
+            if k != "layout":
                 e.set_option(k, val)
         e.run(warm)
-        if "diag" in o:
-            e.set_option("diag", o["diag"])
         engs[nm] = e
     res = {k: [] for k in engs}
     for rep in range(reps):
