@@ -1065,6 +1065,7 @@ constexpr int kTrThreads = 1024;
 // its bucket and serves a bucket's hot edges from a per-bucket list {column, position} in
 // edge order: 4 B per hot edge read instead of 2 + 8 staged, 8 + 2 transposed.
 constexpr int kTrHot = 10240;  // 80 KB of LDS; with the 76 KB bucket tables: 156 KB of 160
+constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 
 // Persistent over its buckets: grid = 8 x (blocks per XCD); XCD x owns the contiguous
 // bucket range [x per, (x + 1) per) and its blocks take every nj-th bucket of it. The next
@@ -1074,7 +1075,7 @@ constexpr int kTrHot = 10240;  // 80 KB of LDS; with the 76 KB bucket tables: 15
 #ifndef FU_TR_WAVES
 #define FU_TR_WAVES 1
 #endif
-template <bool HOT>
+template <int HOTN>  // LDS capacity of the hot table (0: no hot neighbours)
 __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
@@ -1084,7 +1085,8 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
                                                         const int *__restrict__ hoff,
                                                         const unsigned *__restrict__ hlist) {
   __shared__ double s_v[kTrBE];
-  __shared__ double s_hot[HOT ? kTrHot : 1];
+  constexpr bool HOT = HOTN > 0;
+  __shared__ double s_hot[HOT ? HOTN : 1];
   __shared__ unsigned short s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
   __shared__ int s_o[kTrMaxP];      // G_A index of each run
   __shared__ int s_c[kTrBE / 64 + 1];
@@ -1747,6 +1749,111 @@ __global__ __launch_bounds__(kBlock) void k_lag_final(const int *__restrict__ ro
   }
 }
 
+// Kernel 9's mega-hub chains as a few persistent one-wave blocks (option hub_blocks): block
+// b runs the exact chains (CA:106-113) of its hubs one after the other (the host deals the
+// hubs longest first to the least loaded block), streaming Gb and the old flows through two
+// LDS halves, with the loads of the next kHubD - 1 chunks in flight in registers (the chain
+// of R-MAT-24's longest hub, 406,598 elements, is the round's critical path: with one chunk
+// in flight it waited on memory at ~14 ns per element). One 64-thread block with 16 KB of LDS
+// per CU instead of one 256-thread block per hub: the 2,325 hub blocks of R-MAT-24 no longer
+// fill the CUs' wave slots and LDS while the transposes and the heavy rows wait for them.
+// LAGM as k_heavy_multi (lag): the hub's f_{r-2} is materialised while it is staged and
+// k_hub_flows is not launched; hist is indexed by the hub's slot in hub_sorted.
+constexpr int kHubCH = 512;  // pairs per LDS half
+constexpr int kHubD = 4;     // chunks of loads in flight (register sets)
+template <bool CHECK, int LAGM>
+__global__ __launch_bounds__(64) void k_hub_chains(const int *__restrict__ plan, const int *__restrict__ plan_off,
+                                                   const int *__restrict__ hub_sorted,
+                                                   const int *__restrict__ rowptr, const double *__restrict__ v,
+                                                   double *__restrict__ F, const double *__restrict__ a_prev2,
+                                                   double *__restrict__ a_new, const double *__restrict__ target,
+                                                   unsigned long long *__restrict__ err, void *__restrict__ code_new,
+                                                   const PackCtl *__restrict__ ctl, const double *__restrict__ Gb,
+                                                   int fm, const double *__restrict__ Gb_old,
+                                                   double *__restrict__ hist) {
+  constexpr bool LAG = LAGM > 0, mat = LAGM == 2;
+  __shared__ double s_x[2 * kHubCH];
+  __shared__ double s_er_buf[2 * kHubCH + 2];  // one double off s_x's banks
+  double *const s_er = s_er_buf + 1;
+  constexpr int PL = kHubCH / 64;
+  const PackCtl pc = ctl[2];
+  const int t = threadIdx.x;
+  unsigned long long eb = 0;
+  for (int q = plan_off[blockIdx.x]; q < plan_off[blockIdx.x + 1]; ++q) {
+    const int slot = plan[q];
+    const int i = hub_sorted[slot];
+    const int b = rowptr[i], d = rowptr[i + 1] - b;
+    const double own2 = a_prev2[i];
+    double own4 = 0.0;
+    if (LAG) {
+      if (mat) own4 = hist[slot];
+      wave_sync();
+      if (t == 0) hist[slot] = own2;
+    }
+    double S = 0.0, T = 0.0;
+    double nf[kHubD][PL], ng[kHubD][PL], no[kHubD][PL];
+    auto load = [&](int set, int c0) {
+#pragma unroll
+      for (int u = 0; u < PL; ++u) {
+        const int k = min(c0 + t + 64 * u, d - 1);  // clamped: every set issues the same loads
+        ng[set][u] = Gb[b + k];
+        if constexpr (mat) {
+          no[set][u] = Gb_old[b + k];
+          nf[set][u] = ld_f(F, b + k);
+        } else {
+          nf[set][u] = ld_fo(F, b + k, fm, own2);
+        }
+      }
+    };
+    auto put = [&](int set, int c0) {
+      double *xs = s_x + ((c0 / kHubCH) & 1) * kHubCH, *es = s_er + ((c0 / kHubCH) & 1) * kHubCH;
+#pragma unroll
+      for (int u = 0; u < PL; ++u) {
+        const int k = c0 + t + 64 * u;
+        double f2 = nf[set][u];  // f_{r-2}
+        if (LAG && k < d) {
+          if constexpr (mat) {
+            f2 = (recon_fr(nf[set][u], no[set][u], own4) + own2) - no[set][u];
+            st_f(F, b + k, f2, nf[set][u]);
+          } else if (fm) {
+            st_f_full(F, b + k, f2);
+          }
+        }
+        xs[t + 64 * u] = recon_fr(f2, ng[set][u], own2);
+        es[t + 64 * u] = ng[set][u];
+      }
+    };
+    // kHubD register sets in turn: chunk c uses set c % kHubD; the loads of chunks c + 1 ..
+    // c + kHubD - 1 are in flight while chunk c's chain runs
+#pragma unroll
+    for (int k = 0; k < kHubD; ++k) load(k, k * kHubCH);
+    for (int c0 = 0; c0 < d; c0 += kHubD * kHubCH) {
+#pragma unroll
+      for (int k = 0; k < kHubD; ++k) {
+        const int cc = c0 + k * kHubCH;
+        if (cc < d) {
+          put(k, cc);
+          load(k, cc + kHubD * kHubCH);
+          wave_sync();
+          chain_sum(s_x + ((cc / kHubCH) & 1) * kHubCH, s_er + ((cc / kHubCH) & 1) * kHubCH, min(kHubCH, d - cc), S, T);
+          wave_sync();
+        }
+      }
+    }
+    if (t == 0) {
+      const double a = ((v[i] - S) + T) / (double)(d + 1);
+      st_wt(a_new + i, a);
+      if (pc.width) put_code(pc, code_new, i, a);
+      if (CHECK) {
+        const unsigned long long x = err_bits(a, target[i]);
+        eb = eb > x ? eb : x;
+      }
+    }
+  }
+  if (CHECK && t == 0 && eb && eb > __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(err, eb);
+}
+
 // Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
 // reconstruction of kernel 4), so k_round_recon's hub block only runs the chain.
 __global__ __launch_bounds__(kBlock) void k_hub_stage(int nhub, const int4 *__restrict__ hubs,
@@ -2378,6 +2485,9 @@ struct fu_handle {
   int4 *hub_tiles_sorted = nullptr;  // their -3 tiles in the same order
   std::vector<int64_t> h_hub_len;    // their lengths (host)
   int hub_multi = 0;          // kernel 9: mega hubs of <= hub_multi edges as k_heavy_multi blocks (0: none)
+  int hub_blocks = 0;         // kernel 9: mega-hub chains in this many persistent one-wave blocks (0: one block per hub)
+  int hub_plan_for = 0;       // hub_blocks value hub_plan was dealt for
+  int *hub_plan = nullptr, *hub_plan_off = nullptr;  // per block: its hubs (hub_sorted slots), longest first
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2549,8 +2659,10 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *c
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
   for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk, (void *)h->hub_sorted,
-                  (void *)h->hub_tiles_sorted})
+                  (void *)h->hub_tiles_sorted, (void *)h->hub_plan, (void *)h->hub_plan_off})
     if (p) hipFree(p);
+  h->hub_plan = h->hub_plan_off = nullptr;
+  h->hub_plan_for = 0;
   h->hub_blk = nullptr;
   h->hub_sorted = nullptr;
   h->hub_tiles_sorted = nullptr;
@@ -2855,7 +2967,7 @@ int ensure_transpose(fu_handle *h) {
   int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
     if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
-  // hot neighbours (id < H) bypass the staging launch (k_transpose<true>; not k_transpose_pipe)
+  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>; not k_transpose_pipe)
   const int32_t H = h->tr_pipe ? 0 : (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
   std::vector<int64_t> cnt(P, 0);
   for (int64_t e = 0; e < E; ++e)
@@ -3047,6 +3159,34 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   return FU_OK;
 }
 
+// hub_blocks: deal the mega hubs (their slots in hub_sorted, longest first) to the least
+// loaded of P blocks
+int ensure_hub_plan(fu_handle *h) {
+  const int P = std::min(h->hub_blocks, std::max(h->n_hub, 1));
+  if (h->hub_plan && h->hub_plan_for == h->hub_blocks) return FU_OK;
+  if (h->hub_plan) hipFree(h->hub_plan);
+  if (h->hub_plan_off) hipFree(h->hub_plan_off);
+  h->hub_plan = h->hub_plan_off = nullptr;
+  std::vector<std::vector<int32_t>> per(P);
+  std::vector<int64_t> load(P, 0);
+  for (int q = 0; q < h->n_hub; ++q) {  // slots in hub_sorted, longest first
+    const int b = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    per[b].push_back(q);
+    load[b] += h->h_hub_len[q];
+  }
+  std::vector<int32_t> plan, off(1, 0);
+  for (const auto &v : per) {
+    plan.insert(plan.end(), v.begin(), v.end());
+    off.push_back((int32_t)plan.size());
+  }
+  if (int rc = dmalloc(&h->hub_plan, std::max<size_t>(1, plan.size()))) return rc;
+  if (int rc = dmalloc(&h->hub_plan_off, off.size())) return rc;
+  if (!plan.empty()) HIP_TRY(hipMemcpy(h->hub_plan, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(h->hub_plan_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
+  h->hub_plan_for = h->hub_blocks;
+  return FU_OK;
+}
+
 // Kernel 9: k_stage -> k_transpose (the mega-hub buckets first) -> kernel 4's tiles reading
 // the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
 // the remaining buckets and tiles.
@@ -3091,7 +3231,8 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
   const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
   const bool lag_multi = h->lag && multi;
-  const bool lag_hub = h->lag && hubs && h->hub_multi && nbig == 0;
+  // hubs lagged: all as multi-row blocks (hub_multi) or in the persistent hub blocks
+  const bool lag_hub = h->lag && hubs && ((h->hub_multi && nbig == 0) || (h->hub_blocks && !h->hub_multi));
   const int p = r1;
   if (h->lagf[p] && (h->lag_nmulti[p] != (lag_multi ? n_multi : 0) || h->lag_hubs[p] != (int)lag_hub)) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
@@ -3102,14 +3243,20 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (pipe)
       hipLaunchKernelGGL(k_transpose_pipe, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb);
-    else if (h->tr.H)
-      hipLaunchKernelGGL(k_transpose<true>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+    else if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
+      hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
+    else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
+      hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else
-      hipLaunchKernelGGL(k_transpose<false>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+      hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
   };
   if (bh) tr_launch(0, bh);
+  if (hubs && h->hub_blocks && !h->hub_multi) {
+    if (int rc = ensure_hub_plan(h)) return rc;
+  }
   if (hubs) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
@@ -3132,7 +3279,17 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
         else if (lagm == 1) hm(std::integral_constant<int, 1>{});
         else hm(std::integral_constant<int, 2>{});
       }
-      if (nbig)
+      if (nbig && h->hub_blocks && !h->hub_multi) {  // a few persistent one-wave blocks
+        auto hb = [&](auto L) {
+          hipLaunchKernelGGL((k_hub_chains<decltype(C)::value, decltype(L)::value>), dim3(std::min(h->hub_blocks, nmega)),
+                             dim3(64), 0, h->stream2, h->hub_plan, h->hub_plan_off, h->hub_sorted, h->rowptr, h->v,
+                             c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
+                             h->tr.hist[p] + h->tr.hist_hub);
+        };
+        if (!lag_hub) hb(std::integral_constant<int, 0>{});
+        else if (lagm == 1) hb(std::integral_constant<int, 1>{});
+        else hb(std::integral_constant<int, 2>{});
+      } else if (nbig)
         hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
                            0, h->stream2, h->hub_multi ? h->hub_tiles_sorted : tl, h->rowptr, h->col, h->v, c.F, c.ap,
                            c.ap2, c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1,
@@ -3636,6 +3793,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     }
     return FU_OK;
   }
+  if (!std::strcmp(key, "hub_blocks")) {  // kernel 9: mega-hub chains in P persistent one-wave blocks (0: one per hub)
+    if (value < 0 || value > 65536) return fail(FU_ERR_ARG, "fu_set_option: hub_blocks must be in [0, 65536]");
+    h->hub_blocks = (int)value;
+    return FU_OK;
+  }
   if (!std::strcmp(key, "hub_multi")) {  // kernel 9: mega hubs of <= value edges many per chain wave (0: one per block)
     if (value < 0 || value > INT32_MAX) return fail(FU_ERR_ARG, "fu_set_option: hub_multi must be in [0, 2^31)");
     h->hub_multi = (int)value;
@@ -4107,7 +4269,8 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
-                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->hub_sorted, h->hub_tiles_sorted, h->code[0], h->code[1], h->pctl,
+                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->hub_sorted, h->hub_tiles_sorted, h->hub_plan,
+                              h->hub_plan_off, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG, h->col16, h->cbase,
                               h->tnar_geo[0], h->tnar_geo[1], h->tnar_geo[2], h->tnar_geo[3]};
   free_transpose(h);

@@ -36,7 +36,14 @@ VARIANTS = {
     "pre_hubmall": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 1 << 30}),
     "pre_lag": ("pregather", {"layout": "degree", "pack": 0, "lag": 1}),
     "pre_hot": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240}),
-    "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1, "hub_multi": 1 << 30}),
+    "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1}),
+    "pre_hot4k_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096, "lag": 1}),
+    "pre_hot4k": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096}),
+    "pre_hb256": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256}),
+    "pre_hb512": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 512}),
+    "pre_hb256_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1}),
+    "pre_hb256_lag_hot4k": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 4096}),
+    "pre_hb256_lag_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 10240}),
     "pre_lag_hubmall": ("pregather", {"layout": "degree", "pack": 0, "lag": 1, "hub_multi": 1 << 30}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
