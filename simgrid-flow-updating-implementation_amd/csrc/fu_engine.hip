@@ -432,7 +432,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
     const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb, int fm,
     const unsigned short *__restrict__ col16 = nullptr, const int *__restrict__ cbase = nullptr,
-    const int *__restrict__ tnar = nullptr) {
+    const int *__restrict__ tnar = nullptr, int hub_prio = 0) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -585,7 +585,10 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
     if (PRE && t < 64) {
       // kernel 9: the row's estimates are pre-gathered (Gb), so the chain wave streams Gb
-      // and the old flows itself, coalesced, and rebuilds fr as k_hub_stage would
+      // and the old flows itself, coalesced, and rebuilds fr as k_hub_stage would. hub_prio:
+      // the chain wave issues ahead of the other waves on its SIMD (a hub's chain is one
+      // dependent fp64 add per element; shared issue slots stretch it)
+      if (hub_prio) __builtin_amdgcn_s_setprio(3);
       const double own2 = a_prev2[i];
       double nf[PL], ng[PL];
 #pragma unroll
@@ -1770,8 +1773,9 @@ __global__ __launch_bounds__(64) void k_hub_chains(const int *__restrict__ plan,
                                                    unsigned long long *__restrict__ err, void *__restrict__ code_new,
                                                    const PackCtl *__restrict__ ctl, const double *__restrict__ Gb,
                                                    int fm, const double *__restrict__ Gb_old,
-                                                   double *__restrict__ hist) {
+                                                   double *__restrict__ hist, int hub_prio) {
   constexpr bool LAG = LAGM > 0, mat = LAGM == 2;
+  if (hub_prio) __builtin_amdgcn_s_setprio(3);  // the chains issue ahead of the co-resident waves
   __shared__ double s_x[2 * kHubCH];
   __shared__ double s_er_buf[2 * kHubCH + 2];  // one double off s_x's banks
   double *const s_er = s_er_buf + 1;
@@ -2486,6 +2490,7 @@ struct fu_handle {
   std::vector<int64_t> h_hub_len;    // their lengths (host)
   int hub_multi = 0;          // kernel 9: mega hubs of <= hub_multi edges as k_heavy_multi blocks (0: none)
   int hub_blocks = 0;         // kernel 9: mega-hub chains in this many persistent one-wave blocks (0: one block per hub)
+  int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
   int hub_plan_for = 0;       // hub_blocks value hub_plan was dealt for
   int *hub_plan = nullptr, *hub_plan_off = nullptr;  // per block: its hubs (hub_sorted slots), longest first
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
@@ -3284,7 +3289,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
           hipLaunchKernelGGL((k_hub_chains<decltype(C)::value, decltype(L)::value>), dim3(std::min(h->hub_blocks, nmega)),
                              dim3(64), 0, h->stream2, h->hub_plan, h->hub_plan_off, h->hub_sorted, h->rowptr, h->v,
                              c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
-                             h->tr.hist[p] + h->tr.hist_hub);
+                             h->tr.hist[p] + h->tr.hist_hub, h->hub_prio);
         };
         if (!lag_hub) hb(std::integral_constant<int, 0>{});
         else if (lagm == 1) hb(std::integral_constant<int, 1>{});
@@ -3293,7 +3298,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
         hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
                            0, h->stream2, h->hub_multi ? h->hub_tiles_sorted : tl, h->rowptr, h->col, h->v, c.F, c.ap,
                            c.ap2, c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1,
-                           Gb, c.fm);
+                           Gb, c.fm, nullptr, nullptr, nullptr, h->hub_prio);
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
@@ -3791,6 +3796,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "hub_prio")) {  // kernel 9: hub chain waves issue first on their SIMD (1)
+    h->hub_prio = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "hub_blocks")) {  // kernel 9: mega-hub chains in P persistent one-wave blocks (0: one per hub)

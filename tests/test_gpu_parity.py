@@ -627,7 +627,8 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all", "lag", "lag_hubm_all", "lag_hubm",
-                                   "hot", "hot_lag", "hot_pipe", "hot4k", "hubblocks", "hubblocks_lag_hot"])
+                                   "hot", "hot_lag", "hot_pipe", "hot4k", "hubblocks", "hubblocks_lag_hot",
+                                   "prio"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -666,6 +667,9 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("tr_hot", 4096)
     elif multi == "hubblocks":  # mega-hub chains in 7 persistent one-wave blocks (several hubs each)
         eng.set_option("hub_blocks", 7)
+        eng.set_option("hub_prio", 1)
+    elif multi == "prio":
+        eng.set_option("hub_prio", 1)
     elif multi == "hubblocks_lag_hot":
         eng.set_option("hub_blocks", 3)
         eng.set_option("lag", 1)

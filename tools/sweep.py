@@ -42,6 +42,10 @@ VARIANTS = {
     "pre_hb256": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256}),
     "pre_hb512": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 512}),
     "pre_hb256_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1}),
+    "pre_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1}),
+    "pre_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "lag": 1}),
+    "pre_hb256_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1}),
+    "pre_hb256_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1, "lag": 1}),
     "pre_hb256_lag_hot4k": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 4096}),
     "pre_hb256_lag_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 10240}),
     "pre_lag_hubmall": ("pregather", {"layout": "degree", "pack": 0, "lag": 1, "hub_multi": 1 << 30}),
