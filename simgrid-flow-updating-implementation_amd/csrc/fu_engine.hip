@@ -1223,13 +1223,20 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
 // stored, and bucket k + 1's run table and searches are built while bucket k's loads land.
 // Every iteration issues the same loads (a missing next bucket reads element 0 and ignores
 // it), so the wait for bucket k's loads leaves bucket k + 1's in flight. Same G_B as
-// k_transpose.
+// k_transpose; HOTN as k_transpose (the hot edges' list entries are loaded with the bucket's
+// other loads, their values read from the block's LDS copy of a_{r-1}[0, H)).
+template <int HOTN>
 __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, int P, long long E,
                                                              const int *__restrict__ offT,
                                                              const double *__restrict__ GA,
                                                              const unsigned short *__restrict__ pos16,
-                                                             double *__restrict__ GB) {
+                                                             double *__restrict__ GB,
+                                                             const double *__restrict__ a_prev, int H,
+                                                             const int *__restrict__ hoff,
+                                                             const unsigned *__restrict__ hlist) {
+  constexpr bool HOT = HOTN > 0;
   __shared__ double s_v[kTrBE];
+  __shared__ double s_hot[HOT ? HOTN : 1];
   __shared__ unsigned short s_m[kTrMaxP + 1];
   __shared__ int s_o[kTrMaxP];
   __shared__ int s_c[kTrBE / 64 + 1];
@@ -1240,6 +1247,8 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
   if (bk >= bend) return;
+  if (HOT)  // visible after the first table barrier
+    for (int q = t; q < H; q += kTrThreads) s_hot[q] = a_prev[q];
   constexpr int kPerT = kTrBE / kTrThreads;
   int o[2], len[2];
   auto load_runs = [&](int bkk) {  // clamped: a bucket past the range loads the last one's
@@ -1311,22 +1320,46 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
       }
     }
   };
-  auto issue = [&](const int (&g)[kPerT], double (&val)[kPerT], int (&pos)[kPerT]) {
+  // hot edges of a bucket: at most 2 list entries per thread with the other loads
+  unsigned hxA[2] = {0u, 0u}, hxB[2] = {0u, 0u};
+  int hrA[2] = {0, 0}, hrB[2] = {0, 0};  // the bucket's hot list range
+  auto issue = [&](const int (&g)[kPerT], double (&val)[kPerT], int (&pos)[kPerT], int bkk, bool valid,
+                   unsigned (&hx)[2], int (&hr)[2]) {
 #pragma unroll
     for (int k = 0; k < kPerT; ++k) {  // unconditional, from a valid index
       const int q = max(g[k], 0);
       val[k] = GA[q];
       pos[k] = g[k] >= 0 ? (int)pos16[q] : -1;
     }
+    if (HOT) {
+      const int bb = b0 + min(bkk, bend - 1);
+      hr[0] = valid ? hoff[bb] : 0;
+      hr[1] = valid ? hoff[bb + 1] : 0;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = hr[0] + t + k * kTrThreads;
+        hx[k] = hlist[q < hr[1] ? q : 0];
+      }
+    }
   };
   // bucket cur: the loads in (val, pos) -> s_v by position -> G_B, coalesced
-  auto finish = [&](int cur, const double (&val)[kPerT], const int (&pos)[kPerT]) {
+  auto finish = [&](int cur, const double (&val)[kPerT], const int (&pos)[kPerT], const unsigned (&hx)[2],
+                    const int (&hr)[2]) {
     const long long e0 = (long long)(b0 + cur) * kTrBE;
     const int ne = (int)min((long long)kTrBE, E - e0);
     __syncthreads();  // the previous bucket's G_B stores have read s_v
 #pragma unroll
     for (int k = 0; k < kPerT; ++k)
       if (pos[k] >= 0) s_v[pos[k]] = val[k];
+    if (HOT) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+        if (hr[0] + t + k * kTrThreads < hr[1]) s_v[hx[k] & 0xFFFFu] = s_hot[hx[k] >> 16];
+      for (int q = hr[0] + t + 2 * kTrThreads; q < hr[1]; q += kTrThreads) {  // > 2048 hot edges
+        const unsigned x = hlist[q];
+        s_v[x & 0xFFFFu] = s_hot[x >> 16];
+      }
+    }
     __syncthreads();
     for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
   };
@@ -1335,10 +1368,11 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   load_runs(bk);
   search(tables(), gA);
   load_runs(bk + nj);
-  issue(gA, vA, pA);
+  issue(gA, vA, pA, bk, true, hxA, hrA);
   // one step: build + issue bucket nx's loads into N, then finish bucket cur from C
-  auto step = [&](int cur, int (&gN)[kPerT], double (&vN)[kPerT], int (&pN)[kPerT],
-                  const double (&vC)[kPerT], const int (&pC)[kPerT]) -> bool {
+  auto step = [&](int cur, int (&gN)[kPerT], double (&vN)[kPerT], int (&pN)[kPerT], unsigned (&hN)[2],
+                  int (&rN)[2], const double (&vC)[kPerT], const int (&pC)[kPerT], const unsigned (&hC)[2],
+                  const int (&rC)[2]) -> bool {
     const int nx = cur + nj;
     const bool more = nx < bend;
     {
@@ -1349,14 +1383,14 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
         for (int k = 0; k < kPerT; ++k) gN[k] = -1;
     }
     load_runs(nx + nj);
-    issue(gN, vN, pN);
-    finish(cur, vC, pC);
+    issue(gN, vN, pN, nx, more, hN, rN);
+    finish(cur, vC, pC, hC, rC);
     return more;
   };
   for (;;) {
-    if (!step(bk, gB, vB, pB, vA, pA)) break;
+    if (!step(bk, gB, vB, pB, hxB, hrB, vA, pA, hxA, hrA)) break;
     bk += nj;
-    if (!step(bk, gA, vA, pA, vB, pB)) break;
+    if (!step(bk, gA, vA, pA, hxA, hrA, vB, pB, hxB, hrB)) break;
     bk += nj;
   }
 }
@@ -2422,6 +2456,7 @@ struct fu_handle {
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
   hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_tr = nullptr;  // kernel 9 side_tiles: every bucket transposed
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
@@ -2491,6 +2526,7 @@ struct fu_handle {
   int hub_multi = 0;          // kernel 9: mega hubs of <= hub_multi edges as k_heavy_multi blocks (0: none)
   int hub_blocks = 0;         // kernel 9: mega-hub chains in this many persistent one-wave blocks (0: one block per hub)
   int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
+  int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int hub_plan_for = 0;       // hub_blocks value hub_plan was dealt for
   int *hub_plan = nullptr, *hub_plan_off = nullptr;  // per block: its hubs (hub_sorted slots), longest first
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
@@ -2972,8 +3008,8 @@ int ensure_transpose(fu_handle *h) {
   int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
     if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
-  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>; not k_transpose_pipe)
-  const int32_t H = h->tr_pipe ? 0 : (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
+  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>, k_transpose_pipe<HOTN>)
+  const int32_t H = (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
   std::vector<int64_t> cnt(P, 0);
   for (int64_t e = 0; e < E; ++e)
     if (h->h_col[e] >= H) cnt[h->h_col[e] / SN]++;
@@ -3243,11 +3279,19 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
   }
   const int lagm = (lag_multi || lag_hub) ? (h->lagf[p] ? 2 : 1) : 0;
-  const bool pipe = h->tr_pipe && h->tr_bpx > 0 && h->tr.H == 0;
+  const bool pipe = h->tr_pipe && h->tr_bpx > 0;
   auto tr_launch = [&](int b0, int nb) {
-    if (pipe)
-      hipLaunchKernelGGL(k_transpose_pipe, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb);
+    if (pipe && h->tr.H > kTrHotS)
+      hipLaunchKernelGGL(k_transpose_pipe<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
+                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
+                         h->tr.hlist);
+    else if (pipe && h->tr.H)
+      hipLaunchKernelGGL(k_transpose_pipe<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
+                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
+                         h->tr.hlist);
+    else if (pipe)
+      hipLaunchKernelGGL(k_transpose_pipe<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
     else if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
       hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
@@ -3268,6 +3312,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   }
   if (h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
   const bool chk = c.err != nullptr;
+  // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
+  // behind the hub path, once every bucket is transposed, beside the heavy rows
+  const int side = hubs ? h->side_tiles : 0;
+  if (side) HIP_TRY(hipEventRecord(h->ev_tr, h->stream));
   if (hubs) {
     auto chains = [&](auto C) {
       // hub_multi: the hubs of <= hub_multi edges as k_heavy_multi blocks (kMR hubs of similar
@@ -3305,6 +3353,22 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (!lag_hub)
       hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
                          (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
+    if (side) {
+      HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_tr, 0));
+      auto st = [&](auto C) {
+        if (side >= 2 && nh > m1)  // the rows of 129-256 edges (4 per block, in registers)
+          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(nh - m1),
+                             dim3(kBlock), 0, h->stream2, tl + m1, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
+                             h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
+                             c.fm);
+        if (nl)
+          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+                             h->stream2, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err,
+                             cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
+      };
+      if (chk) st(std::true_type{});
+      else st(std::false_type{});
+    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
   }
@@ -3336,8 +3400,8 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
       heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     }
-    heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
-    if (nl)
+    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
+    if (nl && !side)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
@@ -3569,7 +3633,8 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_tr, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
@@ -3768,10 +3833,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_pipe")) {  // kernel 9: software-pipelined transpose (1)
-    if ((value != 0) != (h->tr_pipe != 0)) {
-      if (int rc = lag_finalize_all(h)) return rc;
-      free_transpose(h);  // the layout's hot lists follow it (k_transpose_pipe has none)
-    }
     h->tr_pipe = value != 0;
     return FU_OK;
   }
@@ -3796,6 +3857,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "side_tiles")) {  // kernel 9: light tiles (1), and rows of 129-256 edges (2), on the side stream
+    if (value < 0 || value > 2) return fail(FU_ERR_ARG, "fu_set_option: side_tiles must be 0, 1 or 2");
+    h->side_tiles = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "hub_prio")) {  // kernel 9: hub chain waves issue first on their SIMD (1)
@@ -4291,7 +4357,7 @@ int fu_destroy(fu_handle *h) {
   }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join})
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_tr})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);
