@@ -2452,11 +2452,13 @@ struct fu_handle {
   std::vector<int64_t> h_orig_rowptr;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;            // kernel 4's heavy tiles, concurrently (fork_heavy)
+  hipStream_t stream3 = nullptr;            // kernel 9 split_tr: the heavy rows beside the last transposes
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
   hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_tr = nullptr;  // kernel 9 side_tiles: every bucket transposed
+  hipEvent_t ev_htr = nullptr, ev_s3 = nullptr;  // kernel 9 split_tr: heavy-row buckets done; stream3 done
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
@@ -2527,6 +2529,7 @@ struct fu_handle {
   int hub_blocks = 0;         // kernel 9: mega-hub chains in this many persistent one-wave blocks (0: one block per hub)
   int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
+  int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int hub_plan_for = 0;       // hub_blocks value hub_plan was dealt for
   int *hub_plan = nullptr, *hub_plan_off = nullptr;  // per block: its hubs (hub_sorted slots), longest first
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
@@ -2566,6 +2569,7 @@ struct fu_handle {
   struct TransLayout {
     int P = 0, Q = 0, NB = 0, B = 0;      // slices, blocks per slice, stage blocks, buckets
     int Bh = 0;                           // buckets [0, Bh) hold the mega-hub rows' edges
+    int Bm = 0;                           // buckets [0, Bm) hold every edge of the k_heavy_multi rows
     int4 *brange = nullptr;               // stage blocks: {begin, end} in G_A, slice, 0
     unsigned short *colS = nullptr;       // per G_A element: column offset in its slice
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
@@ -3081,6 +3085,14 @@ int ensure_transpose(fu_handle *h) {
   T.NB = (int)br.size();
   T.B = (int)B;
   T.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
+  {  // the multi-row heavy rows of geometry 1 (contiguous after the hubs under the degree layout)
+    int64_t mend = hub_end;
+    for (int q = 0; q < h->multi_geo[1][1]; ++q) {
+      const int32_t i = h->h_hrows[h->multi_geo[1][0] + q];
+      mend = std::max<int64_t>(mend, h->h_rowptr[i + 1]);
+    }
+    T.Bm = (int)std::max<int64_t>(T.Bh, (mend + kTrBE - 1) / kTrBE);
+  }
   h->tr_ready = true;
   return FU_OK;
 }
@@ -3310,7 +3322,18 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
-  if (h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
+  // split_tr: the buckets of the multi-row heavy rows first, then k_heavy_multi on stream3
+  // beside the remaining (latency-bound) transposes
+  const int bm = std::min(std::max(h->tr.Bm, bh), h->tr.B);
+  const bool split = h->split_tr && bm > bh && bm < h->tr.B;
+  if (split) {
+    tr_launch(bh, bm - bh);
+    HIP_TRY(hipEventRecord(h->ev_htr, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream3, h->ev_htr, 0));
+    tr_launch(bm, h->tr.B - bm);
+  } else if (h->tr.B > bh) {
+    tr_launch(bh, h->tr.B - bh);
+  }
   const bool chk = c.err != nullptr;
   // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
   // behind the hub path, once every bucket is transposed, beside the heavy rows
@@ -3389,8 +3412,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (multi) {
       auto hm = [&](auto L) {
         hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, true, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
-                           dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F,
-                           c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old, h->tr.hist[p]);
+                           dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
+                           h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
+                           h->tr.hist[p]);
       };
       if (!lag_multi) hm(std::integral_constant<int, 0>{});
       else if (lagm == 1) hm(std::integral_constant<int, 1>{});
@@ -3409,6 +3433,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   if (chk) tiles(std::true_type{});
   else tiles(std::false_type{});
   HIP_TRY(hipGetLastError());
+  if (split && multi) {
+    HIP_TRY(hipEventRecord(h->ev_s3, h->stream3));
+    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_s3, 0));
+  }
   if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
     h->lagf[p] = 1;
@@ -3622,7 +3650,8 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, hi) != hipSuccess)
+        hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, hi) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess)
       return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
   }
   {
@@ -3634,7 +3663,9 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_tr, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_tr, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_htr, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&h->ev_s3, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
@@ -3857,6 +3888,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "split_tr")) {  // kernel 9: heavy rows start once their buckets are transposed (1)
+    h->split_tr = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "side_tiles")) {  // kernel 9: light tiles (1), and rows of 129-256 edges (2), on the side stream
@@ -4341,6 +4376,7 @@ int fu_destroy(fu_handle *h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
+  if (h->stream3) hipStreamSynchronize(h->stream3);
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
@@ -4357,13 +4393,14 @@ int fu_destroy(fu_handle *h) {
   }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_tr})
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_tr, h->ev_htr, h->ev_s3})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
+  if (h->stream3) hipStreamDestroy(h->stream3);
   delete h;
   return FU_OK;
 }

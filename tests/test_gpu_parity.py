@@ -628,7 +628,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all", "lag", "lag_hubm_all", "lag_hubm",
                                    "hot", "hot_lag", "hot_pipe", "hot4k", "hubblocks", "hubblocks_lag_hot",
-                                   "prio", "side1", "side2_lag_hot_pipe"])
+                                   "prio", "side1", "side2_lag_hot_pipe", "split", "split_side1_lag_hot"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -672,6 +672,11 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("hub_prio", 1)
     elif multi == "side1":  # light tiles on the side stream behind the hub path
         eng.set_option("side_tiles", 1)
+    elif multi == "split":  # the heavy rows on a third stream once their buckets are transposed
+        eng.set_option("split_tr", 1)
+    elif multi == "split_side1_lag_hot":
+        for key, val in (("split_tr", 1), ("side_tiles", 1), ("lag", 1), ("tr_hot", 3000), ("hub_prio", 1)):
+            eng.set_option(key, val)
     elif multi == "side2_lag_hot_pipe":  # ... and the rows of 129-256 edges
         for key, val in (("side_tiles", 2), ("lag", 1), ("tr_hot", 5000), ("tr_pipe", 1), ("hub_prio", 1)):
             eng.set_option(key, val)

@@ -4,5 +4,5 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "multi_row_chains or lag" > gpurun_out/pytest_c.log 2>&1 || exit $?
 rm -rf gpurun_out/ab
-AB_SPEC="rmat:scale=24,ef=16" AB_ARGS="--warm=3 --timed=20 --reps=3" AB_VARIANTS="deg_np_pre pre_prio_side1 pre_prio_side2 pre_prio_side1_lag pre_prio_side1_hot_pipe" AB_ROUNDS=2 bash tools/ab_proc.sh || exit $?
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prmat_hb -o run -- python3 tools/prof_target.py --spec rmat:scale=24,ef=16 --layout degree --kernel pregather --warm 2 --rounds 20 --pack 0 --opt hub_prio=1 --opt side_tiles=1 > gpurun_out/prmat_hb.log 2>&1
+AB_SPEC="rmat:scale=24,ef=16" AB_ARGS="--warm=3 --timed=20 --reps=3" AB_VARIANTS="deg_np_pre pre_prio_side1 pre_prio_split pre_prio_split_side1 pre_prio_split_side1_hot" AB_ROUNDS=2 bash tools/ab_proc.sh || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prmat_hb -o run -- python3 tools/prof_target.py --spec rmat:scale=24,ef=16 --layout degree --kernel pregather --warm 2 --rounds 20 --pack 0 --opt hub_prio=1 --opt side_tiles=1 --opt split_tr=1 > gpurun_out/prmat_hb.log 2>&1

@@ -49,6 +49,10 @@ VARIANTS = {
     "pre_prio_side1_hot_pipe": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1,
                                               "tr_hot": 10240, "tr_pipe": 1}),
     "pre_pipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
+    "pre_prio_split": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1}),
+    "pre_prio_split_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1, "side_tiles": 1}),
+    "pre_prio_split_side1_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1,
+                                               "side_tiles": 1, "tr_hot": 10240}),
     "pre_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "lag": 1}),
     "pre_hb256_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1}),
     "pre_hb256_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1, "lag": 1}),
