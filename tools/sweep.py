@@ -49,6 +49,14 @@ VARIANTS = {
     "pre_prio_side1_hot_pipe": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1,
                                               "tr_hot": 10240, "tr_pipe": 1}),
     "pre_pipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
+    # one hub per one-wave block (hub_blocks >= hubs), lag: no k_hub_flows
+    "pre_hb4k_prio_lag_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096, "hub_prio": 1,
+                                              "lag": 1, "side_tiles": 1}),
+    "pre_hb4k_prio_lag_side1_split": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096, "hub_prio": 1,
+                                                    "lag": 1, "side_tiles": 1, "split_tr": 1}),
+    "pre_hb4k_prio_lag_side2_split_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096,
+                                                        "hub_prio": 1, "lag": 1, "side_tiles": 2, "split_tr": 1,
+                                                        "tr_hot": 10240}),
     "pre_prio_split": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1}),
     "pre_prio_split_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1, "side_tiles": 1}),
     "pre_prio_split_side1_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1,
