@@ -123,8 +123,16 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "multi_heavy"   kernel 9: rows of more than 256 edges as multi-row chain blocks (default 1);
  *                 "multi_mid" 0 keeps the rows of 257-1024 edges in the register launch.
  * "tr_pipe"       kernel 9: software-pipelined transpose (default 0; needs tr_bpx > 0).
- * "hub_multi"     kernel 9: mega hubs of <= value edges run their chains as multi-row chain
- *                 blocks (16 hubs per chain wave) instead of one block each (default 0: none).
+ * "lag"           kernel 9: the multi-row heavy rows leave f_r unwritten and write f_{r-2}
+ *                 from f_{r-4} and their kept a_{r-4}, two rounds later (default 1); the
+ *                 lagged flows are finalized before fu_get_flows, other kernels and rebuilds.
+ * "tr_hot"        kernel 9: neighbours of id < value served from an LDS table in the
+ *                 transpose instead of staged (default 0; <= 10240).
+ * "hub_prio"      kernel 9: the mega-hub chain waves run at issue priority 3 (default 0).
+ * "side_tiles"    kernel 9: 1 = the light tiles, 2 = also the rows of 129-256 edges, on the
+ *                 side stream behind the hub path once every bucket is transposed (default 0).
+ * "split_tr"      kernel 9: the multi-row heavy rows on a third stream once their own buckets
+ *                 are transposed (default 0).
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).

@@ -1585,7 +1585,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // writes f_r when another kernel, fu_get_flows or a tile rebuild needs it.
 constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
-template <bool CHECK, bool FLOWS = true, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
+template <bool CHECK, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
@@ -1732,7 +1732,7 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       if (CHECK) eb = err_bits(a, target[i]);
     }
   }
-  if (!FLOWS || LAG) {  // mega hubs: k_hub_flows writes their flows; LAG: round r + 2 does
+  if (LAG) {  // round r + 2 (or k_lag_final) writes the flows
     if (CHECK) block_max_to(eb, err);
     return;
   }
@@ -1784,112 +1784,6 @@ __global__ __launch_bounds__(kBlock) void k_lag_final(const int *__restrict__ ro
       if (k < d) st_f(F, b + k, (recon_fr(f8[u], e8[u], own2) + an) - e8[u], f8[u]);
     }
   }
-}
-
-// Kernel 9's mega-hub chains as a few persistent one-wave blocks (option hub_blocks): block
-// b runs the exact chains (CA:106-113) of its hubs one after the other (the host deals the
-// hubs longest first to the least loaded block), streaming Gb and the old flows through two
-// LDS halves, with the loads of the next kHubD - 1 chunks in flight in registers (the chain
-// of R-MAT-24's longest hub, 406,598 elements, is the round's critical path: with one chunk
-// in flight it waited on memory at ~14 ns per element). One 64-thread block with 16 KB of LDS
-// per CU instead of one 256-thread block per hub: the 2,325 hub blocks of R-MAT-24 no longer
-// fill the CUs' wave slots and LDS while the transposes and the heavy rows wait for them.
-// LAGM as k_heavy_multi (lag): the hub's f_{r-2} is materialised while it is staged and
-// k_hub_flows is not launched; hist is indexed by the hub's slot in hub_sorted.
-constexpr int kHubCH = 512;  // pairs per LDS half
-constexpr int kHubD = 4;     // chunks of loads in flight (register sets)
-template <bool CHECK, int LAGM>
-__global__ __launch_bounds__(64) void k_hub_chains(const int *__restrict__ plan, const int *__restrict__ plan_off,
-                                                   const int *__restrict__ hub_sorted,
-                                                   const int *__restrict__ rowptr, const double *__restrict__ v,
-                                                   double *__restrict__ F, const double *__restrict__ a_prev2,
-                                                   double *__restrict__ a_new, const double *__restrict__ target,
-                                                   unsigned long long *__restrict__ err, void *__restrict__ code_new,
-                                                   const PackCtl *__restrict__ ctl, const double *__restrict__ Gb,
-                                                   int fm, const double *__restrict__ Gb_old,
-                                                   double *__restrict__ hist, int hub_prio) {
-  constexpr bool LAG = LAGM > 0, mat = LAGM == 2;
-  if (hub_prio) __builtin_amdgcn_s_setprio(3);  // the chains issue ahead of the co-resident waves
-  __shared__ double s_x[2 * kHubCH];
-  __shared__ double s_er_buf[2 * kHubCH + 2];  // one double off s_x's banks
-  double *const s_er = s_er_buf + 1;
-  constexpr int PL = kHubCH / 64;
-  const PackCtl pc = ctl[2];
-  const int t = threadIdx.x;
-  unsigned long long eb = 0;
-  for (int q = plan_off[blockIdx.x]; q < plan_off[blockIdx.x + 1]; ++q) {
-    const int slot = plan[q];
-    const int i = hub_sorted[slot];
-    const int b = rowptr[i], d = rowptr[i + 1] - b;
-    const double own2 = a_prev2[i];
-    double own4 = 0.0;
-    if (LAG) {
-      if (mat) own4 = hist[slot];
-      wave_sync();
-      if (t == 0) hist[slot] = own2;
-    }
-    double S = 0.0, T = 0.0;
-    double nf[kHubD][PL], ng[kHubD][PL], no[kHubD][PL];
-    auto load = [&](int set, int c0) {
-#pragma unroll
-      for (int u = 0; u < PL; ++u) {
-        const int k = min(c0 + t + 64 * u, d - 1);  // clamped: every set issues the same loads
-        ng[set][u] = Gb[b + k];
-        if constexpr (mat) {
-          no[set][u] = Gb_old[b + k];
-          nf[set][u] = ld_f(F, b + k);
-        } else {
-          nf[set][u] = ld_fo(F, b + k, fm, own2);
-        }
-      }
-    };
-    auto put = [&](int set, int c0) {
-      double *xs = s_x + ((c0 / kHubCH) & 1) * kHubCH, *es = s_er + ((c0 / kHubCH) & 1) * kHubCH;
-#pragma unroll
-      for (int u = 0; u < PL; ++u) {
-        const int k = c0 + t + 64 * u;
-        double f2 = nf[set][u];  // f_{r-2}
-        if (LAG && k < d) {
-          if constexpr (mat) {
-            f2 = (recon_fr(nf[set][u], no[set][u], own4) + own2) - no[set][u];
-            st_f(F, b + k, f2, nf[set][u]);
-          } else if (fm) {
-            st_f_full(F, b + k, f2);
-          }
-        }
-        xs[t + 64 * u] = recon_fr(f2, ng[set][u], own2);
-        es[t + 64 * u] = ng[set][u];
-      }
-    };
-    // kHubD register sets in turn: chunk c uses set c % kHubD; the loads of chunks c + 1 ..
-    // c + kHubD - 1 are in flight while chunk c's chain runs
-#pragma unroll
-    for (int k = 0; k < kHubD; ++k) load(k, k * kHubCH);
-    for (int c0 = 0; c0 < d; c0 += kHubD * kHubCH) {
-#pragma unroll
-      for (int k = 0; k < kHubD; ++k) {
-        const int cc = c0 + k * kHubCH;
-        if (cc < d) {
-          put(k, cc);
-          load(k, cc + kHubD * kHubCH);
-          wave_sync();
-          chain_sum(s_x + ((cc / kHubCH) & 1) * kHubCH, s_er + ((cc / kHubCH) & 1) * kHubCH, min(kHubCH, d - cc), S, T);
-          wave_sync();
-        }
-      }
-    }
-    if (t == 0) {
-      const double a = ((v[i] - S) + T) / (double)(d + 1);
-      st_wt(a_new + i, a);
-      if (pc.width) put_code(pc, code_new, i, a);
-      if (CHECK) {
-        const unsigned long long x = err_bits(a, target[i]);
-        eb = eb > x ? eb : x;
-      }
-    }
-  }
-  if (CHECK && t == 0 && eb && eb > __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(err, eb);
 }
 
 // Mega hubs: (fr, er) of every hub edge into hubxy, hub-major (CA:98-99 + the flow
@@ -2522,16 +2416,9 @@ struct fu_handle {
   int64_t hub_total = 0;
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
   int *hub_blk = nullptr;    // per 256-edge block of the hub edges: the hub of its first edge
-  int *hub_sorted = nullptr;  // the mega hubs' node ids, longest first (option hub_multi)
-  int4 *hub_tiles_sorted = nullptr;  // their -3 tiles in the same order
-  std::vector<int64_t> h_hub_len;    // their lengths (host)
-  int hub_multi = 0;          // kernel 9: mega hubs of <= hub_multi edges as k_heavy_multi blocks (0: none)
-  int hub_blocks = 0;         // kernel 9: mega-hub chains in this many persistent one-wave blocks (0: one block per hub)
   int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
-  int hub_plan_for = 0;       // hub_blocks value hub_plan was dealt for
-  int *hub_plan = nullptr, *hub_plan_off = nullptr;  // per block: its hubs (hub_sorted slots), longest first
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2580,18 +2467,16 @@ struct fu_handle {
     unsigned *hlist = nullptr;            // per hot edge: column << 16 | position in its bucket
     double *GBr[3] = {nullptr, nullptr, nullptr};  // G_B of round r in GBr[r % 3] (one buffer without lag)
     double *hist[2] = {nullptr, nullptr};          // lag: per parity, a_{r-2} of every lagged row
-    int hist_hub = 0;                              // lag: hist slot of the first mega hub
   };
   TransLayout tr;
   bool tr_ready = false;
   // kernel 9 option "lag" (k_heavy_multi<LAG>): per parity p, lagf[p] = F[p] holds f_{r'-2}
   // (not f_{r'}) on the lagged rows, r' = lag_round[p] the last round of that parity; the
-  // lagged rows: lag_nmulti[p] heavy rows and, if lag_hubs[p], every mega hub
-  int lag = 0;
+  // lagged rows: lag_nmulti[p] heavy rows
+  int lag = 1;
   int lagf[2] = {0, 0};
   int64_t lag_round[2] = {0, 0};
   int lag_nmulti[2] = {0, 0};
-  int lag_hubs[2] = {0, 0};
   std::string tr_why;
   int n_cu = 256;
   void *dist = nullptr;  // multi-GPU (fu_dist.hip)
@@ -2703,14 +2588,9 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *c
 
 // Mega-hub side arrays (same rows, same order as the -3 tiles of build_tiles_geom).
 int build_hubs(fu_handle *h) {
-  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk, (void *)h->hub_sorted,
-                  (void *)h->hub_tiles_sorted, (void *)h->hub_plan, (void *)h->hub_plan_off})
+  for (void *p : {(void *)h->hub_rows, (void *)h->hub_off, (void *)h->hubxy, (void *)h->hub_blk})
     if (p) hipFree(p);
-  h->hub_plan = h->hub_plan_off = nullptr;
-  h->hub_plan_for = 0;
   h->hub_blk = nullptr;
-  h->hub_sorted = nullptr;
-  h->hub_tiles_sorted = nullptr;
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
@@ -2741,19 +2621,6 @@ int build_hubs(fu_handle *h) {
   }
   if (int rc = dmalloc(&h->hub_blk, blk.size())) return rc;
   HIP_TRY(hipMemcpy(h->hub_blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
-  std::vector<int32_t> srt;
-  for (const int4 &hr : rows) srt.push_back(hr.x);
-  std::stable_sort(srt.begin(), srt.end(), [&](int32_t x, int32_t y) {
-    return h->h_rowptr[x + 1] - h->h_rowptr[x] > h->h_rowptr[y + 1] - h->h_rowptr[y];
-  });
-  std::vector<int4> stl;
-  for (int32_t x : srt) stl.push_back(make_int4(x, -3, (int)h->h_rowptr[x], (int)h->h_rowptr[x + 1]));
-  if (int rc = dmalloc(&h->hub_sorted, srt.size())) return rc;
-  HIP_TRY(hipMemcpy(h->hub_sorted, srt.data(), sizeof(int32_t) * srt.size(), hipMemcpyHostToDevice));
-  if (int rc = dmalloc(&h->hub_tiles_sorted, stl.size())) return rc;
-  HIP_TRY(hipMemcpy(h->hub_tiles_sorted, stl.data(), sizeof(int4) * stl.size(), hipMemcpyHostToDevice));
-  h->h_hub_len.clear();
-  for (int32_t x : srt) h->h_hub_len.push_back(h->h_rowptr[x + 1] - h->h_rowptr[x]);
   return FU_OK;
 }
 
@@ -3077,9 +2944,8 @@ int ensure_transpose(fu_handle *h) {
     }
     if (int rc = dmalloc(&T.GBr[k], (size_t)E)) return rc;
   }
-  T.hist_hub = h->multi_geo[1][1];
   for (int p = 0; p < 2; ++p)
-    if (int rc = dmalloc(&T.hist[p], (size_t)(T.hist_hub + h->n_hub + 1))) return rc;
+    if (int rc = dmalloc(&T.hist[p], (size_t)(h->multi_geo[1][1] + 1))) return rc;
   T.P = (int)P;
   T.Q = (int)Q;
   T.NB = (int)br.size();
@@ -3112,9 +2978,6 @@ int lag_finalize(fu_handle *h, int p) {
   if (h->lag_nmulti[p])
     hipLaunchKernelGGL(k_lag_final, dim3(h->lag_nmulti[p]), dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0],
                        h->rowptr, h->f[p], Gb, h->tr.hist[p], a);
-  if (h->lag_hubs[p] && h->n_hub)
-    hipLaunchKernelGGL(k_lag_final, dim3(h->n_hub), dim3(kBlock), 0, h->stream, h->hub_sorted, h->rowptr, h->f[p], Gb,
-                       h->tr.hist[p] + h->tr.hist_hub, a);
   HIP_TRY(hipGetLastError());
   h->lagf[p] = 0;
   return FU_OK;
@@ -3212,34 +3075,6 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   return FU_OK;
 }
 
-// hub_blocks: deal the mega hubs (their slots in hub_sorted, longest first) to the least
-// loaded of P blocks
-int ensure_hub_plan(fu_handle *h) {
-  const int P = std::min(h->hub_blocks, std::max(h->n_hub, 1));
-  if (h->hub_plan && h->hub_plan_for == h->hub_blocks) return FU_OK;
-  if (h->hub_plan) hipFree(h->hub_plan);
-  if (h->hub_plan_off) hipFree(h->hub_plan_off);
-  h->hub_plan = h->hub_plan_off = nullptr;
-  std::vector<std::vector<int32_t>> per(P);
-  std::vector<int64_t> load(P, 0);
-  for (int q = 0; q < h->n_hub; ++q) {  // slots in hub_sorted, longest first
-    const int b = (int)(std::min_element(load.begin(), load.end()) - load.begin());
-    per[b].push_back(q);
-    load[b] += h->h_hub_len[q];
-  }
-  std::vector<int32_t> plan, off(1, 0);
-  for (const auto &v : per) {
-    plan.insert(plan.end(), v.begin(), v.end());
-    off.push_back((int32_t)plan.size());
-  }
-  if (int rc = dmalloc(&h->hub_plan, std::max<size_t>(1, plan.size()))) return rc;
-  if (int rc = dmalloc(&h->hub_plan_off, off.size())) return rc;
-  if (!plan.empty()) HIP_TRY(hipMemcpy(h->hub_plan, plan.data(), sizeof(int32_t) * plan.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->hub_plan_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
-  h->hub_plan_for = h->hub_blocks;
-  return FU_OK;
-}
-
 // Kernel 9: k_stage -> k_transpose (the mega-hub buckets first) -> kernel 4's tiles reading
 // the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
 // the remaining buckets and tiles.
@@ -3273,24 +3108,17 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   plan_alone(h, c);
   const int bh = hubs ? h->tr.Bh : 0;
   // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
-  // multi-row heavy rows, and the mega hubs when all of them run as multi-row blocks
-  int nbig = nmega;  // hub_multi: hubs longer than it keep a block each
-  if (h->hub_multi) {
-    nbig = 0;
-    while (nbig < nmega && h->h_hub_len[nbig] > h->hub_multi) ++nbig;
-  }
+  // multi-row heavy rows
   const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
   const int mend = h->multi_mid ? m1 : m0_;
   const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
   const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
   const bool lag_multi = h->lag && multi;
-  // hubs lagged: all as multi-row blocks (hub_multi) or in the persistent hub blocks
-  const bool lag_hub = h->lag && hubs && ((h->hub_multi && nbig == 0) || (h->hub_blocks && !h->hub_multi));
   const int p = r1;
-  if (h->lagf[p] && (h->lag_nmulti[p] != (lag_multi ? n_multi : 0) || h->lag_hubs[p] != (int)lag_hub)) {
+  if (h->lagf[p] && h->lag_nmulti[p] != (lag_multi ? n_multi : 0)) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
   }
-  const int lagm = (lag_multi || lag_hub) ? (h->lagf[p] ? 2 : 1) : 0;
+  const int lagm = lag_multi ? (h->lagf[p] ? 2 : 1) : 0;
   const bool pipe = h->tr_pipe && h->tr_bpx > 0;
   auto tr_launch = [&](int b0, int nb) {
     if (pipe && h->tr.H > kTrHotS)
@@ -3315,9 +3143,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
   };
   if (bh) tr_launch(0, bh);
-  if (hubs && h->hub_blocks && !h->hub_multi) {
-    if (int rc = ensure_hub_plan(h)) return rc;
-  }
   if (hubs) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
@@ -3341,41 +3166,15 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   if (side) HIP_TRY(hipEventRecord(h->ev_tr, h->stream));
   if (hubs) {
     auto chains = [&](auto C) {
-      // hub_multi: the hubs of <= hub_multi edges as k_heavy_multi blocks (kMR hubs of similar
-      // length per block, one chain wave: few blocks hold LDS beside the transposes); the
-      // longer ones keep a block each (deeper prefetch on their long chains)
-      if (h->hub_multi && nmega > nbig) {
-        auto hm = [&](auto L) {
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, false, decltype(L)::value>),
-                             dim3((nmega - nbig + kMR - 1) / kMR), dim3(kBlock), 0, h->stream2, h->hub_sorted + nbig,
-                             nmega - nbig, h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl,
-                             Gb, c.fm, Gb_old, h->tr.hist[p] + h->tr.hist_hub);
-        };
-        if (!lag_hub) hm(std::integral_constant<int, 0>{});
-        else if (lagm == 1) hm(std::integral_constant<int, 1>{});
-        else hm(std::integral_constant<int, 2>{});
-      }
-      if (nbig && h->hub_blocks && !h->hub_multi) {  // a few persistent one-wave blocks
-        auto hb = [&](auto L) {
-          hipLaunchKernelGGL((k_hub_chains<decltype(C)::value, decltype(L)::value>), dim3(std::min(h->hub_blocks, nmega)),
-                             dim3(64), 0, h->stream2, h->hub_plan, h->hub_plan_off, h->hub_sorted, h->rowptr, h->v,
-                             c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
-                             h->tr.hist[p] + h->tr.hist_hub, h->hub_prio);
-        };
-        if (!lag_hub) hb(std::integral_constant<int, 0>{});
-        else if (lagm == 1) hb(std::integral_constant<int, 1>{});
-        else hb(std::integral_constant<int, 2>{});
-      } else if (nbig)
-        hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nbig), dim3(kBlock),
-                           0, h->stream2, h->hub_multi ? h->hub_tiles_sorted : tl, h->rowptr, h->col, h->v, c.F, c.ap,
-                           c.ap2, c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1,
-                           Gb, c.fm, nullptr, nullptr, nullptr, h->hub_prio);
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
+                         0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm, nullptr, nullptr, nullptr,
+                         h->hub_prio);
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
-    if (!lag_hub)
-      hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
-                         (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
+    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
+                       (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
     if (side) {
       HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_tr, 0));
       auto st = [&](auto C) {
@@ -3411,7 +3210,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   auto tiles = [&](auto C) {
     if (multi) {
       auto hm = [&](auto L) {
-        hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, true, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
+        hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
                            dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
                            h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
                            h->tr.hist[p]);
@@ -3442,7 +3241,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     h->lagf[p] = 1;
     h->lag_round[p] = c.r;
     h->lag_nmulti[p] = lag_multi ? n_multi : 0;
-    h->lag_hubs[p] = (int)lag_hub;
   }
   return FU_OK;
 }
@@ -3881,7 +3679,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->tr_bpx = (int)value;
     return FU_OK;
   }
-  if (!std::strcmp(key, "lag")) {  // kernel 9: the multi-row heavy rows (and hubs) write f_r in round r + 2
+  if (!std::strcmp(key, "lag")) {  // kernel 9: the multi-row heavy rows write f_r in round r + 2
     const int lv = value != 0;
     if (lv != h->lag) {
       if (int rc = lag_finalize_all(h)) return rc;  // flows first, with the current G_B ring
@@ -3901,16 +3699,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "hub_prio")) {  // kernel 9: hub chain waves issue first on their SIMD (1)
     h->hub_prio = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_blocks")) {  // kernel 9: mega-hub chains in P persistent one-wave blocks (0: one per hub)
-    if (value < 0 || value > 65536) return fail(FU_ERR_ARG, "fu_set_option: hub_blocks must be in [0, 65536]");
-    h->hub_blocks = (int)value;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_multi")) {  // kernel 9: mega hubs of <= value edges many per chain wave (0: one per block)
-    if (value < 0 || value > INT32_MAX) return fail(FU_ERR_ARG, "fu_set_option: hub_multi must be in [0, 2^31)");
-    h->hub_multi = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
@@ -4380,8 +4168,7 @@ int fu_destroy(fu_handle *h) {
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
-                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->hub_sorted, h->hub_tiles_sorted, h->hub_plan,
-                              h->hub_plan_off, h->code[0], h->code[1], h->pctl,
+                              h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,
                               h->psample, h->st_tiles, h->st_heavy, h->stG, h->col16, h->cbase,
                               h->tnar_geo[0], h->tnar_geo[1], h->tnar_geo[2], h->tnar_geo[3]};
   free_transpose(h);

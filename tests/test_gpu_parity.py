@@ -626,9 +626,8 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "hubm", "hubm_all", "lag", "lag_hubm_all", "lag_hubm",
-                                   "hot", "hot_lag", "hot_pipe", "hot4k", "hubblocks", "hubblocks_lag_hot",
-                                   "prio", "side1", "side2_lag_hot_pipe", "split", "split_side1_lag_hot"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -645,48 +644,30 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("multi_mid", 0)
     elif multi == "pipe":
         eng.set_option("tr_pipe", 1)
-    elif multi == "hubm":  # mega hubs up to 2 * mega as multi-row chain blocks, longer ones alone
-        eng.set_option("hub_multi", 2 * mega)
-    elif multi == "hubm_all":
-        eng.set_option("hub_multi", 1 << 30)
-    elif multi == "lag":  # the multi-row heavy rows write f_r in round r + 2
-        eng.set_option("lag", 1)
-    elif multi == "lag_hubm_all":  # ... and every mega hub (all as multi-row blocks: no k_hub_flows)
-        eng.set_option("lag", 1)
-        eng.set_option("hub_multi", 1 << 30)
-    elif multi == "lag_hubm":  # hubs split: the longer ones keep k_hub_flows, none lagged
-        eng.set_option("lag", 1)
-        eng.set_option("hub_multi", 2 * mega)
+    elif multi == "nolag":  # the two-pass heavy rows (lag is the default)
+        eng.set_option("lag", 0)
     elif multi == "hot":  # neighbours of id < 10240 served from the transpose's LDS
         eng.set_option("tr_hot", 10240)
-    elif multi == "hot_lag":
+    elif multi == "hot_nolag":
         eng.set_option("tr_hot", 3000)
-        eng.set_option("lag", 1)
-        eng.set_option("hub_multi", 1 << 30)
+        eng.set_option("lag", 0)
+    elif multi == "hot_pipe":  # the pipelined transpose with the hot table
+        eng.set_option("tr_hot", 10240)
+        eng.set_option("tr_pipe", 1)
     elif multi == "hot4k":  # the small (32 KB) hot table
         eng.set_option("tr_hot", 4096)
-    elif multi == "hubblocks":  # mega-hub chains in 7 persistent one-wave blocks (several hubs each)
-        eng.set_option("hub_blocks", 7)
-        eng.set_option("hub_prio", 1)
-    elif multi == "prio":
+    elif multi == "prio":  # the hub chain waves at issue priority 3
         eng.set_option("hub_prio", 1)
     elif multi == "side1":  # light tiles on the side stream behind the hub path
         eng.set_option("side_tiles", 1)
+    elif multi == "side2_hot_pipe":  # ... and the rows of 129-256 edges
+        for key, val in (("side_tiles", 2), ("tr_hot", 5000), ("tr_pipe", 1), ("hub_prio", 1)):
+            eng.set_option(key, val)
     elif multi == "split":  # the heavy rows on a third stream once their buckets are transposed
         eng.set_option("split_tr", 1)
-    elif multi == "split_side1_lag_hot":
-        for key, val in (("split_tr", 1), ("side_tiles", 1), ("lag", 1), ("tr_hot", 3000), ("hub_prio", 1)):
+    elif multi == "split_side1_hot":
+        for key, val in (("split_tr", 1), ("side_tiles", 1), ("tr_hot", 3000), ("hub_prio", 1)):
             eng.set_option(key, val)
-    elif multi == "side2_lag_hot_pipe":  # ... and the rows of 129-256 edges
-        for key, val in (("side_tiles", 2), ("lag", 1), ("tr_hot", 5000), ("tr_pipe", 1), ("hub_prio", 1)):
-            eng.set_option(key, val)
-    elif multi == "hubblocks_lag_hot":
-        eng.set_option("hub_blocks", 3)
-        eng.set_option("lag", 1)
-        eng.set_option("tr_hot", 2000)
-    elif multi == "hot_pipe":  # tr_pipe has no hot lists: the layout keeps every neighbour staged
-        eng.set_option("tr_hot", 10240)
-        eng.set_option("tr_pipe", 1)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -967,29 +948,28 @@ def test_copy_bandwidth_plausible():
 
 
 def test_lag_flows_every_round_and_switches():
-    """Kernel 9's lag (the multi-row heavy rows and the mega hubs leave f_r to round r + 2):
-    the flows read after every round (fu_get_flows writes the lagged ones first) and the
-    rounds that continue after each read, the option switched off and on mid-run, hub_multi
-    changed mid-run (the lagged set changes: its flows are written first), and fu_reset, all
-    bitwise against the C oracle."""
+    """Kernel 9's lag (the multi-row heavy rows leave f_r to round r + 2): the flows read
+    after every round (fu_get_flows writes the lagged ones first) and the rounds that continue
+    after each read, a staging-layout rebuild mid-run, the option switched off and on, the
+    lagged set changed mid-run (its flows are written first), and fu_reset, all bitwise
+    against the C oracle."""
     g = fu.Graph.rmat(14, 16, seed=8)
     v = fu.uniform_values(g.n, seed=8)
     eng = fu.CollectAll(g, v, kernel="pregather", hub_threshold=16, layout="given")
     eng.set_option("mega_hub", 600)
     eng.set_option("lag", 1)
-    eng.set_option("hub_multi", 1 << 30)
     for r in range(1, 12):  # rounds 0 .. r-1 run: compare after each
         eng.run(1)
         a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, r, nthreads=16)
         assert np.array_equal(eng.estimates(), a_ref), r
         assert np.array_equal(eng.flows(), f_ref), r
     eng.run(5)
-    eng.set_option("hub_multi", 2 * 600)  # hubs no longer lagged (some keep a block each)
+    eng.set_option("tr_hot", 500)  # the staging layout is rebuilt: the lagged flows are written first
     eng.run(4)
     eng.set_option("lag", 0)
     eng.run(3)
     eng.set_option("lag", 1)
-    eng.set_option("hub_multi", 1 << 30)
+    eng.set_option("multi_mid", 0)  # the lagged set shrinks between two rounds of one parity
     eng.run(7)
     a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 11 + 5 + 4 + 3 + 7, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)

@@ -31,17 +31,11 @@ VARIANTS = {
     "pre_multi0": ("pregather", {"layout": "degree", "pack": 0, "multi_heavy": 0}),
     "pre_multimid0": ("pregather", {"layout": "degree", "pack": 0, "multi_mid": 0}),
     "pre_trpipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
-    "pre_hubm16k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 16384}),
-    "pre_hubm64k": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 65536}),
-    "pre_hubmall": ("pregather", {"layout": "degree", "pack": 0, "hub_multi": 1 << 30}),
     "pre_lag": ("pregather", {"layout": "degree", "pack": 0, "lag": 1}),
     "pre_hot": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240}),
     "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1}),
     "pre_hot4k_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096, "lag": 1}),
     "pre_hot4k": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096}),
-    "pre_hb256": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256}),
-    "pre_hb512": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 512}),
-    "pre_hb256_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1}),
     "pre_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1}),
     "pre_prio_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1}),
     "pre_prio_side2": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 2}),
@@ -49,24 +43,11 @@ VARIANTS = {
     "pre_prio_side1_hot_pipe": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1,
                                               "tr_hot": 10240, "tr_pipe": 1}),
     "pre_pipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
-    # one hub per one-wave block (hub_blocks >= hubs), lag: no k_hub_flows
-    "pre_hb4k_prio_lag_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096, "hub_prio": 1,
-                                              "lag": 1, "side_tiles": 1}),
-    "pre_hb4k_prio_lag_side1_split": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096, "hub_prio": 1,
-                                                    "lag": 1, "side_tiles": 1, "split_tr": 1}),
-    "pre_hb4k_prio_lag_side2_split_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 4096,
-                                                        "hub_prio": 1, "lag": 1, "side_tiles": 2, "split_tr": 1,
-                                                        "tr_hot": 10240}),
     "pre_prio_split": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1}),
     "pre_prio_split_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1, "side_tiles": 1}),
     "pre_prio_split_side1_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1,
                                                "side_tiles": 1, "tr_hot": 10240}),
     "pre_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "lag": 1}),
-    "pre_hb256_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1}),
-    "pre_hb256_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "hub_prio": 1, "lag": 1}),
-    "pre_hb256_lag_hot4k": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 4096}),
-    "pre_hb256_lag_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_blocks": 256, "lag": 1, "tr_hot": 10240}),
-    "pre_lag_hubmall": ("pregather", {"layout": "degree", "pack": 0, "lag": 1, "hub_multi": 1 << 30}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
