@@ -994,3 +994,49 @@ def test_lag_with_autotune_kernel_switches():
     a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 200, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
+
+
+CLASS_EDGE_DEGREES = [0, 1, 2, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 1023, 1024,
+                      1025, 2047, 2048, 2049, 4095, 4096, 4097, 8191, 8192, 8193, 12000]
+
+
+def _class_edge_graph(seed):
+    """Star centres of exactly the degrees above (each row class's first and last degree: heavy
+    rows at > 128, multi-row blocks at > 256, the register launch's 1024, the mega hubs at >
+    8192), their leaves drawn from a random background graph that never touches a centre."""
+    rng = np.random.default_rng(seed)
+    k, n_leaf = len(CLASS_EDGE_DEGREES), 16000
+    n = k + n_leaf
+    src, dst = [], []
+    for c, d in enumerate(CLASS_EDGE_DEGREES):
+        leaves = k + rng.choice(n_leaf, size=d, replace=False)
+        src.append(np.full(d, c))
+        dst.append(leaves)
+    m = 3 * n_leaf
+    src.append(k + rng.integers(0, n_leaf, m))
+    dst.append(k + rng.integers(0, n_leaf, m))
+    g = fu.Graph.from_edges(n, np.concatenate(src), np.concatenate(dst))
+    assert [int(x) for x in g.degrees[:k]] == CLASS_EDGE_DEGREES
+    return g
+
+
+@pytest.mark.parametrize("layout", ["given", "degree"])
+@pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
+                                         ("pregather", {}), ("pregather", {"lag": 0}),
+                                         ("pregather", {"multi_mid": 0, "tr_hot": 64})])
+def test_row_class_boundaries_bitwise(kernel, opts, layout):
+    """Rows of exactly the degree where each row class starts or ends, at the default
+    thresholds, every kernel, against the C oracle after every few rounds (the lagged flows
+    read back in between)."""
+    g = _class_edge_graph(7)
+    v = fu.uniform_values(g.n, seed=3)
+    eng = fu.CollectAll(g, v, kernel=kernel, layout=layout)
+    for key, val in opts.items():
+        eng.set_option(key, val)
+    done = 0
+    for k in (1, 2, 5, 9):
+        eng.run(k)
+        done += k
+        a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, done, nthreads=16)
+        assert np.array_equal(eng.estimates(), a_ref), done
+        assert np.array_equal(eng.flows(), f_ref), done

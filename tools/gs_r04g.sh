@@ -3,6 +3,8 @@
 set -o pipefail
 mkdir -p gpurun_out/er9
 export TMPDIR=/tmp
+# write -> read-back round trips against the Infinity Cache
+timeout -k 10 120 tools/bin/ubench_mall > gpurun_out/er9/ubench_mall.log 2>&1 || exit $?
 # the driver's command, and its kernel trace
 timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > gpurun_out/er9/bench_driver_cmd.log 2>&1 || exit $?
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/er9/prof_driver -o run -- python3 bench.py --gpus 1 --steps 20 --warmup 5 --cpu-seconds 0 > gpurun_out/er9/prof_driver.log 2>&1 || exit $?
