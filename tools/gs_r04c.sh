@@ -1,4 +1,6 @@
 # round 4, GPU session c: persistent hub-chain blocks (hub_blocks), with and without lag / tr_hot
+# (record of a measured session: hub_multi / hub_blocks were removed after it lost, so its
+# variants naming them no longer exist in tools/sweep.py or the engine)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

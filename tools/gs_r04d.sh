@@ -1,4 +1,6 @@
 # round 4, GPU session d: hub chain waves at issue priority (hub_prio), with lag and hub_blocks
+# (record of a measured session: hub_multi / hub_blocks were removed after it lost, so its
+# variants naming them no longer exist in tools/sweep.py or the engine)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -1,4 +1,6 @@
 # round 4, GPU session f: one hub per one-wave block with lag (no k_hub_flows), side tiles, split transposes
+# (record of a measured session: hub_multi / hub_blocks were removed after it lost, so its
+# variants naming them no longer exist in tools/sweep.py or the engine)
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
