@@ -1398,6 +1398,25 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   }
 }
 
+// The isolated rows at the end of the degree layout (fused layouts): a_r = ((v - 0.0) +
+// 0.0) / 1 (CA:106-113 with no neighbours), as the light tiles compute it.
+__global__ __launch_bounds__(kBlock) void k_isolated(int i0, int n, const double *__restrict__ v,
+                                                     double *__restrict__ a_new, const double *__restrict__ target,
+                                                     unsigned long long *__restrict__ err, void *__restrict__ code_new,
+                                                     PackCtl *__restrict__ ctl, int rslot, int check) {
+  const PackCtl pc = ctl[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
+  const int i = i0 + blockIdx.x * kBlock + threadIdx.x;
+  unsigned long long eb = 0;
+  if (i < n) {
+    const double a = ((v[i] - 0.0) + 0.0) / (double)1;
+    st_wt(a_new + i, a);
+    if (pc.width) put_code(pc, code_new, i, a);
+    if (check) eb = err_bits(a, target[i]);
+  }
+  if (check) block_max_to(eb, err);
+}
+
 // Kernel 9 option "fuse": the rows of at most 128 / 256 / 1024 edges (fuse 1 / 2 / 3; a
 // suffix of the rows under the degree layout) take their estimates straight from the
 // transpose's LDS instead of through G_B. Their buckets are row-aligned (at most kFuBE edges
@@ -1409,8 +1428,9 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
 constexpr int kFuBE = 4096;       // edges per fused bucket (u16 positions)
 constexpr int kFuBN = 512;        // rows per fused bucket: one per thread in the row phase
 constexpr int kFuThreads = 512;   // two blocks per CU in 79 KB of LDS each
-template <bool CHECK>
-__global__ __launch_bounds__(kFuThreads) void k_fused_rows(
+constexpr int kFuLong = 64;       // rows of more edges run their chains on a whole wave
+template <bool CHECK, int SPT>  // SPT: slices per thread (P <= SPT x kFuThreads)
+__global__ __launch_bounds__(kFuThreads, 4) void k_fused_rows(
     int b0, int nbk, int P, const int *__restrict__ bst, const int *__restrict__ bnode,
     const int *__restrict__ offT, const double *__restrict__ GA, const unsigned short *__restrict__ pos16,
     const int *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ F,
@@ -1419,8 +1439,13 @@ __global__ __launch_bounds__(kFuThreads) void k_fused_rows(
     int fm) {
   const PackCtl pc = ctl[2];  // packing of a_r (the table written here)
   if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
-  __shared__ double s_v[kFuBE];  // a_{r-1}[col e] in edge order
+  // a_{r-1}[col e] in edge order, one double off s_x's banks (the long rows' chains read
+  // s_x[q] and s_v[q] in the same instruction)
+  __shared__ double s_v_buf[kFuBE + 1];
+  double *const s_v = s_v_buf + 1;
   __shared__ double s_x[kFuBE];  // f_{r-2} on load, fr after the row phase
+  __shared__ int s_long[kFuBE / (kFuLong + 1) + 1];  // the bucket's rows of > kFuLong edges
+  __shared__ int s_nlong;
   // the run tables are dead once the bucket's loads are issued: the row phase reuses them
   __shared__ union {
     struct {
@@ -1441,7 +1466,6 @@ __global__ __launch_bounds__(kFuThreads) void k_fused_rows(
   int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
   unsigned long long eb = 0;
-  constexpr int SPT = kTrMaxP / kFuThreads;  // slices per thread: 4t .. 4t + 3
   constexpr int kPerT = kFuBE / kFuThreads;
   int o[SPT], len[SPT];
   auto load_runs = [&](int bkk) {
@@ -1499,75 +1523,135 @@ __global__ __launch_bounds__(kFuThreads) void k_fused_rows(
     }
     if (t == 0) s_u.t.c[kFuBE / 64] = P;
     __syncthreads();
-    int g[kPerT];
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k) {
-      const int m = t + k * kFuThreads;
-      g[k] = -1;
-      if (m < nst) {
-        int lo = s_u.t.c[m >> 6], hi = s_u.t.c[(m >> 6) + 1];
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_u.t.m[mid] > m) hi = mid; else lo = mid + 1;
-        }
-        const int run = lo - 1;
-        g[k] = s_u.t.o[run] + (m - s_u.t.m[run]);
-      }
-    }
-    // every load of the bucket in flight at once: staged estimates, positions, old flows,
-    // the rows' words
-    double val[kPerT], fx[kPerT];
-    unsigned short pos[kPerT];
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k) {
-      val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
-      pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
-      const int q = t + k * kFuThreads;
-      fx[k] = (q < ne && !fm) ? ld_f(F, e0 + q) : 0.0;
-    }
+    // the rows' words first, then the bucket's loads in two halves (searches, staged
+    // estimates, positions, old flows; scattered into s_v / s_x as they land)
     const int rp = t < nn ? rowptr[nb + t] - e0 : 0;
     const int rp_end = t == 0 ? rowptr[nb + nn] - e0 : 0;  // (nn may equal the thread count)
     const double vv = t < nn ? v[nb + t] : 0.0, own2 = t < nn ? a_prev2[nb + t] : 0.0;
-    const int next = bk + nj;
-    if (next < bend) load_runs(next);  // in flight beside this bucket's loads
-    __syncthreads();  // the searches are done with the run tables
+    unsigned fhi[kPerT];  // f_{r-2}'s high words: the flow store skips an unchanged one (st_f)
 #pragma unroll
-    for (int k = 0; k < kPerT; ++k) {
-      const int q = t + k * kFuThreads;
-      if (g[k] >= 0) s_v[pos[k]] = val[k];
-      if (q < ne) s_x[q] = fx[k];
-    }
-    if (t < nn) s_rp[t] = (unsigned short)rp;
-    if (t == 0) s_rp[nn] = (unsigned short)rp_end;
-    __syncthreads();
-    // rows: one per thread, the exact left-to-right sums (CA:106-113)
-    if (t < nn) {
-      const int qb = s_rp[t], qe = s_rp[t + 1];
-      double S = 0.0, T = 0.0;
-      const double fo0 = fm ? old_flow(fm, own2) : 0.0;
-      for (int q = qb; q < qe; ++q) {
-        const double er = s_v[q];
-        const double fr = recon_fr(fm ? fo0 : s_x[q], er, own2);
-        s_x[q] = fr;
-        s_u.r.own[q] = (unsigned short)t;
-        S = S + fr;
-        T = T + er;
+    for (int h2 = 0; h2 < 2; ++h2) {
+      constexpr int HK = kPerT / 2;
+      int g[HK];
+#pragma unroll
+      for (int u = 0; u < HK; ++u) {
+        const int m = t + (h2 * HK + u) * kFuThreads;
+        g[u] = -1;
+        if (m < nst) {
+          int lo = s_u.t.c[m >> 6], hi = s_u.t.c[(m >> 6) + 1];
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_u.t.m[mid] > m) hi = mid; else lo = mid + 1;
+          }
+          const int run = lo - 1;
+          g[u] = s_u.t.o[run] + (m - s_u.t.m[run]);
+        }
       }
-      const double a = ((vv - S) + T) / (double)(qe - qb + 1);
-      s_u.r.a[t] = a;
-      st_wt(a_new + nb + t, a);
-      if (pc.width) put_code(pc, code_new, nb + t, a);
+      double val[HK], fx[HK];
+      unsigned short pos[HK];
+#pragma unroll
+      for (int u = 0; u < HK; ++u) {
+        val[u] = g[u] >= 0 ? GA[g[u]] : 0.0;
+        pos[u] = g[u] >= 0 ? pos16[g[u]] : (unsigned short)0;
+        const int q = t + (h2 * HK + u) * kFuThreads;
+        fx[u] = (q < ne && !fm) ? ld_f(F, e0 + q) : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < HK; ++u) {
+        const int q = t + (h2 * HK + u) * kFuThreads;
+        if (g[u] >= 0) s_v[pos[u]] = val[u];
+        if (q < ne) s_x[q] = fx[u];
+        fhi[h2 * HK + u] = (unsigned)__double2hiint(fx[u]);
+      }
+    }
+    const int next = bk + nj;
+    if (next < bend) load_runs(next);  // in flight while this bucket's rows run
+    if (t < nn) s_rp[t] = (unsigned short)rp;
+    if (t == 0) {
+      s_rp[nn] = (unsigned short)rp_end;
+      s_nlong = 0;
+    }
+    __syncthreads();  // the searches are done with the run tables; s_v, s_x, s_rp complete
+    // rows of <= kFuLong edges: one per thread, the exact left-to-right sums (CA:106-113),
+    // four elements' LDS reads in flight at a time; longer rows are listed for the waves
+    auto finish_row = [&](int r, double S, double T, int d, double vr) {
+      const double a = ((vr - S) + T) / (double)(d + 1);
+      s_u.r.a[r] = a;
+      st_wt(a_new + nb + r, a);
+      if (pc.width) put_code(pc, code_new, nb + r, a);
       if (CHECK) {
-        const unsigned long long x = err_bits(a, target[nb + t]);
+        const unsigned long long x = err_bits(a, target[nb + r]);
         eb = x > eb ? x : eb;
       }
+    };
+    if (t < nn) {
+      const int qb = s_rp[t], qe = s_rp[t + 1];
+      if (qe - qb > kFuLong) {
+        s_long[atomicAdd(&s_nlong, 1)] = t;  // (any order: rows are independent)
+      } else {
+        double S = 0.0, T = 0.0;
+        const double fo0 = fm ? old_flow(fm, own2) : 0.0;
+        int q = qb;
+        for (; q + 4 <= qe; q += 4) {
+          double er[4], fr[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            er[u] = s_v[q + u];
+            fr[u] = fm ? fo0 : s_x[q + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            fr[u] = recon_fr(fr[u], er[u], own2);
+            s_x[q + u] = fr[u];
+            s_u.r.own[q + u] = (unsigned short)t;
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            S = S + fr[u];
+            T = T + er[u];
+          }
+        }
+        for (; q < qe; ++q) {
+          const double er = s_v[q];
+          const double fr = recon_fr(fm ? fo0 : s_x[q], er, own2);
+          s_x[q] = fr;
+          s_u.r.own[q] = (unsigned short)t;
+          S = S + fr;
+          T = T + er;
+        }
+        finish_row(t, S, T, qe - qb, vv);
+      }
+    }
+    __syncthreads();
+    // rows of > kFuLong edges: one per wave, fr rebuilt by the lanes, then the exact chains on
+    // even / odd lanes (chain_sum)
+    for (int k = w; k < s_nlong; k += kFuThreads / 64) {
+      const int r = s_long[k];
+      const int qb = s_rp[r], qe = s_rp[r + 1], d = qe - qb;
+      const double vr = v[nb + r], o2 = a_prev2[nb + r];
+      const double fo0 = fm ? old_flow(fm, o2) : 0.0;
+      for (int q = qb + lane; q < qe; q += 64) {
+        s_x[q] = recon_fr(fm ? fo0 : s_x[q], s_v[q], o2);
+        s_u.r.own[q] = (unsigned short)r;
+      }
+      wave_sync();
+      double S = 0.0, T = 0.0;
+      chain_sum<4>(s_x + qb, s_v + qb, d, S, T);  // (4-element batches: two blocks per CU)
+      if (lane == 0) finish_row(r, S, T, d, vr);
+      wave_sync();
     }
     __syncthreads();
     // new flows, coalesced, in place (CA:117-118)
 #pragma unroll
     for (int k = 0; k < kPerT; ++k) {
       const int q = t + k * kFuThreads;
-      if (q < ne) st_fo(F, e0 + q, (s_x[q] + s_u.r.a[s_u.r.own[q]]) - s_v[q], fx[k], fm);
+      if (q < ne) {
+        const double f = (s_x[q] + s_u.r.a[s_u.r.own[q]]) - s_v[q];
+        unsigned *wd = reinterpret_cast<unsigned *>(F);
+        const long long i = fhi_idx(e0 + q);
+        st_wt(wd + i + 32, (unsigned)__double2loint(f));
+        if (fm || (unsigned)__double2hiint(f) != fhi[k]) st_wt(wd + i, (unsigned)__double2hiint(f));
+      }
     }
     __syncthreads();  // the next bucket rewrites the tables and s_v / s_x
     bk = next;
@@ -2654,6 +2738,7 @@ struct fu_handle {
     int *bnode = nullptr;                 // B - Bf + 1: first row of each fused bucket
     int fuse = 0;                         // the fuse mode the layout was built for (0: none)
     int fkey = 0;                         // fuse_key() it was built under
+    int iso0 = 0;                         // fuse: rows [iso0, n) are isolated (k_isolated)
   };
   TransLayout tr;
   bool tr_ready = false;
@@ -3100,13 +3185,17 @@ int ensure_transpose(fu_handle *h) {
   std::vector<int32_t> bst, bnode;
   for (int64_t e = 0; e < e_f; e += kTrBE) bst.push_back((int32_t)e);
   const int64_t Bf = (int64_t)bst.size();
-  for (int32_t i = i_f; i < h->n;) {  // greedy: whole rows, <= kFuBE edges, <= kFuBN rows
+  // the isolated rows at the end (the degree layout's last rows) go to k_isolated
+  int32_t i_0 = h->n;
+  if (fmode)
+    while (i_0 > i_f && h->h_rowptr[i_0] == h->h_rowptr[i_0 - 1]) --i_0;
+  for (int32_t i = i_f; i < i_0;) {  // greedy: whole rows, <= kFuBE edges, <= kFuBN rows
     const int32_t b = i;
-    while (i < h->n && i - b < kFuBN && h->h_rowptr[i + 1] - h->h_rowptr[b] <= kFuBE) ++i;
+    while (i < i_0 && i - b < kFuBN && h->h_rowptr[i + 1] - h->h_rowptr[b] <= kFuBE) ++i;
     bst.push_back((int32_t)h->h_rowptr[b]);
     bnode.push_back(b);
   }
-  bnode.push_back(h->n);
+  bnode.push_back(i_0);
   if (bst.empty()) bst.push_back(0);
   const int64_t B = (int64_t)bst.size();
   bst.push_back((int32_t)E);
@@ -3169,6 +3258,7 @@ int ensure_transpose(fu_handle *h) {
   if (int rc = up(&T.bst, bst.data(), bst.size())) return rc;
   if (int rc = up(&T.bnode, bnode.data(), bnode.size())) return rc;
   T.Bf = (int)Bf;
+  T.iso0 = i_0;
   T.fuse = fmode;
   T.fkey = fuse_key(h);
   T.H = H;
@@ -3406,17 +3496,23 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   }
   const bool chk = c.err != nullptr;
   auto fused = [&]() {
-    if (!fz || h->tr.B <= bf) return;
+    if (!fz) return;
+    if (h->tr.iso0 < h->n)
+      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->tr.iso0)), dim3(kBlock), 0, h->stream, h->tr.iso0, h->n,
+                         h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1, chk ? 1 : 0);
+    if (h->tr.B <= bf) return;
     const int nbk = h->tr.B - bf, per = (nbk + 7) / 8;
     const unsigned grid = 8u * (unsigned)std::min(per, 2 * std::max(1, h->n_cu / 8));
-    if (chk)
-      hipLaunchKernelGGL(k_fused_rows<true>, dim3(grid), dim3(kFuThreads), 0, h->stream, bf, nbk, h->tr.P, h->tr.bst,
-                         h->tr.bnode, h->tr.offT, h->tr.GA, h->tr.pos16, h->rowptr, h->v, c.F, c.ap2, c.an, h->target,
-                         c.err, h->code[r1], h->pctl, r1, c.fm);
-    else
-      hipLaunchKernelGGL(k_fused_rows<false>, dim3(grid), dim3(kFuThreads), 0, h->stream, bf, nbk, h->tr.P, h->tr.bst,
-                         h->tr.bnode, h->tr.offT, h->tr.GA, h->tr.pos16, h->rowptr, h->v, c.F, c.ap2, c.an, h->target,
-                         c.err, h->code[r1], h->pctl, r1, c.fm);
+    auto go = [&](auto C, auto SP) {
+      hipLaunchKernelGGL((k_fused_rows<decltype(C)::value, decltype(SP)::value>), dim3(grid), dim3(kFuThreads), 0,
+                         h->stream, bf, nbk, h->tr.P, h->tr.bst, h->tr.bnode, h->tr.offT, h->tr.GA, h->tr.pos16,
+                         h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
+    };
+    const bool p2 = h->tr.P <= 2 * kFuThreads;
+    if (chk && p2) go(std::true_type{}, std::integral_constant<int, 2>{});
+    else if (chk) go(std::true_type{}, std::integral_constant<int, kTrMaxP / kFuThreads>{});
+    else if (p2) go(std::false_type{}, std::integral_constant<int, 2>{});
+    else go(std::false_type{}, std::integral_constant<int, kTrMaxP / kFuThreads>{});
   };
   if (!h->fuse_late) fused();
   // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
