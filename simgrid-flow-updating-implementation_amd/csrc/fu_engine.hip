@@ -1425,12 +1425,29 @@ __global__ __launch_bounds__(kBlock) void k_isolated(int i0, int n, const double
 // coalesced, one thread per row reconstructs fr and sums in row order, CA:106-113, then
 // the new flows coalesced, CA:117-118). Per fused edge that saves G_B's 8-byte store and
 // 8-byte load, and the light-tile launches. Same operations in the same order: same bits.
-constexpr int kFuBE = 4096;       // edges per fused bucket (u16 positions)
-constexpr int kFuBN = 512;        // rows per fused bucket: one per thread in the row phase
-constexpr int kFuThreads = 512;   // two blocks per CU in 79 KB of LDS each
+#ifndef FU_FUBE
+#define FU_FUBE 4096
+#endif
+#ifndef FU_FUTH
+#define FU_FUTH 512
+#endif
+#ifndef FU_FUBPC
+#define FU_FUBPC 2
+#endif
+#ifndef FU_FZ_DIAG
+#define FU_FZ_DIAG 0  // timing-only experiment builds: 1 = no row phase and no flow stores
+#endif
+constexpr int kFuBE = FU_FUBE;       // edges per fused bucket (u16 positions)
+constexpr int kFuThreads = FU_FUTH;  // two blocks per CU in 79 KB of LDS each
+constexpr int kFuBN = kFuThreads;    // rows per fused bucket: one per thread in the row phase
+constexpr int kFuBPC = FU_FUBPC;     // blocks per CU the launch assumes
+#ifndef FU_FUMAXP
+#define FU_FUMAXP 2048
+#endif
+constexpr int kFuMaxP = FU_FUMAXP;   // slices a fused layout may have (run tables in LDS)
 constexpr int kFuLong = 64;       // rows of more edges run their chains on a whole wave
 template <bool CHECK, int SPT>  // SPT: slices per thread (P <= SPT x kFuThreads)
-__global__ __launch_bounds__(kFuThreads, 4) void k_fused_rows(
+__global__ __launch_bounds__(kFuThreads, kFuBPC * kFuThreads / 256) void k_fused_rows(
     int b0, int nbk, int P, const int *__restrict__ bst, const int *__restrict__ bnode,
     const int *__restrict__ offT, const double *__restrict__ GA, const unsigned short *__restrict__ pos16,
     const int *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ F,
@@ -1449,8 +1466,8 @@ __global__ __launch_bounds__(kFuThreads, 4) void k_fused_rows(
   // the run tables are dead once the bucket's loads are issued: the row phase reuses them
   __shared__ union {
     struct {
-      unsigned short m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
-      int o[kTrMaxP];                 // G_A index of each run
+      unsigned short m[kFuMaxP + 1];  // first element (bucket order) of each slice's run
+      int o[kFuMaxP];                 // G_A index of each run
       int c[kFuBE / 64 + 1];          // coarse table
     } t;
     struct {
@@ -1572,6 +1589,12 @@ __global__ __launch_bounds__(kFuThreads, 4) void k_fused_rows(
       s_nlong = 0;
     }
     __syncthreads();  // the searches are done with the run tables; s_v, s_x, s_rp complete
+    if (FU_FZ_DIAG == 1) {
+      if (t == 0) st_wt(a_new + nb, s_v[0] + s_x[0]);  // keeps the loads
+      __syncthreads();
+      bk = next;
+      continue;
+    }
     // rows of <= kFuLong edges: one per thread, the exact left-to-right sums (CA:106-113),
     // four elements' LDS reads in flight at a time; longer rows are listed for the waves
     auto finish_row = [&](int r, double S, double T, int d, double vr) {
@@ -3174,7 +3197,7 @@ int ensure_transpose(fu_handle *h) {
       ++cnt;
       mx = std::max<int64_t>(mx, h->h_hrows[h->multi_geo[1][0] + q]);
     }
-    bool ok = mx == cnt - 1 && cnt < h->n;
+    bool ok = mx == cnt - 1 && cnt < h->n && P <= kFuMaxP;
     for (int32_t i = (int32_t)cnt; ok && i < h->n; ++i) ok = h->h_rowptr[i + 1] - h->h_rowptr[i] <= kFuBE;
     if (ok) {
       i_f = (int32_t)cnt;
@@ -3502,17 +3525,18 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                          h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1, chk ? 1 : 0);
     if (h->tr.B <= bf) return;
     const int nbk = h->tr.B - bf, per = (nbk + 7) / 8;
-    const unsigned grid = 8u * (unsigned)std::min(per, 2 * std::max(1, h->n_cu / 8));
+    const unsigned grid = 8u * (unsigned)std::min(per, kFuBPC * std::max(1, h->n_cu / 8));
     auto go = [&](auto C, auto SP) {
       hipLaunchKernelGGL((k_fused_rows<decltype(C)::value, decltype(SP)::value>), dim3(grid), dim3(kFuThreads), 0,
                          h->stream, bf, nbk, h->tr.P, h->tr.bst, h->tr.bnode, h->tr.offT, h->tr.GA, h->tr.pos16,
                          h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
     };
+    constexpr int kS = (kFuMaxP + kFuThreads - 1) / kFuThreads;  // slices per thread at kFuMaxP
     const bool p2 = h->tr.P <= 2 * kFuThreads;
     if (chk && p2) go(std::true_type{}, std::integral_constant<int, 2>{});
-    else if (chk) go(std::true_type{}, std::integral_constant<int, kTrMaxP / kFuThreads>{});
+    else if (chk) go(std::true_type{}, std::integral_constant<int, (kS > 2 ? kS : 2)>{});
     else if (p2) go(std::false_type{}, std::integral_constant<int, 2>{});
-    else go(std::false_type{}, std::integral_constant<int, kTrMaxP / kFuThreads>{});
+    else go(std::false_type{}, std::integral_constant<int, (kS > 2 ? kS : 2)>{});
   };
   if (!h->fuse_late) fused();
   // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
