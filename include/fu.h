@@ -133,12 +133,6 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 side stream behind the hub path once every bucket is transposed (default 0).
  * "split_tr"      kernel 9: the multi-row heavy rows on a third stream once their own buckets
  *                 are transposed (default 0).
- * "fuse"          kernel 9: the rows of <= 128 (1), 256 (2) or 1024 (3) edges read their
- *                 estimates from the transpose's LDS in row-aligned buckets (k_fused_rows),
- *                 never through G_B (default 0). Needs those rows to be the last rows (the
- *                 degree layout); otherwise the layout is built without (fu_get_info [21]).
- *                 tr_hot is ignored while it is on. "fuse_late" 1: k_fused_rows after the
- *                 heavy rows instead of before them.
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).
@@ -181,8 +175,7 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done);
  * [3] = rounds done, [4]/[5] = kernel 4 tile geometry (edges / nodes), [6] = autotune
  * passes, [7] = packing width of the last pass, [8..12] = the last pass's ns per round for
  * its candidates (kernel 4 at 2048x256, kernel 4 at 512x64, kernel 8, kernel 4 at
- * 1024x128, kernel 9; 0 = not run), [20] = mega hubs, [21] = kernel 9's fuse mode in effect
- * (-1 = no kernel 9 layout built), [22] = its fused buckets, [23..26] = the autotune winner per
+ * 1024x128, kernel 9; 0 = not run), [20] = mega hubs, [23..26] = the autotune winner per
  * packing width 0, 8, 16, 32 (kernel * 10 + kernel-4 geometry index, -1 = not tuned yet),
  * [27..30] = kernel 8 slices per layout (element bytes 1, 2, 4, 8; 0 = not built).
  * With kernel "auto" (the default) fu_tune, or a run with enough rounds left, times the

@@ -43,19 +43,18 @@ __device__ inline unsigned long long err_bits(double a, double t) {
   return (unsigned long long)__double_as_longlong(fabs(a - t));
 }
 
-template <int NT = kBlock>  // threads per block
 __device__ inline void block_max_to(unsigned long long x, unsigned long long *dst) {
   for (int off = 32; off > 0; off >>= 1) {
     unsigned long long y = __shfl_xor(x, off, 64);
     x = x > y ? x : y;
   }
-  __shared__ unsigned long long s_w[NT / 64];
+  __shared__ unsigned long long s_w[kBlock / 64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   if (lane == 0) s_w[w] = x;
   __syncthreads();
   if (threadIdx.x == 0) {
     unsigned long long m = s_w[0];
-    for (int k = 1; k < NT / 64; ++k) m = m > s_w[k] ? m : s_w[k];
+    for (int k = 1; k < kBlock / 64; ++k) m = m > s_w[k] ? m : s_w[k];
     // a plain read first: only blocks that raise the running max issue the atomic (a stale
     // read only costs an extra atomic, never a wrong max). Without it 16K blocks serialise
     // on one address.
@@ -1080,8 +1079,7 @@ constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 #define FU_TR_WAVES 1
 #endif
 template <int HOTN>  // LDS capacity of the hot table (0: no hot neighbours)
-__global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P,
-                                                        const int *__restrict__ bst,
+__global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
@@ -1120,8 +1118,8 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   load_runs(bk, o, len);
   for (;;) {
   const int bb = b0 + bk;
-  const long long e0 = bst[bb];
-  const int ne = bst[bb + 1] - bst[bb];
+  const long long e0 = (long long)bb * kTrBE;
+  const int ne = (int)min((long long)kTrBE, E - e0);
   // exclusive scan of len0 + len1 over the block: wave shuffles, then the 16 wave totals
   int x = len[0] + len[1];
 #pragma unroll
@@ -1228,8 +1226,7 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
 // k_transpose; HOTN as k_transpose (the hot edges' list entries are loaded with the bucket's
 // other loads, their values read from the block's LDS copy of a_{r-1}[0, H)).
 template <int HOTN>
-__global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, int P,
-                                                             const int *__restrict__ bst,
+__global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, int P, long long E,
                                                              const int *__restrict__ offT,
                                                              const double *__restrict__ GA,
                                                              const unsigned short *__restrict__ pos16,
@@ -1348,8 +1345,8 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   // bucket cur: the loads in (val, pos) -> s_v by position -> G_B, coalesced
   auto finish = [&](int cur, const double (&val)[kPerT], const int (&pos)[kPerT], const unsigned (&hx)[2],
                     const int (&hr)[2]) {
-    const long long e0 = bst[b0 + cur];
-    const int ne = bst[b0 + cur + 1] - bst[b0 + cur];
+    const long long e0 = (long long)(b0 + cur) * kTrBE;
+    const int ne = (int)min((long long)kTrBE, E - e0);
     __syncthreads();  // the previous bucket's G_B stores have read s_v
 #pragma unroll
     for (int k = 0; k < kPerT; ++k)
@@ -1396,290 +1393,6 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
     if (!step(bk, gA, vA, pA, hxA, hrA, vB, pB, hxB, hrB)) break;
     bk += nj;
   }
-}
-
-// The isolated rows at the end of the degree layout (fused layouts): a_r = ((v - 0.0) +
-// 0.0) / 1 (CA:106-113 with no neighbours), as the light tiles compute it.
-__global__ __launch_bounds__(kBlock) void k_isolated(int i0, int n, const double *__restrict__ v,
-                                                     double *__restrict__ a_new, const double *__restrict__ target,
-                                                     unsigned long long *__restrict__ err, void *__restrict__ code_new,
-                                                     PackCtl *__restrict__ ctl, int rslot, int check) {
-  const PackCtl pc = ctl[2];
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
-  const int i = i0 + blockIdx.x * kBlock + threadIdx.x;
-  unsigned long long eb = 0;
-  if (i < n) {
-    const double a = ((v[i] - 0.0) + 0.0) / (double)1;
-    st_wt(a_new + i, a);
-    if (pc.width) put_code(pc, code_new, i, a);
-    if (check) eb = err_bits(a, target[i]);
-  }
-  if (check) block_max_to(eb, err);
-}
-
-// Kernel 9 option "fuse": the rows of at most 128 / 256 / 1024 edges (fuse 1 / 2 / 3; a
-// suffix of the rows under the degree layout) take their estimates straight from the
-// transpose's LDS instead of through G_B. Their buckets are row-aligned (at most kFuBE edges
-// and kFuBN rows, bst / bnode); a block transposes a bucket into LDS as k_transpose does and
-// then runs the light-tile round on it (k_round_recon's light tile: f_{r-2} staged
-// coalesced, one thread per row reconstructs fr and sums in row order, CA:106-113, then
-// the new flows coalesced, CA:117-118). Per fused edge that saves G_B's 8-byte store and
-// 8-byte load, and the light-tile launches. Same operations in the same order: same bits.
-#ifndef FU_FUBE
-#define FU_FUBE 4096
-#endif
-#ifndef FU_FUTH
-#define FU_FUTH 512
-#endif
-#ifndef FU_FUBPC
-#define FU_FUBPC 2
-#endif
-#ifndef FU_FZ_DIAG
-#define FU_FZ_DIAG 0  // timing-only experiment builds: 1 = no row phase and no flow stores
-#endif
-constexpr int kFuBE = FU_FUBE;       // edges per fused bucket (u16 positions)
-constexpr int kFuThreads = FU_FUTH;  // two blocks per CU in 79 KB of LDS each
-constexpr int kFuBN = kFuThreads;    // rows per fused bucket: one per thread in the row phase
-constexpr int kFuBPC = FU_FUBPC;     // blocks per CU the launch assumes
-#ifndef FU_FUMAXP
-#define FU_FUMAXP 2048
-#endif
-constexpr int kFuMaxP = FU_FUMAXP;   // slices a fused layout may have (run tables in LDS)
-constexpr int kFuLong = 64;       // rows of more edges run their chains on a whole wave
-template <bool CHECK, int SPT>  // SPT: slices per thread (P <= SPT x kFuThreads)
-__global__ __launch_bounds__(kFuThreads, kFuBPC * kFuThreads / 256) void k_fused_rows(
-    int b0, int nbk, int P, const int *__restrict__ bst, const int *__restrict__ bnode,
-    const int *__restrict__ offT, const double *__restrict__ GA, const unsigned short *__restrict__ pos16,
-    const int *__restrict__ rowptr, const double *__restrict__ v, double *__restrict__ F,
-    const double *__restrict__ a_prev2, double *__restrict__ a_new, const double *__restrict__ target,
-    unsigned long long *__restrict__ err, void *__restrict__ code_new, PackCtl *__restrict__ ctl, int rslot,
-    int fm) {
-  const PackCtl pc = ctl[2];  // packing of a_r (the table written here)
-  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
-  // a_{r-1}[col e] in edge order, one double off s_x's banks (the long rows' chains read
-  // s_x[q] and s_v[q] in the same instruction)
-  __shared__ double s_v_buf[kFuBE + 1];
-  double *const s_v = s_v_buf + 1;
-  __shared__ double s_x[kFuBE];  // f_{r-2} on load, fr after the row phase
-  __shared__ int s_long[kFuBE / (kFuLong + 1) + 1];  // the bucket's rows of > kFuLong edges
-  __shared__ int s_nlong;
-  // the run tables are dead once the bucket's loads are issued: the row phase reuses them
-  __shared__ union {
-    struct {
-      unsigned short m[kFuMaxP + 1];  // first element (bucket order) of each slice's run
-      int o[kFuMaxP];                 // G_A index of each run
-      int c[kFuBE / 64 + 1];          // coarse table
-    } t;
-    struct {
-      unsigned short own[kFuBE];  // row (in the bucket) of each edge
-      double a[kFuBN];            // a_r of the bucket's rows
-    } r;
-  } s_u;
-  __shared__ unsigned short s_rp[kFuBN + 1];
-  __shared__ int s_w[kFuThreads / 64];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int per = (nbk + 7) >> 3;
-  const int nj = (int)(gridDim.x >> 3);
-  int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
-  unsigned long long eb = 0;
-  constexpr int kPerT = kFuBE / kFuThreads;
-  int o[SPT], len[SPT];
-  auto load_runs = [&](int bkk) {
-    const int bb = b0 + bkk;
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) {
-      const int sl = SPT * t + j;
-      o[j] = sl < P ? offT[(long long)bb * P + sl] : 0;
-      len[j] = sl < P ? offT[(long long)(bb + 1) * P + sl] - o[j] : 0;
-    }
-  };
-  if (bk < bend) load_runs(bk);
-  while (bk < bend) {
-    const int bb = b0 + bk;
-    const int e0 = bst[bb], ne = bst[bb + 1] - e0;
-    const int nb = bnode[bk], nn = bnode[bk + 1] - nb;
-    int x = 0;
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) x += len[j];
-    const int mine = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) s_w[w] = x;
-    __syncthreads();
-    int base = 0;
-    for (int k = 0; k < w; ++k) base += s_w[k];
-    int excl = base + x - mine;
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) {
-      const int sl = SPT * t + j;
-      if (sl < P) {
-        s_u.t.m[sl] = (unsigned short)excl;
-        s_u.t.o[sl] = o[j];
-      }
-      excl += len[j];
-    }
-    if (t == 0) {
-      int tot = 0;
-      for (int k = 0; k < kFuThreads / 64; ++k) tot += s_w[k];
-      s_u.t.m[P] = (unsigned short)tot;
-    }
-    __syncthreads();
-    const int nst = s_u.t.m[P];  // == ne: every edge of a fused bucket is staged
-    if (t < kFuBE / 64) {
-      const int m = t * 64;
-      int lo = 1, hi = P;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_u.t.m[mid] > m) hi = mid; else lo = mid + 1;
-      }
-      s_u.t.c[t] = lo;
-    }
-    if (t == 0) s_u.t.c[kFuBE / 64] = P;
-    __syncthreads();
-    // the rows' words first, then the bucket's loads in two halves (searches, staged
-    // estimates, positions, old flows; scattered into s_v / s_x as they land)
-    const int rp = t < nn ? rowptr[nb + t] - e0 : 0;
-    const int rp_end = t == 0 ? rowptr[nb + nn] - e0 : 0;  // (nn may equal the thread count)
-    const double vv = t < nn ? v[nb + t] : 0.0, own2 = t < nn ? a_prev2[nb + t] : 0.0;
-    unsigned fhi[kPerT];  // f_{r-2}'s high words: the flow store skips an unchanged one (st_f)
-#pragma unroll
-    for (int h2 = 0; h2 < 2; ++h2) {
-      constexpr int HK = kPerT / 2;
-      int g[HK];
-#pragma unroll
-      for (int u = 0; u < HK; ++u) {
-        const int m = t + (h2 * HK + u) * kFuThreads;
-        g[u] = -1;
-        if (m < nst) {
-          int lo = s_u.t.c[m >> 6], hi = s_u.t.c[(m >> 6) + 1];
-          while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (s_u.t.m[mid] > m) hi = mid; else lo = mid + 1;
-          }
-          const int run = lo - 1;
-          g[u] = s_u.t.o[run] + (m - s_u.t.m[run]);
-        }
-      }
-      double val[HK], fx[HK];
-      unsigned short pos[HK];
-#pragma unroll
-      for (int u = 0; u < HK; ++u) {
-        val[u] = g[u] >= 0 ? GA[g[u]] : 0.0;
-        pos[u] = g[u] >= 0 ? pos16[g[u]] : (unsigned short)0;
-        const int q = t + (h2 * HK + u) * kFuThreads;
-        fx[u] = (q < ne && !fm) ? ld_f(F, e0 + q) : 0.0;
-      }
-#pragma unroll
-      for (int u = 0; u < HK; ++u) {
-        const int q = t + (h2 * HK + u) * kFuThreads;
-        if (g[u] >= 0) s_v[pos[u]] = val[u];
-        if (q < ne) s_x[q] = fx[u];
-        fhi[h2 * HK + u] = (unsigned)__double2hiint(fx[u]);
-      }
-    }
-    const int next = bk + nj;
-    if (next < bend) load_runs(next);  // in flight while this bucket's rows run
-    if (t < nn) s_rp[t] = (unsigned short)rp;
-    if (t == 0) {
-      s_rp[nn] = (unsigned short)rp_end;
-      s_nlong = 0;
-    }
-    __syncthreads();  // the searches are done with the run tables; s_v, s_x, s_rp complete
-    if (FU_FZ_DIAG == 1) {
-      if (t == 0) st_wt(a_new + nb, s_v[0] + s_x[0]);  // keeps the loads
-      __syncthreads();
-      bk = next;
-      continue;
-    }
-    // rows of <= kFuLong edges: one per thread, the exact left-to-right sums (CA:106-113),
-    // four elements' LDS reads in flight at a time; longer rows are listed for the waves
-    auto finish_row = [&](int r, double S, double T, int d, double vr) {
-      const double a = ((vr - S) + T) / (double)(d + 1);
-      s_u.r.a[r] = a;
-      st_wt(a_new + nb + r, a);
-      if (pc.width) put_code(pc, code_new, nb + r, a);
-      if (CHECK) {
-        const unsigned long long x = err_bits(a, target[nb + r]);
-        eb = x > eb ? x : eb;
-      }
-    };
-    if (t < nn) {
-      const int qb = s_rp[t], qe = s_rp[t + 1];
-      if (qe - qb > kFuLong) {
-        s_long[atomicAdd(&s_nlong, 1)] = t;  // (any order: rows are independent)
-      } else {
-        double S = 0.0, T = 0.0;
-        const double fo0 = fm ? old_flow(fm, own2) : 0.0;
-        int q = qb;
-        for (; q + 4 <= qe; q += 4) {
-          double er[4], fr[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            er[u] = s_v[q + u];
-            fr[u] = fm ? fo0 : s_x[q + u];
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            fr[u] = recon_fr(fr[u], er[u], own2);
-            s_x[q + u] = fr[u];
-            s_u.r.own[q + u] = (unsigned short)t;
-          }
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            S = S + fr[u];
-            T = T + er[u];
-          }
-        }
-        for (; q < qe; ++q) {
-          const double er = s_v[q];
-          const double fr = recon_fr(fm ? fo0 : s_x[q], er, own2);
-          s_x[q] = fr;
-          s_u.r.own[q] = (unsigned short)t;
-          S = S + fr;
-          T = T + er;
-        }
-        finish_row(t, S, T, qe - qb, vv);
-      }
-    }
-    __syncthreads();
-    // rows of > kFuLong edges: one per wave, fr rebuilt by the lanes, then the exact chains on
-    // even / odd lanes (chain_sum)
-    for (int k = w; k < s_nlong; k += kFuThreads / 64) {
-      const int r = s_long[k];
-      const int qb = s_rp[r], qe = s_rp[r + 1], d = qe - qb;
-      const double vr = v[nb + r], o2 = a_prev2[nb + r];
-      const double fo0 = fm ? old_flow(fm, o2) : 0.0;
-      for (int q = qb + lane; q < qe; q += 64) {
-        s_x[q] = recon_fr(fm ? fo0 : s_x[q], s_v[q], o2);
-        s_u.r.own[q] = (unsigned short)r;
-      }
-      wave_sync();
-      double S = 0.0, T = 0.0;
-      chain_sum<4>(s_x + qb, s_v + qb, d, S, T);  // (4-element batches: two blocks per CU)
-      if (lane == 0) finish_row(r, S, T, d, vr);
-      wave_sync();
-    }
-    __syncthreads();
-    // new flows, coalesced, in place (CA:117-118)
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k) {
-      const int q = t + k * kFuThreads;
-      if (q < ne) {
-        const double f = (s_x[q] + s_u.r.a[s_u.r.own[q]]) - s_v[q];
-        unsigned *wd = reinterpret_cast<unsigned *>(F);
-        const long long i = fhi_idx(e0 + q);
-        st_wt(wd + i + 32, (unsigned)__double2loint(f));
-        if (fm || (unsigned)__double2hiint(f) != fhi[k]) st_wt(wd + i, (unsigned)__double2hiint(f));
-      }
-    }
-    __syncthreads();  // the next bucket rewrites the tables and s_v / s_x
-    bk = next;
-  }
-  if (CHECK) block_max_to<kFuThreads>(eb, err);
 }
 
 template <bool CHECK, int TE, int TN, bool RF = true, bool LO = true>
@@ -2706,8 +2419,6 @@ struct fu_handle {
   int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
-  int fuse = 0;               // kernel 9: rows of <= 128 / 256 / 1024 edges (1 / 2 / 3) read the transpose's LDS
-  int fuse_late = 0;          // kernel 9: k_fused_rows after the heavy rows (1) or before them (0)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2756,12 +2467,6 @@ struct fu_handle {
     unsigned *hlist = nullptr;            // per hot edge: column << 16 | position in its bucket
     double *GBr[3] = {nullptr, nullptr, nullptr};  // G_B of round r in GBr[r % 3] (one buffer without lag)
     double *hist[2] = {nullptr, nullptr};          // lag: per parity, a_{r-2} of every lagged row
-    int *bst = nullptr;                   // B + 1: first edge of each bucket
-    int Bf = 0;                           // option fuse: buckets [Bf, B) are the fused rows' (row-aligned)
-    int *bnode = nullptr;                 // B - Bf + 1: first row of each fused bucket
-    int fuse = 0;                         // the fuse mode the layout was built for (0: none)
-    int fkey = 0;                         // fuse_key() it was built under
-    int iso0 = 0;                         // fuse: rows [iso0, n) are isolated (k_isolated)
   };
   TransLayout tr;
   bool tr_ready = false;
@@ -3151,16 +2856,13 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
 void free_transpose(fu_handle *h) {
   auto &T = h->tr;
   for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA,
-                  (void *)T.GBr[0], (void *)T.hist[0], (void *)T.hist[1], (void *)T.hoff, (void *)T.hlist,
-                  (void *)T.bst, (void *)T.bnode})
+                  (void *)T.GBr[0], (void *)T.hist[0], (void *)T.hist[1], (void *)T.hoff, (void *)T.hlist})
     if (p) hipFree(p);
   if (T.GBr[1] != T.GBr[0]) hipFree(T.GBr[1]);
   if (T.GBr[2] != T.GBr[0]) hipFree(T.GBr[2]);
   T = fu_handle::TransLayout{};
   h->tr_ready = false;
 }
-
-inline int fuse_key(const fu_handle *h) { return h->fuse | h->mid_heavy << 4 | h->wave_heavy << 5; }
 
 int ensure_transpose(fu_handle *h) {
   if (h->tr_ready) return FU_OK;
@@ -3172,59 +2874,13 @@ int ensure_transpose(fu_handle *h) {
     h->tr_why = E == 0 ? "kernel 9 (pregather): no edges" : "kernel 9 (pregather): more than 2^25 nodes";
     return fail(FU_ERR_GRAPH, h->tr_why);
   }
+  const int64_t B = (E + kTrBE - 1) / kTrBE;
   // buckets [0, Bh) hold every mega-hub edge: transposed first, so the hub chains can start
   int64_t hub_end = 0;
   for (int32_t i = 0; i < h->n; ++i)
     if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
-  // option fuse: the rows outside the fused classes (the mega hubs, the rows of the heavy
-  // tiles [n_hub, tf)) must be exactly the rows [0, i_f) (the degree layout); the rest,
-  // [i_f, n), go to row-aligned buckets after the fixed ones
-  int32_t i_f = h->n;
-  int fmode = 0;
-  if (h->fuse && h->wave_heavy && !h->dist) {
-    const int nmega = h->n_hub, nh = h->nheavy_geo[1];
-    const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-    const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
-    const int tf = h->fuse >= 3 ? m0 : h->fuse == 2 ? m1 : nh;
-    const int64_t nrh = std::min<int64_t>(h->multi_geo[1][1], 4LL * (tf - nmega));
-    int64_t cnt = 0, mx = -1;
-    for (int32_t i = 0; i < h->n; ++i)
-      if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) {
-        ++cnt;
-        mx = std::max<int64_t>(mx, i);
-      }
-    for (int64_t q = 0; q < nrh; ++q) {
-      ++cnt;
-      mx = std::max<int64_t>(mx, h->h_hrows[h->multi_geo[1][0] + q]);
-    }
-    bool ok = mx == cnt - 1 && cnt < h->n && P <= kFuMaxP;
-    for (int32_t i = (int32_t)cnt; ok && i < h->n; ++i) ok = h->h_rowptr[i + 1] - h->h_rowptr[i] <= kFuBE;
-    if (ok) {
-      i_f = (int32_t)cnt;
-      fmode = h->fuse;
-    }
-  }
-  const int64_t e_f = h->h_rowptr[i_f];
-  std::vector<int32_t> bst, bnode;
-  for (int64_t e = 0; e < e_f; e += kTrBE) bst.push_back((int32_t)e);
-  const int64_t Bf = (int64_t)bst.size();
-  // the isolated rows at the end (the degree layout's last rows) go to k_isolated
-  int32_t i_0 = h->n;
-  if (fmode)
-    while (i_0 > i_f && h->h_rowptr[i_0] == h->h_rowptr[i_0 - 1]) --i_0;
-  for (int32_t i = i_f; i < i_0;) {  // greedy: whole rows, <= kFuBE edges, <= kFuBN rows
-    const int32_t b = i;
-    while (i < i_0 && i - b < kFuBN && h->h_rowptr[i + 1] - h->h_rowptr[b] <= kFuBE) ++i;
-    bst.push_back((int32_t)h->h_rowptr[b]);
-    bnode.push_back(b);
-  }
-  bnode.push_back(i_0);
-  if (bst.empty()) bst.push_back(0);
-  const int64_t B = (int64_t)bst.size();
-  bst.push_back((int32_t)E);
-  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>, k_transpose_pipe<HOTN>);
-  // not with fuse (no room for the hot table beside a fused bucket)
-  const int32_t H = fmode ? 0 : (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
+  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>, k_transpose_pipe<HOTN>)
+  const int32_t H = (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
   std::vector<int64_t> cnt(P, 0);
   for (int64_t e = 0; e < E; ++e)
     if (h->h_col[e] >= H) cnt[h->h_col[e] / SN]++;
@@ -3243,16 +2899,16 @@ int ensure_transpose(fu_handle *h) {
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
     hoff[b] = (int32_t)hlist.size();
-    const int64_t e0 = bst[b], e1 = bst[b + 1];
-    for (int64_t e = e0; e < e1; ++e) {
+    const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
+    for (int64_t e = b * kTrBE; e < e1; ++e) {
       const int32_t c = h->h_col[e];
       if (c < H) {  // {column, position in the bucket}, edge order
-        hlist.push_back(((uint32_t)c << 16) | (uint32_t)(e - e0));
+        hlist.push_back(((uint32_t)c << 16) | (uint32_t)(e - b * kTrBE));
         continue;
       }
       const int64_t g = cur[c / SN]++;
       colS[g] = (uint16_t)(c % SN);
-      pos[g] = (uint16_t)(e - e0);
+      pos[g] = (uint16_t)(e - b * kTrBE);
     }
   }
   hoff[B] = (int32_t)hlist.size();
@@ -3278,12 +2934,6 @@ int ensure_transpose(fu_handle *h) {
   if (int rc = up(&T.offT, offT.data(), offT.size())) return rc;
   if (int rc = up(&T.hoff, hoff.data(), hoff.size())) return rc;
   if (int rc = up(&T.hlist, hlist.data(), hlist.size())) return rc;
-  if (int rc = up(&T.bst, bst.data(), bst.size())) return rc;
-  if (int rc = up(&T.bnode, bnode.data(), bnode.size())) return rc;
-  T.Bf = (int)Bf;
-  T.iso0 = i_0;
-  T.fuse = fmode;
-  T.fkey = fuse_key(h);
   T.H = H;
   if (int rc = dmalloc(&T.GA, (size_t)total)) return rc;
   // G_B: a ring of three with lag (round r reads G_B of round r - 2 for the lagged rows)
@@ -3300,14 +2950,14 @@ int ensure_transpose(fu_handle *h) {
   T.Q = (int)Q;
   T.NB = (int)br.size();
   T.B = (int)B;
-  T.Bh = (int)std::min<int64_t>(Bf, (hub_end + kTrBE - 1) / kTrBE);
+  T.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
   {  // the multi-row heavy rows of geometry 1 (contiguous after the hubs under the degree layout)
     int64_t mend = hub_end;
     for (int q = 0; q < h->multi_geo[1][1]; ++q) {
       const int32_t i = h->h_hrows[h->multi_geo[1][0] + q];
       mend = std::max<int64_t>(mend, h->h_rowptr[i + 1]);
     }
-    T.Bm = (int)std::max<int64_t>(T.Bh, std::min<int64_t>(fmode ? Bf : B, (mend + kTrBE - 1) / kTrBE));
+    T.Bm = (int)std::max<int64_t>(T.Bh, (mend + kTrBE - 1) / kTrBE);
   }
   h->tr_ready = true;
   return FU_OK;
@@ -3429,10 +3079,6 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
 // the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
 // the remaining buckets and tiles.
 int launch_k9(fu_handle *h, RoundCtx &c) {
-  if (h->tr_ready && h->fuse && h->tr.fkey != fuse_key(h)) {  // the fused rows follow mid_heavy / wave_heavy
-    if (int rc = lag_finalize_all(h)) return rc;
-    free_transpose(h);
-  }
   if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
   double *Gb = h->tr.GBr[c.r % 3];
   const double *Gb_old = h->tr.GBr[(c.r + 1) % 3];  // G_B of round r - 2 (lag)
@@ -3464,10 +3110,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
   // multi-row heavy rows
   const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-  // fuse: the rows of the heavy tiles [tf, nh) and the light tiles run in k_fused_rows
-  const int fz = h->tr.fuse;
-  const int tf = fz >= 3 ? m0_ : fz == 2 ? m1 : nh;
-  const int mend = std::min(h->multi_mid ? m1 : m0_, tf);
+  const int mend = h->multi_mid ? m1 : m0_;
   const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
   const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
   const bool lag_multi = h->lag && multi;
@@ -3480,24 +3123,24 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   auto tr_launch = [&](int b0, int nb) {
     if (pipe && h->tr.H > kTrHotS)
       hipLaunchKernelGGL(k_transpose_pipe<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
-                         h->tr.P, h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
+                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
                          h->tr.hlist);
     else if (pipe && h->tr.H)
       hipLaunchKernelGGL(k_transpose_pipe<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
-                         h->tr.P, h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
+                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
                          h->tr.hlist);
     else if (pipe)
       hipLaunchKernelGGL(k_transpose_pipe<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
     else if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
       hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
       hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else
       hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         h->tr.bst, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
   };
   if (bh) tr_launch(0, bh);
   if (hubs) {
@@ -3507,38 +3150,16 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // split_tr: the buckets of the multi-row heavy rows first, then k_heavy_multi on stream3
   // beside the remaining (latency-bound) transposes
   const int bm = std::min(std::max(h->tr.Bm, bh), h->tr.B);
-  const int bf = h->tr.Bf;  // the fixed buckets; [bf, B) are the fused rows'
-  const bool split = h->split_tr && bm > bh && bm < bf;
+  const bool split = h->split_tr && bm > bh && bm < h->tr.B;
   if (split) {
     tr_launch(bh, bm - bh);
     HIP_TRY(hipEventRecord(h->ev_htr, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream3, h->ev_htr, 0));
-    tr_launch(bm, bf - bm);
-  } else if (bf > bh) {
-    tr_launch(bh, bf - bh);
+    tr_launch(bm, h->tr.B - bm);
+  } else if (h->tr.B > bh) {
+    tr_launch(bh, h->tr.B - bh);
   }
   const bool chk = c.err != nullptr;
-  auto fused = [&]() {
-    if (!fz) return;
-    if (h->tr.iso0 < h->n)
-      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->tr.iso0)), dim3(kBlock), 0, h->stream, h->tr.iso0, h->n,
-                         h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1, chk ? 1 : 0);
-    if (h->tr.B <= bf) return;
-    const int nbk = h->tr.B - bf, per = (nbk + 7) / 8;
-    const unsigned grid = 8u * (unsigned)std::min(per, kFuBPC * std::max(1, h->n_cu / 8));
-    auto go = [&](auto C, auto SP) {
-      hipLaunchKernelGGL((k_fused_rows<decltype(C)::value, decltype(SP)::value>), dim3(grid), dim3(kFuThreads), 0,
-                         h->stream, bf, nbk, h->tr.P, h->tr.bst, h->tr.bnode, h->tr.offT, h->tr.GA, h->tr.pos16,
-                         h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
-    };
-    constexpr int kS = (kFuMaxP + kFuThreads - 1) / kFuThreads;  // slices per thread at kFuMaxP
-    const bool p2 = h->tr.P <= 2 * kFuThreads;
-    if (chk && p2) go(std::true_type{}, std::integral_constant<int, 2>{});
-    else if (chk) go(std::true_type{}, std::integral_constant<int, (kS > 2 ? kS : 2)>{});
-    else if (p2) go(std::false_type{}, std::integral_constant<int, 2>{});
-    else go(std::false_type{}, std::integral_constant<int, (kS > 2 ? kS : 2)>{});
-  };
-  if (!h->fuse_late) fused();
   // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
   // behind the hub path, once every bucket is transposed, beside the heavy rows
   const int side = hubs ? h->side_tiles : 0;
@@ -3557,12 +3178,12 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (side) {
       HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_tr, 0));
       auto st = [&](auto C) {
-        if (side >= 2 && tf > m1)  // the rows of 129-256 edges (4 per block, in registers)
-          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(tf - m1),
+        if (side >= 2 && nh > m1)  // the rows of 129-256 edges (4 per block, in registers)
+          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(nh - m1),
                              dim3(kBlock), 0, h->stream2, tl + m1, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
                              h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                              c.fm);
-        if (nl && !fz)
+        if (nl)
           hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                              h->stream2, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err,
                              cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
@@ -3597,20 +3218,19 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       if (!lag_multi) hm(std::integral_constant<int, 0>{});
       else if (lagm == 1) hm(std::integral_constant<int, 1>{});
       else hm(std::integral_constant<int, 2>{});
-      if (!h->multi_mid) heavy(C, std::integral_constant<int, kMidRL>{}, m0, std::min(m1, tf));
+      if (!h->multi_mid) heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     } else {
-      heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, std::min(m0, tf));
-      heavy(C, std::integral_constant<int, kMidRL>{}, m0, std::min(m1, tf));
+      heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
+      heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     }
-    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, std::min(nh, tf));
-    if (nl && !side && !fz)
+    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
+    if (nl && !side)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
   };
   if (chk) tiles(std::true_type{});
   else tiles(std::false_type{});
-  if (h->fuse_late) fused();
   HIP_TRY(hipGetLastError());
   if (split && multi) {
     HIP_TRY(hipEventRecord(h->ev_s3, h->stream3));
@@ -4068,19 +3688,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     }
     return FU_OK;
   }
-  if (!std::strcmp(key, "fuse")) {  // kernel 9: rows of <= 128 / 256 / 1024 edges (1 / 2 / 3) fused with their transpose
-    if (value < 0 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: fuse must be 0, 1, 2 or 3");
-    if ((int)value != h->fuse) {
-      if (int rc = lag_finalize_all(h)) return rc;  // the lagged set may change with the buckets
-      free_transpose(h);                            // the bucket layout follows the option
-      h->fuse = (int)value;
-    }
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "fuse_late")) {  // kernel 9: k_fused_rows after the heavy rows (1) or before (0)
-    h->fuse_late = value != 0;
-    return FU_OK;
-  }
   if (!std::strcmp(key, "split_tr")) {  // kernel 9: heavy rows start once their buckets are transposed (1)
     h->split_tr = value != 0;
     return FU_OK;
@@ -4474,8 +4081,6 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   info[7] = h->tuned_width;
   for (int k = 0; k < kNCands; ++k) info[8 + k] = (int64_t)((double)h->tune_ms[k] * 1e6);  // ns per round
   info[20] = h->n_hub;
-  info[21] = h->tr_ready ? h->tr.fuse : -1;         // kernel 9 layout: fuse mode in effect (-1: not built)
-  info[22] = h->tr_ready ? h->tr.B - h->tr.Bf : 0;  // ... and its fused (row-aligned) buckets
   for (int k = 0; k < 4; ++k)  // autotune winner per packing width 0, 8, 16, 32 (kernel * 10 + geometry; -1 = none)
     info[23 + k] = h->tune_cache[k] < 0 ? -1 : kCands[h->tune_cache[k]].kernel * 10 + kCands[h->tune_cache[k]].geo;
   for (int li = 0; li < 4; ++li) info[27 + li] = h->st[li].P;  // kernel 8 slices per layout (0 = not built)

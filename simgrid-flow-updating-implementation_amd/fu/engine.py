@@ -30,7 +30,6 @@ def handle_info(h) -> dict:
             "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
             "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
             "tuned_pack_width": int(a[7]), "mega_hubs": int(a[20]),
-            "fuse": int(a[21]), "fused_buckets": int(a[22]),
             "stage_slices": [int(x) for x in a[27:31]],
             "tune_winner_by_width": {w: _cand_name(int(a[23 + k])) for k, w in
                                      enumerate((0, 8, 16, 32)) if a[23 + k] >= 0},

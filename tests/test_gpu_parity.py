@@ -141,10 +141,10 @@ def test_option_errors():
     for k in (1, 2, 3, 5, 6, 7, 10, 11):  # removed variants / out of range
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
-    for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks"):
+    for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
-    for key, val in (("fuse", 4), ("fuse", -1), ("side_tiles", 3)):
+    for key, val in (("side_tiles", 3), ("side_tiles", -1)):
         with pytest.raises(fu.FuError):
             eng.set_option(key, val)
     with pytest.raises(fu.FuError):
@@ -630,8 +630,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "fuse1", "fuse2",
-                                   "fuse3", "fuse3_late", "fuse3_mid0", "fuse2_side2_split_hot", "fuse1_nolag_pipe"])
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -672,12 +671,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     elif multi == "split_side1_hot":
         for key, val in (("split_tr", 1), ("side_tiles", 1), ("tr_hot", 3000), ("hub_prio", 1)):
             eng.set_option(key, val)
-    elif str(multi).startswith("fuse"):  # rows of <= 128 / 256 / 1024 edges fused with their transpose
-        eng.set_option("fuse", int(multi[4]))
-        opts = {"late": ("fuse_late", 1), "mid0": ("multi_mid", 0), "side2": ("side_tiles", 2),
-                "split": ("split_tr", 1), "hot": ("tr_hot", 3000), "nolag": ("lag", 0), "pipe": ("tr_pipe", 1)}
-        for part in multi.split("_")[1:]:
-            eng.set_option(*opts[part])
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -688,8 +681,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     assert np.max(np.abs(a_ref - tgt)) == tr[-1]
-    if str(multi).startswith("fuse"):  # the degree layout admits it: the layout was built with it
-        assert eng.info()["fuse"] == int(multi[4]) and eng.info()["fused_buckets"] > 0
 
 
 @pytest.mark.parametrize("mega", [100, 1000])
@@ -1035,10 +1026,7 @@ def _class_edge_graph(seed):
 @pytest.mark.parametrize("layout", ["given", "degree"])
 @pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
                                          ("pregather", {}), ("pregather", {"lag": 0}),
-                                         ("pregather", {"multi_mid": 0, "tr_hot": 64}),
-                                         ("pregather", {"fuse": 1}), ("pregather", {"fuse": 2}),
-                                         ("pregather", {"fuse": 3, "fuse_late": 1}),
-                                         ("pregather", {"fuse": 3, "mid_heavy": 0})])
+                                         ("pregather", {"multi_mid": 0, "tr_hot": 64})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):
     """Rows of exactly the degree where each row class starts or ends, at the default
     thresholds, every kernel, against the C oracle after every few rounds (the lagged flows
@@ -1055,33 +1043,3 @@ def test_row_class_boundaries_bitwise(kernel, opts, layout):
         a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, done, nthreads=16)
         assert np.array_equal(eng.estimates(), a_ref), done
         assert np.array_equal(eng.flows(), f_ref), done
-
-
-def test_fuse_switches_mid_run_bitwise():
-    """Kernel 9's fused rows under the degree layout with lag: flows read after every round,
-    then the fuse mode, mid_heavy (the fused split is rebuilt) and multi_mid (the lagged set
-    shrinks) switched between runs, and fu_reset, all bitwise against the C oracle."""
-    g = fu.Graph.rmat(14, 16, seed=9)
-    v = fu.uniform_values(g.n, seed=9)
-    eng = fu.CollectAll(g, v, kernel="pregather", hub_threshold=32, layout="degree")
-    eng.set_option("mega_hub", 900)
-    eng.set_option("fuse", 3)
-    for r in range(1, 8):
-        eng.run(1)
-        a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, r, nthreads=16)
-        assert np.array_equal(eng.estimates(), a_ref), r
-        assert np.array_equal(eng.flows(), f_ref), r
-    assert eng.info()["fuse"] == 3
-    done = 7
-    for key, val, k in (("fuse", 1, 3), ("fuse", 0, 2), ("fuse", 2, 5), ("mid_heavy", 0, 3),
-                        ("mid_heavy", 1, 4), ("fuse", 3, 3), ("multi_mid", 0, 5), ("fuse_late", 1, 4)):
-        eng.set_option(key, val)
-        eng.run(k)
-        done += k
-    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, done, nthreads=16)
-    assert np.array_equal(eng.estimates(), a_ref)
-    assert np.array_equal(eng.flows(), f_ref)
-    eng.reset()
-    eng.run(6)
-    a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, 6, nthreads=16)
-    assert np.array_equal(eng.flows(), f_ref) and np.array_equal(eng.estimates(), a_ref)

@@ -1,4 +1,5 @@
 # round 4, GPU session h: kernel 9's fused rows (option fuse): GPU parity suite, then the
+# (record of a measured session: option fuse was removed after it lost, profiles/r04/fuse/)
 # R-MAT-24 A/B against the default, a kernel trace and PMC bytes of the best candidate
 set -o pipefail
 mkdir -p gpurun_out/h

@@ -1,4 +1,5 @@
 # round 4, GPU session i: fused rows, second form (isolated tail in k_isolated, rows of > 64
+# (record of a measured session: option fuse was removed after it lost, profiles/r04/fuse/)
 # edges on whole waves, unrolled short rows): parity, R-MAT-24 A/B, kernel traces
 set -o pipefail
 mkdir -p gpurun_out/i

@@ -1,4 +1,5 @@
 # round 4, GPU session j: where k_fused_rows' time goes (timing-only experiment builds):
+# (record of a measured session: option fuse was removed after it lost, profiles/r04/fuse/)
 # the default geometry, without the row phase (fzd1), 2048-edge buckets at four blocks per CU
 # (fz2k, fz2kd1), one block per CU (fz1blk); kernel traces of fuse 1 on R-MAT-24
 set -o pipefail

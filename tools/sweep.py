@@ -48,13 +48,6 @@ VARIANTS = {
     "pre_prio_split_side1_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1,
                                                "side_tiles": 1, "tr_hot": 10240}),
     "pre_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "lag": 1}),
-    "pre_fuse1": ("pregather", {"layout": "degree", "pack": 0, "fuse": 1}),
-    "pre_fuse2": ("pregather", {"layout": "degree", "pack": 0, "fuse": 2}),
-    "pre_fuse3": ("pregather", {"layout": "degree", "pack": 0, "fuse": 3}),
-    "pre_fuse1_late": ("pregather", {"layout": "degree", "pack": 0, "fuse": 1, "fuse_late": 1}),
-    "pre_fuse2_late": ("pregather", {"layout": "degree", "pack": 0, "fuse": 2, "fuse_late": 1}),
-    "pre_fuse3_late": ("pregather", {"layout": "degree", "pack": 0, "fuse": 3, "fuse_late": 1}),
-    "pre_fuse3_prio": ("pregather", {"layout": "degree", "pack": 0, "fuse": 3, "hub_prio": 1}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
