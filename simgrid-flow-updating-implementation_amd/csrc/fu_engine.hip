@@ -1395,6 +1395,26 @@ __global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, 
   }
 }
 
+// Kernel 9: the isolated rows at the end of the degree layout (the last light tiles have no
+// edges): a_r = ((v - 0.0) + 0.0) / 1 (CA:106-113 with no neighbours), as a light tile
+// computes it, one thread per row instead of a tile block per 128 rows.
+__global__ __launch_bounds__(kBlock) void k_isolated(int i0, int n, const double *__restrict__ v,
+                                                     double *__restrict__ a_new, const double *__restrict__ target,
+                                                     unsigned long long *__restrict__ err, void *__restrict__ code_new,
+                                                     PackCtl *__restrict__ ctl, int rslot, int check) {
+  const PackCtl pc = ctl[2];
+  if (blockIdx.x == 0 && threadIdx.x == 0) ctl[rslot] = pc;
+  const int i = i0 + blockIdx.x * kBlock + threadIdx.x;
+  unsigned long long eb = 0;
+  if (i < n) {
+    const double a = ((v[i] - 0.0) + 0.0) / (double)1;
+    st_wt(a_new + i, a);
+    if (pc.width) put_code(pc, code_new, i, a);
+    if (check) eb = err_bits(a, target[i]);
+  }
+  if (check) block_max_to(eb, err);
+}
+
 template <bool CHECK, int TE, int TN, bool RF = true, bool LO = true>
 __global__ __launch_bounds__(kBlock) void k_round_staged(
     const int4 *__restrict__ tiles, int t0, int ntl,
@@ -2406,6 +2426,8 @@ struct fu_handle {
   int ntiles_geo[4] = {0, 0, 0, 0};
   int nheavy_geo[4] = {0, 0, 0, 0};  // leading non-light tiles
   int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
+  int niso_geo[4] = {0, 0, 0, 0};    // kernel 9: trailing light tiles of isolated rows only (k_isolated runs them)
+  int iso0_geo[4] = {0, 0, 0, 0};    // ... their first row (rows [iso0, n) are isolated)
   int mid_geo[4][2] = {};            // heavy tiles [mid_geo[0], mid_geo[1]) lead with a row of 64 x (kHeavyRL, kMidRL] edges
   int multi_geo[4][2] = {};          // hrows offset and count of this geometry's sorted heavy rows
   int multi_heavy = 1;               // kernel 9: rows > 64 x kHeavyRL as k_heavy_multi blocks
@@ -2419,6 +2441,7 @@ struct fu_handle {
   int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
+  int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2495,7 +2518,7 @@ constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 // {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
 int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *count, int *nheavy,
                      int *nbound, int *mid,
-                     int *multi) {
+                     int *multi, int *niso, int *iso0) {
   std::vector<int4> heavy, light, hubs;
   const int32_t n = h->n;
   int32_t i = 0;
@@ -2554,6 +2577,16 @@ int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *c
   *nheavy = (int)all.size();
   // multi-GPU (ghost estimate slots exist): light tiles that read a ghost go first, so the
   // halo exchange can start once they are done, beside the interior tiles
+  // the light tiles at the end with no edges (the degree layout's isolated rows: R-MAT-24 has
+  // 7.9 M, 62 K tiles of 128): kernel 9 runs them as k_isolated, one thread per row
+  *niso = 0;
+  *iso0 = h->n;
+  if (h->na == h->n) {
+    size_t q = light.size();
+    while (q > 0 && light[q - 1].z == light[q - 1].w) --q;
+    *niso = (int)(light.size() - q);
+    if (*niso) *iso0 = light[q].x;
+  }
   *nbound = 0;
   if (h->na > h->n) {
     auto has_ghost = [&](const int4 &tl) {
@@ -2634,7 +2667,8 @@ int build_tiles(fu_handle *h) {
   for (int g = 0; g < 4; ++g)
     if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->tnar_geo[g], &h->ntiles_geo[g],
                                   &h->nheavy_geo[g],
-                                  &h->nbound_geo[g], h->mid_geo[g], h->multi_geo[g]))
+                                  &h->nbound_geo[g], h->mid_geo[g], h->multi_geo[g], &h->niso_geo[g],
+                                  &h->iso0_geo[g]))
       return rc;
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
@@ -3085,7 +3119,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   if (!Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
   const int r1 = (int)(c.r & 1);
   const void *cp = h->code[(c.r - 1) & 1];
-  const int nmega = h->n_hub, nh = h->nheavy_geo[1], nl = h->ntiles_geo[1] - nh;
+  const int nmega = h->n_hub, nh = h->nheavy_geo[1];
+  const int niso = h->iso_rows ? h->niso_geo[1] : 0;  // trailing isolated-row tiles: k_isolated
+  const int nl = h->ntiles_geo[1] - nh - niso;
   // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
   const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
   const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
@@ -3183,6 +3219,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                              dim3(kBlock), 0, h->stream2, tl + m1, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
                              h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                              c.fm);
+        if (niso)
+          hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream2,
+                             h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
+                             decltype(C)::value ? 1 : 0);
         if (nl)
           hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                              h->stream2, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err,
@@ -3224,6 +3264,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     }
     if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
+    if (niso && !side)
+      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream,
+                         h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
+                         decltype(C)::value ? 1 : 0);
     if (nl && !side)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
@@ -3686,6 +3730,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "iso_rows")) {  // kernel 9: trailing isolated rows one thread each (1) or as tiles (0)
+    h->iso_rows = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "split_tr")) {  // kernel 9: heavy rows start once their buckets are transposed (1)

@@ -630,7 +630,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot"])
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -671,6 +671,8 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     elif multi == "split_side1_hot":
         for key, val in (("split_tr", 1), ("side_tiles", 1), ("tr_hot", 3000), ("hub_prio", 1)):
             eng.set_option(key, val)
+    elif multi == "iso0":  # the trailing isolated rows as light tiles (k_isolated is the default)
+        eng.set_option("iso_rows", 0)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -1026,7 +1028,8 @@ def _class_edge_graph(seed):
 @pytest.mark.parametrize("layout", ["given", "degree"])
 @pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
                                          ("pregather", {}), ("pregather", {"lag": 0}),
-                                         ("pregather", {"multi_mid": 0, "tr_hot": 64})])
+                                         ("pregather", {"multi_mid": 0, "tr_hot": 64}),
+                                         ("pregather", {"iso_rows": 0}), ("pregather", {"side_tiles": 2})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):
     """Rows of exactly the degree where each row class starts or ends, at the default
     thresholds, every kernel, against the C oracle after every few rounds (the lagged flows
