@@ -2442,7 +2442,6 @@ struct fu_handle {
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
-  int light_geo = 1;          // kernel 9: light tiles of geometry 1 (1024 x 128) or 2 (1024 x 256)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3121,24 +3120,8 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int r1 = (int)(c.r & 1);
   const void *cp = h->code[(c.r - 1) & 1];
   const int nmega = h->n_hub, nh = h->nheavy_geo[1];
-  // light tiles: geometry 1 (1024 x 128) or, option light_geo 2, geometry 2's 1024 x 256 (the
-  // same rows: light is d <= hub_threshold at 1024 edges in both); the trailing tiles of
-  // isolated rows run as k_isolated (iso_rows)
-  const int lg = h->light_geo;
-  const int niso = h->iso_rows ? h->niso_geo[lg] : 0;
-  const int nl = h->ntiles_geo[lg] - h->nheavy_geo[lg] - niso;
-  const int4 *tll = h->tiles_geo[lg] + h->nheavy_geo[lg];
-  const int iso0 = h->iso0_geo[lg];
-  auto light_tiles = [&](auto C, hipStream_t st) {
-    if (lg == 2)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 256, 1, true>), dim3(nl), dim3(kBlock), 0, st,
-                         tll, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp, h->code[r1],
-                         h->pctl, r1, nullptr, nullptr, nullptr, 0, h->tr.GBr[c.r % 3], c.fm);
-    else
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0, st,
-                         tll, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp, h->code[r1],
-                         h->pctl, r1, nullptr, nullptr, nullptr, 0, h->tr.GBr[c.r % 3], c.fm);
-  };
+  const int niso = h->iso_rows ? h->niso_geo[1] : 0;  // trailing isolated-row tiles: k_isolated
+  const int nl = h->ntiles_geo[1] - nh - niso;
   // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
   const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
   const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
@@ -3237,9 +3220,13 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                              h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                              c.fm);
         if (niso)
-          hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - iso0)), dim3(kBlock), 0, h->stream2, iso0, h->n, h->v,
-                             c.an, h->target, c.err, h->code[r1], h->pctl, r1, decltype(C)::value ? 1 : 0);
-        if (nl) light_tiles(C, h->stream2);
+          hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream2,
+                             h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
+                             decltype(C)::value ? 1 : 0);
+        if (nl)
+          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+                             h->stream2, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err,
+                             cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
       };
       if (chk) st(std::true_type{});
       else st(std::false_type{});
@@ -3278,9 +3265,13 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     }
     if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
     if (niso && !side)
-      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - iso0)), dim3(kBlock), 0, h->stream, iso0, h->n, h->v, c.an,
-                         h->target, c.err, h->code[r1], h->pctl, r1, decltype(C)::value ? 1 : 0);
-    if (nl && !side) light_tiles(C, h->stream);
+      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream,
+                         h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
+                         decltype(C)::value ? 1 : 0);
+    if (nl && !side)
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+                         h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
   };
   if (chk) tiles(std::true_type{});
   else tiles(std::false_type{});
@@ -3739,11 +3730,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "light_geo")) {  // kernel 9: light tiles 1024 x 128 (1) or 1024 x 256 (2)
-    if (value != 1 && value != 2) return fail(FU_ERR_ARG, "fu_set_option: light_geo must be 1 or 2");
-    h->light_geo = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "iso_rows")) {  // kernel 9: trailing isolated rows one thread each (1) or as tiles (0)

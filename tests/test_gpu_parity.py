@@ -144,7 +144,7 @@ def test_option_errors():
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
-    for key, val in (("side_tiles", 3), ("side_tiles", -1), ("light_geo", 0), ("light_geo", 3)):
+    for key, val in (("side_tiles", 3), ("side_tiles", -1)):
         with pytest.raises(fu.FuError):
             eng.set_option(key, val)
     with pytest.raises(fu.FuError):
@@ -630,7 +630,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "lg2", "lg2_side1"])
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -673,11 +673,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
             eng.set_option(key, val)
     elif multi == "iso0":  # the trailing isolated rows as light tiles (k_isolated is the default)
         eng.set_option("iso_rows", 0)
-    elif multi == "lg2":  # light tiles of 1024 edges x 256 rows
-        eng.set_option("light_geo", 2)
-    elif multi == "lg2_side1":
-        eng.set_option("light_geo", 2)
-        eng.set_option("side_tiles", 1)
     else:
         eng.set_option("multi_heavy", multi)
     eng.set_option("pack_every", 4)
@@ -1034,8 +1029,7 @@ def _class_edge_graph(seed):
 @pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
                                          ("pregather", {}), ("pregather", {"lag": 0}),
                                          ("pregather", {"multi_mid": 0, "tr_hot": 64}),
-                                         ("pregather", {"iso_rows": 0}), ("pregather", {"side_tiles": 2}),
-                                         ("pregather", {"light_geo": 2}), ("pregather", {"light_geo": 2, "iso_rows": 0})])
+                                         ("pregather", {"iso_rows": 0}), ("pregather", {"side_tiles": 2})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):
     """Rows of exactly the degree where each row class starts or ends, at the default
     thresholds, every kernel, against the C oracle after every few rounds (the lagged flows

@@ -1,4 +1,5 @@
 # round 4, GPU session l: kernel 9's light tiles at 1024 x 256 (light_geo 2): parity, R-MAT-24 A/B
+# (record of a measured session: option light_geo was removed after it lost)
 set -o pipefail
 mkdir -p gpurun_out/l
 export TMPDIR=/tmp
