@@ -2442,6 +2442,7 @@ struct fu_handle {
   int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
+  int multi_short = 0;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3146,9 +3147,11 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
   // multi-row heavy rows
   const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-  const int mend = h->multi_mid ? m1 : m0_;
+  // multi_short: the rows of 129-256 edges (heavy tiles [m1, nh)) join the multi-row blocks
+  const int mend = h->multi_mid ? (h->multi_short ? nh : m1) : m0_;
   const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
   const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
+  const int m1s = multi && h->multi_mid && h->multi_short ? nh : m1;  // one-row-per-wave tiles [m1s, nh)
   const bool lag_multi = h->lag && multi;
   const int p = r1;
   if (h->lagf[p] && h->lag_nmulti[p] != (lag_multi ? n_multi : 0)) {
@@ -3214,9 +3217,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (side) {
       HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_tr, 0));
       auto st = [&](auto C) {
-        if (side >= 2 && nh > m1)  // the rows of 129-256 edges (4 per block, in registers)
-          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(nh - m1),
-                             dim3(kBlock), 0, h->stream2, tl + m1, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
+        if (side >= 2 && nh > m1s)  // the rows of 129-256 edges (4 per block, in registers)
+          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(nh - m1s),
+                             dim3(kBlock), 0, h->stream2, tl + m1s, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
                              h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                              c.fm);
         if (niso)
@@ -3263,7 +3266,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
       heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     }
-    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1, nh);
+    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1s, nh);
     if (niso && !side)
       hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream,
                          h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
@@ -3730,6 +3733,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "multi_short")) {  // kernel 9: rows of 129-256 edges as multi-row blocks (1)
+    h->multi_short = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "iso_rows")) {  // kernel 9: trailing isolated rows one thread each (1) or as tiles (0)

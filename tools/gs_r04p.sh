@@ -1,0 +1,8 @@
+# round 4, GPU session p: the rows of 129-256 edges in the multi-row blocks (multi_short)
+set -o pipefail
+mkdir -p gpurun_out/p
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_parity.py -k "multi_row_chains or row_class or lag" > gpurun_out/p/pytest.log 2>&1 || exit $?
+rm -rf gpurun_out/ab
+AB_SPEC="rmat:scale=24,ef=16" AB_ARGS="--warm=3 --timed=20 --reps=3" AB_VARIANTS="deg_np_pre pre_short" AB_ROUNDS=3 bash tools/ab_proc.sh || exit $?
+mv gpurun_out/ab gpurun_out/p/ab
