@@ -135,7 +135,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 are transposed (default 0).
  * "iso_rows"      kernel 9: the trailing light tiles of isolated rows (the degree layout's last
  *                 rows) run as one thread per row (k_isolated, 1, default) or as tiles (0).
- * "multi_short"   kernel 9: the rows of 129-256 edges run in the multi-row blocks too (default 0).
+ * "multi_short"   kernel 9: the rows of 129-256 edges run in the multi-row blocks too (default 1;
+ *                 0: one row per wave, four per block).
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
  * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).

@@ -630,7 +630,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "short", "short_side2_nolag"])
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "short0", "short_side2_nolag"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -673,8 +673,8 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
             eng.set_option(key, val)
     elif multi == "iso0":  # the trailing isolated rows as light tiles (k_isolated is the default)
         eng.set_option("iso_rows", 0)
-    elif multi == "short":  # the rows of 129-256 edges in the multi-row blocks too
-        eng.set_option("multi_short", 1)
+    elif multi == "short0":  # the rows of 129-256 edges one per wave (multi_short is the default)
+        eng.set_option("multi_short", 0)
     elif multi == "short_side2_nolag":
         for key, val in (("multi_short", 1), ("side_tiles", 2), ("lag", 0)):
             eng.set_option(key, val)
@@ -1035,7 +1035,7 @@ def _class_edge_graph(seed):
                                          ("pregather", {}), ("pregather", {"lag": 0}),
                                          ("pregather", {"multi_mid": 0, "tr_hot": 64}),
                                          ("pregather", {"iso_rows": 0}), ("pregather", {"side_tiles": 2}),
-                                         ("pregather", {"multi_short": 1}),
+                                         ("pregather", {"multi_short": 0}),
                                          ("pregather", {"multi_short": 1, "multi_heavy": 0})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):
     """Rows of exactly the degree where each row class starts or ends, at the default

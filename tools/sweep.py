@@ -51,6 +51,8 @@ VARIANTS = {
     "pre_iso0": ("pregather", {"layout": "degree", "pack": 0, "iso_rows": 0}),
     "pre_short": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1}),
     "pre_short_side1": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "side_tiles": 1}),
+    "pre_short_ht64": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "hub_threshold": 64}),
+    "pre_short_ht96": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "hub_threshold": 96}),
     "pre_short_split": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "split_tr": 1}),
     "pre_side1": ("pregather", {"layout": "degree", "pack": 0, "side_tiles": 1}),
     "pre_side2": ("pregather", {"layout": "degree", "pack": 0, "side_tiles": 2}),
