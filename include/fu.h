@@ -331,7 +331,9 @@ int fu_dist_exchange_local(fu_handle **hs, int32_t nranks);
 int fu_dist_run_local(fu_handle **hs, int32_t nranks, int32_t rounds);
 /* Device time (ms) of the last round's halo on the rank's communication stream: from the
  * start of the pack (boundary tiles done) to the ghost slots written. The halo overlaps the
- * round's interior tiles. Waits for that halo. FU_ERR_STATE before the first exchange. */
+ * round's interior tiles. Waits for that halo. FU_ERR_STATE before the first exchange; 0 for
+ * an RCCL rank with nothing to send or receive (one rank), whose rounds skip the
+ * communication stream altogether. */
 int fu_dist_halo_time(fu_handle *h, float *ms);
 
 /* Partition-aware random geometric graph: rank `part` of `nparts` generates only its slab

@@ -53,6 +53,7 @@ struct DistState {
   hipEvent_t ev_h0 = nullptr, ev_h1 = nullptr;
   bool timed_once = false;
   bool halo_pending = false;
+  bool any_halo = true;          // RCCL transport: this rank sends or receives estimates (else no comm-stream hop)
   int64_t packed_round = -1;     // in-process transport: round whose packed halo awaits the exchange
   int64_t exchanged_round = -1;  // in-process transport: last round whose halo was exchanged
 };
@@ -135,6 +136,10 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
   }
   double *a = fu__handle_halo_a(h);
   hipStream_t cs = d->comm_stream;
+  if (d->comm && !d->any_halo) {  // nothing to exchange (one rank): no hop through the comm stream
+    d->timed_once = true;
+    return FU_OK;
+  }
   HIPD_TRY(hipEventRecord(d->ev_bnd, s));
   HIPD_TRY(hipStreamWaitEvent(cs, d->ev_bnd, 0));
   HIPD_TRY(hipEventRecord(d->ev_h0, cs));
@@ -215,6 +220,7 @@ static int dist_create(int32_t n_local, int64_t e_local, const int64_t *rowptr, 
   d->send_a_off.assign(send_a_off, send_a_off + nranks + 1);
   d->recv_a_off.assign(recv_a_off, recv_a_off + nranks + 1);
   d->n_send_a = nsa;
+  d->any_halo = nsa > 0 || recv_a_off[nranks] > 0;
   auto bail = [&](int code) { fu_destroy(h); return code; };
   auto alloc = [&](void **p, size_t bytes) { return hipMalloc(p, bytes ? bytes : 8) == hipSuccess; };
   if (!alloc((void **)&d->send_a_idx, sizeof(int) * nsa) || !alloc((void **)&d->sbuf_a, sizeof(double) * nsa))
@@ -335,6 +341,10 @@ int fu_dist_halo_time(fu_handle *h, float *ms) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   if (!d) return fail(FU_ERR_ARG, "fu_dist_halo_time: not a multi-GPU handle");
   if (!d->timed_once) return fail(FU_ERR_STATE, "fu_dist_halo_time: no halo exchanged yet");
+  if (d->comm && !d->any_halo) {  // a rank with nothing to exchange
+    *ms = 0.0f;
+    return FU_OK;
+  }
   // in-process transport: ev_h0 is re-recorded by every round's pack, ev_h1 only by the
   // exchange, so the pair is one halo only when the last packed round was exchanged
   if (!d->comm && d->packed_round != d->exchanged_round)
