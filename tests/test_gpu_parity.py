@@ -949,6 +949,21 @@ def test_bench_rccl_two_ranks_parity_and_convergence():
     assert line["err_after_conv_rounds"] is not None and line["components"] >= 1
 
 
+def test_bench_rccl_parity_arrays_one_rank():
+    """bench.py's RCCL correctness check, end to end at one RCCL rank (the only size one GPU
+    allows): the slab run through fu_dist_create + RCCL, rank 0's single-GPU reference on
+    the global RGG and the bitwise verdict. The N > 1 gather and the slab order are the
+    ones test_dist_rgg_slabs_local_transport_bitwise pins on three in-process ranks."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from fu.dist import unique_id
+
+    arrs = bench.rccl_parity_arrays(1, 0, 0, None, unique_id, n=1 << 16, rounds=12)
+    assert bench.parity_verdict(*arrs) == (True, "bitwise")
+
+
 def test_copy_bandwidth_plausible():
     """bench.py's roofline.copy_GBs: a float4 copy of 256 MB reads as an HBM-class rate."""
     gbs = fu.copy_bandwidth(0, 256 << 20, 3)
