@@ -1078,7 +1078,7 @@ constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 #ifndef FU_TR_WAVES
 #define FU_TR_WAVES 1
 #endif
-template <int HOTN>  // LDS capacity of the hot table (0: no hot neighbours)
+template <int HOTN, bool NT = false>  // HOTN: LDS capacity of the hot table (0: none); NT: streamed G_A / G_B non-temporal
 __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
@@ -1182,7 +1182,8 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   unsigned short pos[kPerT];
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
-    val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
+    if constexpr (NT) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
+    else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
   unsigned hx[HOT ? 2 : 1];  // the bucket's hot edges: at most 2 per thread in one pass
@@ -1211,7 +1212,10 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
     }
   }
   __syncthreads();
-  for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
+  for (int q = t; q < ne; q += kTrThreads) {
+    if constexpr (NT) __builtin_nontemporal_store(s_v[q], GB + e0 + q);
+    else GB[e0 + q] = s_v[q];
+  }
   if (next >= bend) break;
   __syncthreads();  // the shared tables and s_v are rewritten for the next bucket
   bk = next;
@@ -2443,6 +2447,7 @@ struct fu_handle {
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
+  int tr_nt = 0;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3177,6 +3182,9 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
       hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
+    else if (h->tr_nt)
+      hipLaunchKernelGGL((k_transpose<0, true>), dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
     else
       hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
@@ -3733,6 +3741,10 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
       free_transpose(h);                            // the ring's size follows the option
       h->lag = lv;
     }
+    return FU_OK;
+  }
+  if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose streams G_A / G_B non-temporally (1)
+    h->tr_nt = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "multi_short")) {  // kernel 9: rows of 129-256 edges as multi-row blocks (1)
