@@ -875,7 +875,6 @@ struct StageArgs {
   const int *dtab[4];                  // per light tile: kStageRuns x (G index - m) of each run
   int sel[4];                          // layout used for tables of width 8, 16, 32, 0
   int f64;                             // kernel 9: always stage the doubles (layout 3)
-  int nt;                              // kernel 9 (tr_nt 2): non-temporal G_A stores
 };
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
@@ -925,11 +924,10 @@ __device__ __forceinline__ void stage_load(ColVec<StageU<T>::EPL> (&c)[StageU<T>
   for (int u = 0; u < U; ++u)
     if (g + u * STEP < g1) ld_cols<EPL>(c[u], colS + g + u * STEP);
 }
-typedef unsigned fu_v4u __attribute__((ext_vector_type(4)));
 template <typename T, bool LDS>
 __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[StageU<T>::U], int g, int g1,
                                           const unsigned char *s_tab, const T *__restrict__ tab, int nb,
-                                          T *__restrict__ G, bool nt) {
+                                          T *__restrict__ G) {
   constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, STEP = kStageThreads * EPL;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -942,15 +940,9 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
         if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
         else val[j] = tab[nb + (int)off];
       }
-      if (nt) {  // kernel 9 (tr_nt 2): G_A is read once, by a later launch
-        fu_v4u w;
-        __builtin_memcpy(&w, val, 16);
-        __builtin_nontemporal_store(w, reinterpret_cast<fu_v4u *>(G + gg));
-      } else {
-        uint4 w;
-        __builtin_memcpy(&w, val, 16);
-        *reinterpret_cast<uint4 *>(G + gg) = w;
-      }
+      uint4 w;
+      __builtin_memcpy(&w, val, 16);
+      *reinterpret_cast<uint4 *>(G + gg) = w;
     }
   }
 }
@@ -962,7 +954,7 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
 template <typename T, bool LDS>
 __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt, int g0, int g1,
                                            const unsigned short *__restrict__ colS,
-                                           const T *__restrict__ tab, T *__restrict__ G, bool nt) {
+                                           const T *__restrict__ tab, T *__restrict__ G) {
   constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, BSTEP = U * kStageThreads * EPL;
   constexpr int kW = kStageLds / 16 / kStageThreads;
   const int t = threadIdx.x;
@@ -993,11 +985,11 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
   for (;;) {
     if (g >= g1) break;
     stage_load<T, LDS>(cb, g + BSTEP, g1, colS);
-    stage_put<T, LDS>(ca, g, g1, s_tab, tab, nb, G, nt);
+    stage_put<T, LDS>(ca, g, g1, s_tab, tab, nb, G);
     g += BSTEP;
     if (g >= g1) break;
     stage_load<T, LDS>(ca, g + BSTEP, g1, colS);
-    stage_put<T, LDS>(cb, g, g1, s_tab, tab, nb, G, nt);
+    stage_put<T, LDS>(cb, g, g1, s_tab, tab, nb, G);
     g += BSTEP;
   }
 }
@@ -1037,10 +1029,10 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
   do {                                                                                                \
     if ((int)sizeof(T) <= LB)                                                                         \
       stage_body<T, true>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),         \
-                          reinterpret_cast<T *>(G), sa.nt != 0);                                      \
+                          reinterpret_cast<T *>(G));                                                  \
     else                                                                                              \
       stage_body<T, false>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),        \
-                           reinterpret_cast<T *>(G), sa.nt != 0);                                     \
+                           reinterpret_cast<T *>(G));                                                 \
   } while (0)
   if (wb == 1) FU_BODY(unsigned char);
   else if (wb == 2) FU_BODY(unsigned short);
@@ -1190,13 +1182,9 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   unsigned short pos[kPerT];
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
-    if constexpr (NT) {
-      val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
-      pos[k] = g[k] >= 0 ? __builtin_nontemporal_load(pos16 + g[k]) : (unsigned short)0;
-    } else {
-      val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
-      pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
-    }
+    if constexpr (NT) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
+    else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
+    pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
   unsigned hx[HOT ? 2 : 1];  // the bucket's hot edges: at most 2 per thread in one pass
   int h0 = 0, h1 = 0;
@@ -1621,7 +1609,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // writes f_r when another kernel, fu_get_flows or a tile rebuild needs it.
 constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
-template <bool CHECK, int LAGM = 0, bool NTG = false>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1; NTG: G_B loads non-temporal
+template <bool CHECK, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
@@ -1672,10 +1660,8 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = min(c * kMCH + lane, max(rd[j] - 1, 0));
-      if constexpr (NTG) er[j] = __builtin_nontemporal_load(Gb + rb[j] + k);
-      else er[j] = Gb[rb[j] + k];
-      if constexpr (mat && NTG) eo[j] = __builtin_nontemporal_load(Gb_old + rb[j] + k);
-      else if constexpr (mat) eo[j] = Gb_old[rb[j] + k];
+      er[j] = Gb[rb[j] + k];
+      if constexpr (mat) eo[j] = Gb_old[rb[j] + k];
       if constexpr (mat) fo[j] = ld_f(F, rb[j] + k);
       else fo[j] = ld_fo(F, rb[j] + k, fm, ro2[j]);
     }
@@ -2461,7 +2447,7 @@ struct fu_handle {
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
-  int tr_nt = 0;              // kernel 9: non-temporal G_A / position loads and G_B stores in k_transpose (1), G_A stores in k_stage (2), G_B loads in k_heavy_multi (3)
+  int tr_nt = 0;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3156,7 +3142,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   sa.brange[3] = h->tr.brange;
   sa.colS[3] = h->tr.colS;
   sa.f64 = 1;
-  sa.nt = h->tr_nt >= 2;
   {
     hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap,
                        cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
@@ -3276,16 +3261,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   auto tiles = [&](auto C) {
     if (multi) {
       auto hm = [&](auto L) {
-        if (h->tr_nt >= 3)
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value, true>),
-                             dim3((n_multi + kMR - 1) / kMR), dim3(kBlock), 0, split ? h->stream3 : h->stream,
-                             h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F, c.ap2, c.an, h->target,
-                             c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old, h->tr.hist[p]);
-        else
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
-                             dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
-                             h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm,
-                             Gb_old, h->tr.hist[p]);
+        hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
+                           dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
+                           h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
+                           h->tr.hist[p]);
       };
       if (!lag_multi) hm(std::integral_constant<int, 0>{});
       else if (lagm == 1) hm(std::integral_constant<int, 1>{});
@@ -3764,8 +3743,8 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     }
     return FU_OK;
   }
-  if (!std::strcmp(key, "tr_nt")) {  // kernel 9: G_A / G_B streamed non-temporally (1: k_transpose, 2: and k_stage)
-    if (value < 0 || value > 3) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0, 1, 2 or 3");
+  if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose streams G_A / G_B non-temporally (1)
+    if (value != 0 && value != 1) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0 or 1");
     h->tr_nt = (int)value;
     return FU_OK;
   }
