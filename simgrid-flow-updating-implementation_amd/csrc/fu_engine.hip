@@ -2447,7 +2447,7 @@ struct fu_handle {
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
-  int tr_nt = 0;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
+  int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
