@@ -1609,7 +1609,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // writes f_r when another kernel, fu_get_flows or a tile rebuild needs it.
 constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
-template <bool CHECK, int LAGM = 0, bool NTG = false>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1; NTG: G_B loads non-temporal
+template <bool CHECK, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
     const int *__restrict__ hrows, int nrows, const int *__restrict__ rowptr, const double *__restrict__ v,
     double *__restrict__ F, const double *__restrict__ a_prev2, double *__restrict__ a_new,
@@ -1660,10 +1660,8 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int k = min(c * kMCH + lane, max(rd[j] - 1, 0));
-      if constexpr (NTG) er[j] = __builtin_nontemporal_load(Gb + rb[j] + k);
-      else er[j] = Gb[rb[j] + k];
-      if constexpr (mat && NTG) eo[j] = __builtin_nontemporal_load(Gb_old + rb[j] + k);
-      else if constexpr (mat) eo[j] = Gb_old[rb[j] + k];
+      er[j] = Gb[rb[j] + k];
+      if constexpr (mat) eo[j] = Gb_old[rb[j] + k];
       if constexpr (mat) fo[j] = ld_f(F, rb[j] + k);
       else fo[j] = ld_fo(F, rb[j] + k, fm, ro2[j]);
     }
@@ -2449,7 +2447,7 @@ struct fu_handle {
   int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
-  int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1), and G_B loads in k_heavy_multi (2)
+  int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3263,16 +3261,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   auto tiles = [&](auto C) {
     if (multi) {
       auto hm = [&](auto L) {
-        if (h->tr_nt >= 2)  // the multi-row blocks' G_B loads non-temporal as well
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value, true>),
-                             dim3((n_multi + kMR - 1) / kMR), dim3(kBlock), 0, split ? h->stream3 : h->stream,
-                             h->hrows + h->multi_geo[1][0], n_multi, h->rowptr, h->v, c.F, c.ap2, c.an, h->target,
-                             c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old, h->tr.hist[p]);
-        else
-          hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
-                             dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
-                             h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm,
-                             Gb_old, h->tr.hist[p]);
+        hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
+                           dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
+                           h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
+                           h->tr.hist[p]);
       };
       if (!lag_multi) hm(std::integral_constant<int, 0>{});
       else if (lagm == 1) hm(std::integral_constant<int, 1>{});
@@ -3752,7 +3744,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose streams G_A / G_B non-temporally (1)
-    if (value < 0 || value > 2) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0, 1 or 2");
+    if (value != 0 && value != 1) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0 or 1");
     h->tr_nt = (int)value;
     return FU_OK;
   }

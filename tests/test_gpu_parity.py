@@ -144,7 +144,7 @@ def test_option_errors():
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
-    for key, val in (("side_tiles", 3), ("side_tiles", -1), ("tr_nt", 3)):
+    for key, val in (("side_tiles", 3), ("side_tiles", -1), ("tr_nt", 2)):
         with pytest.raises(fu.FuError):
             eng.set_option(key, val)
     with pytest.raises(fu.FuError):
@@ -630,7 +630,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
 
 
 @pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "short0", "short_side2_nolag", "trnt0", "trnt_pipe", "trnt2", "trnt2_nolag"])
+                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "short0", "short_side2_nolag", "trnt0", "trnt_pipe"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -675,11 +675,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("iso_rows", 0)
     elif multi == "trnt0":  # plain G_A loads / G_B stores in the transposes (tr_nt is the default)
         eng.set_option("tr_nt", 0)
-    elif multi == "trnt2":  # and the multi-row blocks' G_B loads
-        eng.set_option("tr_nt", 2)
-    elif multi == "trnt2_nolag":
-        eng.set_option("tr_nt", 2)
-        eng.set_option("lag", 0)
     elif multi == "trnt_pipe":  # (the pipelined transpose keeps its plain loads and stores)
         eng.set_option("tr_nt", 1)
         eng.set_option("tr_pipe", 1)

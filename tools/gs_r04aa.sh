@@ -1,4 +1,5 @@
 # round 4, GPU session aa: the multi-row blocks' G_B loads non-temporal too (tr_nt 2): the
+# (record of a measured session: tr_nt 2 was removed after it lost)
 # kernel-9 parity tests first (a crash ends the session), then the R-MAT A/B against tr_nt 1
 set -o pipefail
 mkdir -p gpurun_out/aa
