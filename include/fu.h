@@ -122,19 +122,13 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 0 = one block per bucket).
  * "multi_heavy"   kernel 9: rows of more than 256 edges as multi-row chain blocks (default 1);
  *                 "multi_mid" 0 keeps the rows of 257-1024 edges in the register launch.
- * "tr_pipe"       kernel 9: software-pipelined transpose (default 0; needs tr_bpx > 0).
  * "lag"           kernel 9: the multi-row heavy rows leave f_r unwritten and write f_{r-2}
  *                 from f_{r-4} and their kept a_{r-4}, two rounds later (default 1); the
  *                 lagged flows are finalized before fu_get_flows, other kernels and rebuilds.
  * "tr_hot"        kernel 9: neighbours of id < value served from an LDS table in the
  *                 transpose instead of staged (default 0; <= 10240).
- * "hub_prio"      kernel 9: the mega-hub chain waves run at issue priority 3 (default 0).
- * "side_tiles"    kernel 9: 1 = the light tiles, 2 = also the rows of 129-256 edges, on the
- *                 side stream behind the hub path once every bucket is transposed (default 0).
- * "split_tr"      kernel 9: the multi-row heavy rows on a third stream once their own buckets
- *                 are transposed (default 0).
- * "iso_rows"      kernel 9: the trailing light tiles of isolated rows (the degree layout's last
- *                 rows) run as one thread per row (k_isolated, 1, default) or as tiles (0).
+ * "iso_rows"      kernel 9: the trailing run of degree-0 rows (the degree layout's last rows)
+ *                 runs as one thread per row (k_isolated, 1, default) or as light tiles (0).
  * "multi_short"   kernel 9: the rows of 129-256 edges run in the multi-row blocks too (default 1;
  *                 0: one row per wave, four per block).
  * "tr_nt"         kernel 9: k_transpose's G_A loads and G_B stores non-temporal (default 1).
@@ -146,7 +140,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "stage_layout"  kernel 8, tests: -1 = by packing width, 0..3 = the 1/2/4/8-byte layout.
  * "staged_lo"     kernel 8: staged indices loaded ahead of the flows (1, default) or
  *                 interleaved with them (0; the round-1 order, kept for A/B and tests).
- * Timing-only ablations ("diag") exist only in a -DFU_DIAG build (tools/). */
+ * Removed after measurement (FU_ERR_ARG): "tr_pipe", "hub_prio", "side_tiles", "split_tr"
+ * (DESIGN.md §4.12), "hub_multi", "hub_blocks", "fuse", "light_geo". */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);

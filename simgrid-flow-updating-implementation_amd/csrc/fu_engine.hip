@@ -19,8 +19,10 @@
 #include <vector>
 
 #include "fu_common.h"
+#include "fu_plan.h"
 
 using namespace fu;
+namespace FP = fu::plan;
 
 #define HIP_TRY(expr)                                                                     \
   do {                                                                                    \
@@ -31,7 +33,23 @@ using namespace fu;
 
 namespace {
 
+// row-class and table constants shared with the host plans (fu_plan.h)
+using FP::kGeoEdges;
+using FP::kGeoNodes;
+using FP::kHeavyRL;
+using FP::kMidRL;
+using FP::kMR;
+using FP::kR0E;
+using FP::kStageLds;
+using FP::kStageRuns;
+using FP::kStageTE;
+using FP::kStageTN;
+using FP::kTrBE;
+using FP::kTrHot;
+using FP::kTrMaxP;
+
 constexpr int kBlock = 256;      // threads per block (4 waves of 64)
+static_assert(kBlock == FP::kHubBlk, "k_hub_stage / k_hub_flows blocks follow the plan's hub table");
 constexpr int kTileEdges = 2048;  // max edges staged in LDS per light tile
 constexpr int kTileNodes = kBlock;
 
@@ -279,7 +297,6 @@ __device__ __forceinline__ void st_fo(double *F, int e, double v, double f_old, 
 // listed the row of every block's first edge (blk_row), the block's rows' pointers go to
 // LDS, and each edge's row is a short binary search there (a hub's edges all land in one
 // row; a block whose rows span more than kR0E, runs of isolated nodes, searches rowptr).
-constexpr int kR0E = 1024;
 __global__ __launch_bounds__(kBlock) void k_round0_flows(long long E, const int *__restrict__ rowptr,
                                                          const int *__restrict__ blk_row,
                                                          const double *__restrict__ a, double *__restrict__ F0,
@@ -409,14 +426,9 @@ __device__ inline T ld_stream(const T *p) {
 // Heavy rows (one per wave) up to 64 x max(kHeavyRL, chunk / 64) edges keep their operands
 // in registers (measured on R-MAT-24: 8 or 16 per lane cost more in occupancy than the
 // second pass they save).
-#ifndef FU_HEAVY_RL
-#define FU_HEAVY_RL 4
-#endif
-constexpr int kHeavyRL = FU_HEAVY_RL;
 // kernel 9's second heavy launch: rows of 64 x (kHeavyRL, kMidRL] edges keep their operands
 // in registers (no second pass over the row for its flows), at a lower occupancy than the
 // other heavy rows can afford (R-MAT-24: 19 % of the edges sit in rows of 641-1024)
-constexpr int kMidRL = 16;
 
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
@@ -432,7 +444,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     int rslot, const double2 *__restrict__ hubxy, const int *__restrict__ hub_off,
     const int *__restrict__ hrows, int hub_sep, const double *__restrict__ Gb, int fm,
     const unsigned short *__restrict__ col16 = nullptr, const int *__restrict__ cbase = nullptr,
-    const int *__restrict__ tnar = nullptr, int hub_prio = 0) {
+    const int *__restrict__ tnar = nullptr) {
   static_assert(TE % kBlock == 0 && TN <= kBlock && TN <= 256, "tile geometry");
   const PackCtl pp = ctl[rslot ^ 1];  // packing of a_{r-1} (the table gathered here)
   const PackCtl pc = ctl[2];          // packing of a_r (the table written here)
@@ -585,10 +597,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     constexpr int CH = TE / 2, PL = CH / 64;  // pairs per chunk, per lane
     if (PRE && t < 64) {
       // kernel 9: the row's estimates are pre-gathered (Gb), so the chain wave streams Gb
-      // and the old flows itself, coalesced, and rebuilds fr as k_hub_stage would. hub_prio:
-      // the chain wave issues ahead of the other waves on its SIMD (a hub's chain is one
-      // dependent fp64 add per element; shared issue slots stretch it)
-      if (hub_prio) __builtin_amdgcn_s_setprio(3);
+      // and the old flows itself, coalesced, and rebuilds fr as k_hub_stage would
       const double own2 = a_prev2[i];
       double nf[PL], ng[PL];
 #pragma unroll
@@ -862,10 +871,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
 // kernel 4 heavy tiles in a launch of their own. Results are bitwise those of kernel 4.
 // ------------------------------------------------------------------------------------
 constexpr int kStageThreads = 1024;   // one block per CU (the slice takes 128 KB of its LDS)
-constexpr int kStageLds = 131072;     // bytes of table per slice
-constexpr int kStageTE = 1024, kStageTN = 128;
 constexpr int kStageU = 4;            // steps per lane in flight
-constexpr int kStageRuns = 64;        // slice runs per tile the u16 index can address
 
 struct StageArgs {
   int P[4], Q[4], SN[4], NB[4];        // slices, blocks per slice, nodes per slice, blocks
@@ -1055,19 +1061,12 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
 // beside the flows. Bytes per edge: stage 2 + 8, transpose 8 + 2 + 8, round 8 (instead of
 // col 4 + one random 8-byte gather).
 // ------------------------------------------------------------------------------------
-#ifndef FU_TR_BE
-#define FU_TR_BE 8192
-#endif
-constexpr int kTrBE = FU_TR_BE;  // edges per bucket (8K: 76 KB of LDS, two blocks per CU; R-MAT-24 7.78 -> 7.59 ms vs 16K)
-static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 positions, coarse table");
-constexpr int kTrMaxP = 2048;  // slices of 16K nodes: n <= 2^25
 constexpr int kTrThreads = 1024;
 // Hot estimates (option tr_hot): the neighbours of id < H (H <= kTrHot; under the degree
 // layout the H highest-degree nodes: R-MAT-24's first 10K take 23 % of all gathers) never
 // pass through the staging launch. Each transpose block keeps a_{r-1}[0, H) in LDS beside
 // its bucket and serves a bucket's hot edges from a per-bucket list {column, position} in
 // edge order: 4 B per hot edge read instead of 2 + 8 staged, 8 + 2 transposed.
-constexpr int kTrHot = 10240;  // 80 KB of LDS; with the 76 KB bucket tables: 156 KB of 160
 constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 
 // Persistent over its buckets: grid = 8 x (blocks per XCD); XCD x owns the contiguous
@@ -1219,183 +1218,6 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   if (next >= bend) break;
   __syncthreads();  // the shared tables and s_v are rewritten for the next bucket
   bk = next;
-  }
-}
-
-// k_transpose software-pipelined over the block's buckets (option tr_pipe): the G_A and
-// position loads of bucket k + 1 are in flight while bucket k is scattered into LDS and
-// stored, and bucket k + 1's run table and searches are built while bucket k's loads land.
-// Every iteration issues the same loads (a missing next bucket reads element 0 and ignores
-// it), so the wait for bucket k's loads leaves bucket k + 1's in flight. Same G_B as
-// k_transpose; HOTN as k_transpose (the hot edges' list entries are loaded with the bucket's
-// other loads, their values read from the block's LDS copy of a_{r-1}[0, H)).
-template <int HOTN>
-__global__ __launch_bounds__(kTrThreads) void k_transpose_pipe(int b0, int nbk, int P, long long E,
-                                                             const int *__restrict__ offT,
-                                                             const double *__restrict__ GA,
-                                                             const unsigned short *__restrict__ pos16,
-                                                             double *__restrict__ GB,
-                                                             const double *__restrict__ a_prev, int H,
-                                                             const int *__restrict__ hoff,
-                                                             const unsigned *__restrict__ hlist) {
-  constexpr bool HOT = HOTN > 0;
-  __shared__ double s_v[kTrBE];
-  __shared__ double s_hot[HOT ? HOTN : 1];
-  __shared__ unsigned short s_m[kTrMaxP + 1];
-  __shared__ int s_o[kTrMaxP];
-  __shared__ int s_c[kTrBE / 64 + 1];
-  __shared__ int s_w[kTrThreads / 64];
-  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int per = (nbk + 7) >> 3;
-  const int nj = (int)(gridDim.x >> 3);
-  int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-  const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
-  if (bk >= bend) return;
-  if (HOT)  // visible after the first table barrier
-    for (int q = t; q < H; q += kTrThreads) s_hot[q] = a_prev[q];
-  constexpr int kPerT = kTrBE / kTrThreads;
-  int o[2], len[2];
-  auto load_runs = [&](int bkk) {  // clamped: a bucket past the range loads the last one's
-    const int bb = b0 + min(bkk, bend - 1);
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int sl = min(2 * t + j, P - 1);
-      const int a0 = offT[(long long)bb * P + sl], a1 = offT[(long long)(bb + 1) * P + sl];
-      o[j] = 2 * t + j < P ? a0 : 0;
-      len[j] = 2 * t + j < P ? a1 - a0 : 0;
-    }
-  };
-  // run table of the bucket whose runs are in o / len: s_m (first element of each run),
-  // s_o (its G_A index), s_c (coarse table); returns the staged element count
-  auto tables = [&]() -> int {
-    int x = len[0] + len[1];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off, 64);
-      if (lane >= off) x += y;
-    }
-    __syncthreads();  // the previous bucket's searches are done with the tables
-    if (lane == 63) s_w[w] = x;
-    __syncthreads();
-    int base = 0;
-    for (int k = 0; k < w; ++k) base += s_w[k];
-    const int excl = base + x - (len[0] + len[1]);
-    if (2 * t < P) {
-      s_m[2 * t] = excl;
-      s_o[2 * t] = o[0];
-    }
-    if (2 * t + 1 < P) {
-      s_m[2 * t + 1] = excl + len[0];
-      s_o[2 * t + 1] = o[1];
-    }
-    if (t == 0) {
-      int tot = 0;
-      for (int k = 0; k < kTrThreads / 64; ++k) tot += s_w[k];
-      s_m[P] = tot;
-    }
-    __syncthreads();
-    const int nst = s_m[P];
-    if (t < kTrBE / 64) {
-      const int m = t * 64;
-      int lo = 1, hi = P;
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if (s_m[mid] > m) hi = mid; else lo = mid + 1;
-      }
-      s_c[t] = lo;
-    }
-    if (t == 0) s_c[kTrBE / 64] = P;
-    __syncthreads();
-    return nst;
-  };
-  auto search = [&](int nst, int (&g)[kPerT]) {
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k) {
-      const int m = t + k * kTrThreads;
-      g[k] = -1;
-      if (m < nst) {
-        int lo = s_c[m >> 6], hi = s_c[(m >> 6) + 1];
-        while (lo < hi) {
-          const int mid = (lo + hi) >> 1;
-          if (s_m[mid] > m) hi = mid; else lo = mid + 1;
-        }
-        const int run = lo - 1;
-        g[k] = s_o[run] + (m - s_m[run]);
-      }
-    }
-  };
-  // hot edges of a bucket: at most 2 list entries per thread with the other loads
-  unsigned hxA[2] = {0u, 0u}, hxB[2] = {0u, 0u};
-  int hrA[2] = {0, 0}, hrB[2] = {0, 0};  // the bucket's hot list range
-  auto issue = [&](const int (&g)[kPerT], double (&val)[kPerT], int (&pos)[kPerT], int bkk, bool valid,
-                   unsigned (&hx)[2], int (&hr)[2]) {
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k) {  // unconditional, from a valid index
-      const int q = max(g[k], 0);
-      val[k] = GA[q];
-      pos[k] = g[k] >= 0 ? (int)pos16[q] : -1;
-    }
-    if (HOT) {
-      const int bb = b0 + min(bkk, bend - 1);
-      hr[0] = valid ? hoff[bb] : 0;
-      hr[1] = valid ? hoff[bb + 1] : 0;
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int q = hr[0] + t + k * kTrThreads;
-        hx[k] = hlist[q < hr[1] ? q : 0];
-      }
-    }
-  };
-  // bucket cur: the loads in (val, pos) -> s_v by position -> G_B, coalesced
-  auto finish = [&](int cur, const double (&val)[kPerT], const int (&pos)[kPerT], const unsigned (&hx)[2],
-                    const int (&hr)[2]) {
-    const long long e0 = (long long)(b0 + cur) * kTrBE;
-    const int ne = (int)min((long long)kTrBE, E - e0);
-    __syncthreads();  // the previous bucket's G_B stores have read s_v
-#pragma unroll
-    for (int k = 0; k < kPerT; ++k)
-      if (pos[k] >= 0) s_v[pos[k]] = val[k];
-    if (HOT) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-        if (hr[0] + t + k * kTrThreads < hr[1]) s_v[hx[k] & 0xFFFFu] = s_hot[hx[k] >> 16];
-      for (int q = hr[0] + t + 2 * kTrThreads; q < hr[1]; q += kTrThreads) {  // > 2048 hot edges
-        const unsigned x = hlist[q];
-        s_v[x & 0xFFFFu] = s_hot[x >> 16];
-      }
-    }
-    __syncthreads();
-    for (int q = t; q < ne; q += kTrThreads) GB[e0 + q] = s_v[q];
-  };
-  int gA[kPerT], gB[kPerT], pA[kPerT], pB[kPerT];
-  double vA[kPerT], vB[kPerT];
-  load_runs(bk);
-  search(tables(), gA);
-  load_runs(bk + nj);
-  issue(gA, vA, pA, bk, true, hxA, hrA);
-  // one step: build + issue bucket nx's loads into N, then finish bucket cur from C
-  auto step = [&](int cur, int (&gN)[kPerT], double (&vN)[kPerT], int (&pN)[kPerT], unsigned (&hN)[2],
-                  int (&rN)[2], const double (&vC)[kPerT], const int (&pC)[kPerT], const unsigned (&hC)[2],
-                  const int (&rC)[2]) -> bool {
-    const int nx = cur + nj;
-    const bool more = nx < bend;
-    {
-      const int nst = tables();  // (runs of nx, or the clamped last bucket's: ignored)
-      search(nst, gN);
-      if (!more)
-#pragma unroll
-        for (int k = 0; k < kPerT; ++k) gN[k] = -1;
-    }
-    load_runs(nx + nj);
-    issue(gN, vN, pN, nx, more, hN, rN);
-    finish(cur, vC, pC, hC, rC);
-    return more;
-  };
-  for (;;) {
-    if (!step(bk, gB, vB, pB, hxB, hrB, vA, pA, hxA, hrA)) break;
-    bk += nj;
-    if (!step(bk, gA, vA, pA, hxA, hrA, vB, pB, hxB, hrB)) break;
-    bk += nj;
   }
 }
 
@@ -1607,7 +1429,6 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 // already (fm = 1, 2: computed, and stored as the base of round r + 2); LAGM = 2: F holds
 // f_{r-4} (the previous round of this parity was lagged). lag_finalize
 // writes f_r when another kernel, fu_get_flows or a tile rebuild needs it.
-constexpr int kMR = 16;   // rows per block
 constexpr int kMCH = 64;  // elements per row per chunk (one per lane)
 template <bool CHECK, int LAGM = 0>  // LAGM: 0 = no lag, 1 = lagin 0, 2 = lagin 1
 __global__ __launch_bounds__(kBlock) void k_heavy_multi(
@@ -2370,13 +2191,10 @@ struct fu_handle {
   std::vector<int64_t> h_orig_rowptr;
   hipStream_t stream = nullptr;
   hipStream_t stream2 = nullptr;            // kernel 4's heavy tiles, concurrently (fork_heavy)
-  hipStream_t stream3 = nullptr;            // kernel 9 split_tr: the heavy rows beside the last transposes
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
   hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_tr = nullptr;  // kernel 9 side_tiles: every bucket transposed
-  hipEvent_t ev_htr = nullptr, ev_s3 = nullptr;  // kernel 9 split_tr: heavy-row buckets done; stream3 done
   int32_t n = 0;
   int64_t E = 0;
   int32_t na = 0;  // estimate slots: n local + ghost estimates (multi-GPU)
@@ -2401,7 +2219,6 @@ struct fu_handle {
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
-  int tr_pipe = 0;       // kernel 9: software-pipelined transpose (k_transpose_pipe; needs tr_bpx > 0)
   int tr_hot = 0;        // kernel 9: neighbours of id < tr_hot (<= kTrHot) served from the transpose's LDS
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int c16 = 1;           // kernel 4: narrow light tiles read 2-byte column offsets
@@ -2432,6 +2249,7 @@ struct fu_handle {
   int nbound_geo[4] = {0, 0, 0, 0};  // multi-GPU: light tiles with ghost neighbours, right after the heavy ones
   int niso_geo[4] = {0, 0, 0, 0};    // kernel 9: trailing light tiles of isolated rows only (k_isolated runs them)
   int iso0_geo[4] = {0, 0, 0, 0};    // ... their first row (rows [iso0, n) are isolated)
+  FP::Tiles tiles1;                  // host copy of geometry 1's plan (kernel 9's schedule)
   int mid_geo[4][2] = {};            // heavy tiles [mid_geo[0], mid_geo[1]) lead with a row of 64 x (kHeavyRL, kMidRL] edges
   int multi_geo[4][2] = {};          // hrows offset and count of this geometry's sorted heavy rows
   int multi_heavy = 1;               // kernel 9: rows > 64 x kHeavyRL as k_heavy_multi blocks
@@ -2442,9 +2260,6 @@ struct fu_handle {
   int64_t hub_total = 0;
   int4 *hub_rows = nullptr;  // {node, row begin, row end, offset in hubxy}
   int *hub_blk = nullptr;    // per 256-edge block of the hub edges: the hub of its first edge
-  int hub_prio = 0;           // kernel 9: the hub chain waves at instruction-issue priority 3 (s_setprio)
-  int side_tiles = 0;         // kernel 9: light tiles (1; + rows of 129-256 edges: 2) on the side stream
-  int split_tr = 0;           // kernel 9: the multi-row heavy rows on stream3 once their buckets are transposed
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
   int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
@@ -2480,7 +2295,7 @@ struct fu_handle {
   void *stG = nullptr;                    // staged estimates, 8 B per G element
   int seen_width = 0;                     // packing width the host last saw
   int st_force = -1;                      // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
-  std::vector<int4> h_light;              // host copy (layout construction)
+  std::vector<FP::I4> h_light;            // host copy (layout construction)
   // kernel 9 (pregather): slice-major G_A, per-bucket run starts, edge-order Gb
   struct TransLayout {
     int P = 0, Q = 0, NB = 0, B = 0;      // slices, blocks per slice, stage blocks, buckets
@@ -2516,112 +2331,53 @@ extern "C" void fu__dist_free(fu_handle *h);
 
 namespace {
 
-constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
-constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 
-// Kernel 4 tiles of te edges x tn nodes: mega hubs ({i, -3, b, e}), heavy rows (four per
-// block, one per wave, longest first: {hrows offset, -4, count, 0}; or one per block
-// {i, -1, b, e}), then light tiles ({first node, end node, first edge, end edge}).
-int build_tiles_geom(fu_handle *h, int te, int tn, int4 **dst, int **nar, int *count, int *nheavy,
-                     int *nbound, int *mid,
-                     int *multi, int *niso, int *iso0) {
-  std::vector<int4> heavy, light, hubs;
-  const int32_t n = h->n;
-  int32_t i = 0;
-  while (i < n) {
-    int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    if (d > h->mega_hub) {
-      hubs.push_back(make_int4(i, -3, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
-      ++i;
-      continue;
-    }
-    if (d > h->hub_threshold || d > te) {
-      heavy.push_back(make_int4(i, -1, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1]));
-      ++i;
-      continue;
-    }
-    int32_t b = i;
-    int64_t eb = h->h_rowptr[b];
-    while (i < n && i - b < tn) {
-      int64_t di = h->h_rowptr[i + 1] - h->h_rowptr[i];
-      if (di > h->hub_threshold || di > te || di > h->mega_hub) break;  // (mega_hub may be < hub_threshold)
-      if (h->h_rowptr[i + 1] - eb > te) break;
-      ++i;
-    }
-    light.push_back(make_int4(b, i, (int)h->h_rowptr[b], (int)h->h_rowptr[i]));
-  }
-  // every mega hub must lead the list: its tile index is its hub_off / hubxy slot
-  int64_t n_mega = 0;
-  for (int32_t r = 0; r < n; ++r) n_mega += h->h_rowptr[r + 1] - h->h_rowptr[r] > h->mega_hub;
-  if ((int64_t)hubs.size() != n_mega) return fail(FU_ERR_STATE, "build_tiles: a mega hub fell into a light tile");
-  // mega hubs, then heavy tiles first so their long sequential chains start early
-  std::vector<int4> all(hubs);
-  if (h->wave_heavy && !heavy.empty()) {
-    std::vector<int32_t> rows;
-    for (const int4 &hv : heavy) rows.push_back(hv.x);
-    std::stable_sort(rows.begin(), rows.end(), [&](int32_t x, int32_t y) {
-      return h->h_rowptr[x + 1] - h->h_rowptr[x] > h->h_rowptr[y + 1] - h->h_rowptr[y];
-    });
-    const size_t base = h->h_hrows.size();  // each geometry appends its own list
-    h->h_hrows.insert(h->h_hrows.end(), rows.begin(), rows.end());
-    multi[0] = (int)base;  // this geometry's sorted heavy rows (k_heavy_multi takes a prefix)
-    multi[1] = (int)rows.size();
-    // tiles whose longest (first) row fits kMidRL registers per lane but not kHeavyRL
-    auto deg = [&](int32_t x) { return h->h_rowptr[x + 1] - h->h_rowptr[x]; };
-    mid[0] = mid[1] = (int)all.size();
-    for (size_t q = 0; q < rows.size(); q += 4) {
-      const int64_t d0 = deg(rows[q]);
-      if (d0 > 64 * kMidRL) mid[0] = mid[1] = (int)all.size() + 1;
-      else if (d0 > 64 * kHeavyRL) mid[1] = (int)all.size() + 1;
-      all.push_back(make_int4((int)(base + q), -4, (int)std::min<size_t>(4, rows.size() - q), 0));
-    }
-  } else {
-    mid[0] = mid[1] = (int)hubs.size();
-    multi[0] = multi[1] = 0;
-    all.insert(all.end(), heavy.begin(), heavy.end());
-  }
-  *nheavy = (int)all.size();
-  // multi-GPU (ghost estimate slots exist): light tiles that read a ghost go first, so the
-  // halo exchange can start once they are done, beside the interior tiles
-  // the light tiles at the end with no edges (the degree layout's isolated rows: R-MAT-24 has
-  // 7.9 M, 62 K tiles of 128): kernel 9 runs them as k_isolated, one thread per row
-  *niso = 0;
-  *iso0 = h->n;
-  if (h->na == h->n) {
-    size_t q = light.size();
-    while (q > 0 && light[q - 1].z == light[q - 1].w) --q;
-    *niso = (int)(light.size() - q);
-    if (*niso) *iso0 = light[q].x;
-  }
-  *nbound = 0;
-  if (h->na > h->n) {
-    auto has_ghost = [&](const int4 &tl) {
-      for (int32_t e = tl.z; e < tl.w; ++e)
-        if (h->h_col[e] >= h->n) return true;
-      return false;
-    };
-    auto mid = std::stable_partition(light.begin(), light.end(), has_ghost);
-    *nbound = (int)(mid - light.begin());
-  }
-  const size_t nlead = all.size();
-  all.insert(all.end(), light.begin(), light.end());
+// The handle's graph as the host plans see it (fu_plan.h).
+FP::Graph plan_graph(const fu_handle *h) {
+  FP::Graph g;
+  g.n = h->n;
+  g.na = h->na;
+  g.E = h->E;
+  g.rowptr = h->h_rowptr.data();
+  g.col = h->h_col.data();
+  g.cbase = h->h_cbase.data();
+  return g;
+}
+
+// host vector -> fresh device array (at least one element)
+template <typename D, typename S>
+int upload(D **dst, const std::vector<S> &src) {
+  static_assert(sizeof(D) == sizeof(S), "upload: element layouts differ");
   if (*dst) hipFree(*dst);
   *dst = nullptr;
-  *count = (int)all.size();
-  if (int rc = dmalloc(dst, all.size())) return rc;
-  HIP_TRY(hipMemcpy(*dst, all.data(), sizeof(int4) * all.size(), hipMemcpyHostToDevice));
-  // light tiles whose 1024-edge blocks are all narrow read the 2-byte column offsets
-  std::vector<int32_t> nf(all.size(), 0);
-  for (size_t q = nlead; q < all.size(); ++q) {
-    const int64_t a0 = all[q].z, a1 = all[q].w;
-    bool ok = a1 > a0;
-    for (int64_t b = a0 / kR0E; ok && b <= (a1 - 1) / kR0E; ++b) ok = h->h_cbase[b] >= 0;
-    nf[q] = ok ? 1 : 0;
-  }
-  if (*nar) hipFree(*nar);
-  *nar = nullptr;
-  if (int rc = dmalloc(nar, nf.size())) return rc;
-  HIP_TRY(hipMemcpy(*nar, nf.data(), sizeof(int32_t) * nf.size(), hipMemcpyHostToDevice));
+  if (int rc = dmalloc(dst, std::max<size_t>(1, src.size()))) return rc;
+  if (!src.empty()) HIP_TRY(hipMemcpy(*dst, src.data(), sizeof(S) * src.size(), hipMemcpyHostToDevice));
+  return FU_OK;
+}
+
+// Kernel 4 tiles of geometry g (FP::build_tiles_geom: mega hubs, heavy rows, light tiles, the
+// trailing degree-0 rows), uploaded; the heavy rows are appended to h_hrows.
+int build_tiles_geom(fu_handle *h, int geo) {
+  FP::TileOpts o;
+  o.hub_threshold = h->hub_threshold;
+  o.mega_hub = h->mega_hub;
+  o.wave_heavy = h->wave_heavy;
+  FP::Tiles t;
+  std::string why;
+  if (!FP::build_tiles_geom(plan_graph(h), kGeoEdges[geo], kGeoNodes[geo], o, h->h_hrows, t, &why))
+    return fail(FU_ERR_STATE, why);
+  if (int rc = upload(&h->tiles_geo[geo], t.all)) return rc;
+  if (int rc = upload(&h->tnar_geo[geo], t.narrow)) return rc;
+  h->ntiles_geo[geo] = (int)t.all.size();
+  h->nheavy_geo[geo] = t.nheavy;
+  h->nbound_geo[geo] = t.nbound;
+  h->mid_geo[geo][0] = t.mid[0];
+  h->mid_geo[geo][1] = t.mid[1];
+  h->multi_geo[geo][0] = t.multi[0];
+  h->multi_geo[geo][1] = t.multi[1];
+  h->niso_geo[geo] = t.niso;
+  h->iso0_geo[geo] = t.iso0;
+  if (geo == 1) h->tiles1 = t;
   return FU_OK;
 }
 
@@ -2633,34 +2389,15 @@ int build_hubs(fu_handle *h) {
   h->hub_rows = nullptr;
   h->hub_off = nullptr;
   h->hubxy = nullptr;
-  std::vector<int4> rows;
-  std::vector<int32_t> off;
-  int64_t tot = 0;
-  for (int32_t i = 0; i < h->n; ++i) {
-    const int64_t d = h->h_rowptr[i + 1] - h->h_rowptr[i];
-    if (d > h->mega_hub) {
-      rows.push_back(make_int4(i, (int)h->h_rowptr[i], (int)h->h_rowptr[i + 1], (int)tot));
-      off.push_back((int32_t)tot);
-      tot += d;
-    }
-  }
-  h->n_hub = (int)rows.size();
-  h->hub_total = tot;
-  if (rows.empty()) return FU_OK;
-  if (int rc = dmalloc(&h->hub_rows, rows.size())) return rc;
-  if (int rc = dmalloc(&h->hub_off, off.size())) return rc;
-  if (int rc = dmalloc(&h->hubxy, (size_t)tot)) return rc;
-  HIP_TRY(hipMemcpy(h->hub_rows, rows.data(), sizeof(int4) * rows.size(), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(h->hub_off, off.data(), sizeof(int32_t) * off.size(), hipMemcpyHostToDevice));
-  std::vector<int32_t> blk((size_t)((tot + kBlock - 1) / kBlock));
-  for (size_t b = 0, hh = 0; b < blk.size(); ++b) {
-    const int64_t q0 = (int64_t)b * kBlock;
-    while (hh + 1 < off.size() && off[hh + 1] <= q0) ++hh;
-    blk[b] = (int32_t)hh;
-  }
-  if (int rc = dmalloc(&h->hub_blk, blk.size())) return rc;
-  HIP_TRY(hipMemcpy(h->hub_blk, blk.data(), sizeof(int32_t) * blk.size(), hipMemcpyHostToDevice));
-  return FU_OK;
+  FP::Hubs hb;
+  FP::build_hubs(plan_graph(h), h->mega_hub, hb);
+  h->n_hub = (int)hb.rows.size();
+  h->hub_total = hb.total;
+  if (hb.rows.empty()) return FU_OK;
+  if (int rc = upload(&h->hub_rows, hb.rows)) return rc;
+  if (int rc = upload(&h->hub_off, hb.off)) return rc;
+  if (int rc = dmalloc(&h->hubxy, (size_t)hb.total)) return rc;
+  return upload(&h->hub_blk, hb.blk);
 }
 
 void free_transpose(fu_handle *h);
@@ -2671,11 +2408,7 @@ int build_tiles(fu_handle *h) {
   free_transpose(h);  // its hub exclusion follows the tiles
   h->h_hrows.clear();
   for (int g = 0; g < 4; ++g)
-    if (int rc = build_tiles_geom(h, kGeoEdges[g], kGeoNodes[g], &h->tiles_geo[g], &h->tnar_geo[g], &h->ntiles_geo[g],
-                                  &h->nheavy_geo[g],
-                                  &h->nbound_geo[g], h->mid_geo[g], h->multi_geo[g], &h->niso_geo[g],
-                                  &h->iso0_geo[g]))
-      return rc;
+    if (int rc = build_tiles_geom(h, g)) return rc;
   if (h->hrows) hipFree(h->hrows);
   h->hrows = nullptr;
   if (int rc = dmalloc(&h->hrows, std::max<size_t>(1, h->h_hrows.size()))) return rc;
@@ -2689,167 +2422,51 @@ inline double *cur_a(fu_handle *h) { return h->a[(int)((h->rounds + 2) % 3)]; }
 inline double *cur_f(fu_handle *h) { return h->f[(int)((h->rounds + 1) & 1)]; }
 
 // ---- kernel 8 preparation -------------------------------------------------------------
-constexpr int kStageMaxP = 512;  // slices per layout (more: layout not built)
 
 // Light tiles (kStageTE x kStageTN) and the rows above the tile limit (kernel 8).
 int ensure_light(fu_handle *h) {
   if (h->st_tiles) return FU_OK;
-  const int32_t n = h->n;
-  const auto &rp = h->h_rowptr;
-  const int64_t lim = std::min<int64_t>(h->hub_threshold, kStageTE);
-  std::vector<int4> light, heavy;
-  for (int32_t i = 0; i < n;) {
-    const int64_t d = rp[i + 1] - rp[i];
-    if (d > lim) {
-      heavy.push_back(make_int4(i, -1, (int)rp[i], (int)rp[i + 1]));
-      ++i;
-      continue;
-    }
-    const int32_t b = i;
-    while (i < n && i - b < kStageTN) {
-      const int64_t di = rp[i + 1] - rp[i];
-      if (di > lim || rp[i + 1] - rp[b] > kStageTE) break;
-      ++i;
-    }
-    light.push_back(make_int4(b, i, (int)rp[b], (int)rp[i]));
-  }
-  // multi-GPU (ghost estimate slots exist): light tiles that read a ghost go first, so the
-  // halo exchange can start once they are done, beside the interior tiles (as kernel 4)
-  h->st_nbound = 0;
-  if (h->na > h->n) {
-    auto has_ghost = [&](const int4 &tl) {
-      for (int32_t e = tl.z; e < tl.w; ++e)
-        if (h->h_col[e] >= n) return true;
-      return false;
-    };
-    h->st_nbound = (int)(std::stable_partition(light.begin(), light.end(), has_ghost) - light.begin());
-  }
-  h->h_light = light;
-  if (int rc = dmalloc(&h->st_tiles, std::max<size_t>(1, light.size()))) return rc;
-  if (int rc = dmalloc(&h->st_heavy, std::max<size_t>(1, heavy.size()))) return rc;
-  if (!light.empty()) HIP_TRY(hipMemcpy(h->st_tiles, light.data(), sizeof(int4) * light.size(), hipMemcpyHostToDevice));
-  if (!heavy.empty()) HIP_TRY(hipMemcpy(h->st_heavy, heavy.data(), sizeof(int4) * heavy.size(), hipMemcpyHostToDevice));
-  h->st_ntiles = (int)light.size();
-  h->st_nheavy = (int)heavy.size();
+  FP::StageLight sl;
+  FP::build_stage_light(plan_graph(h), h->hub_threshold, sl);
+  h->st_nbound = sl.nbound;
+  h->h_light = sl.light;
+  if (int rc = upload(&h->st_tiles, sl.light)) return rc;
+  if (int rc = upload(&h->st_heavy, sl.heavy)) return rc;
+  h->st_ntiles = (int)sl.light.size();
+  h->st_nheavy = (int)sl.heavy.size();
   return FU_OK;
 }
 
 // The staged-estimate buffer G and the four slice layouts (element bytes 1, 2, 4, 8; slice =
-// kStageLds / bytes nodes). G is slice-major: for slice s and block part q (the light tiles
-// cut into Q contiguous parts, one stage block each), the tiles' edges whose neighbour lies
-// in slice s, tile by tile, in position order; each (s, q) region padded to 16 elements (a
-// lane stores 16 bytes) with column offset 0 (never read). A tile's edges of one slice are
-// therefore one contiguous run of G: per edge the round kernel reads u16 {position, run}
-// and per tile the run offsets D (G index = m + D[run], m = index in slice order). A layout
-// is built only if every light tile touches at most kStageRuns slices.
+// kStageLds / bytes nodes; FP::build_stage_layouts). A tile's edges of one slice are one
+// contiguous run of G: per edge the round kernel reads u16 {position, run} and per tile the
+// run offsets D (G index = m + D[run], m = index in slice order).
 int ensure_stage(fu_handle *h) {
   if (h->st_ready) return FU_OK;
   if (!h->st_why.empty()) return fail(FU_ERR_GRAPH, h->st_why);
   if (int rc = ensure_light(h)) return rc;
-  const std::vector<int4> &light = h->h_light;
-  const int T = (int)light.size();
-  auto up = [&](auto **dst, const auto *src, size_t cnt) -> int {
-    if (int rc = dmalloc(dst, std::max<size_t>(1, cnt))) return rc;
-    if (cnt) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * cnt, hipMemcpyHostToDevice));
-    return FU_OK;
-  };
-  int64_t gmax = 16;
-  std::string why = "kernel 8 (staged slices): no light tiles";
-  for (int li = 0; li < 4 && T > 0; ++li) {
-    auto &L = h->st[li];
-    const int64_t SN = std::min<int64_t>(kStageLds >> li, 65536);  // column offsets are u16
-    const int64_t P = ((int64_t)h->na + SN - 1) / SN;  // multi-GPU: the ghost slots are slices too
-    if (P > kStageMaxP) {
-      why = "kernel 8 (staged slices): more than " + std::to_string(kStageMaxP) + " slices";
-      continue;
-    }
-    const int64_t Q = std::max<int64_t>(1, std::min<int64_t>(T, (h->n_cu + P / 2) / P));
-    auto part = [&](int t) { return (int64_t)t * Q / T; };
-    // elements per (slice, part) and runs per tile
-    std::vector<int64_t> cnt(P * Q, 0);
-    std::vector<int32_t> stamp(P, -1);
-    bool ok = true;
-    for (int t = 0; t < T && ok; ++t) {
-      int runs = 0;
-      const int64_t q = part(t);
-      for (int32_t e = light[t].z; e < light[t].w; ++e) {
-        const int32_t s = h->h_col[e] / (int32_t)SN;
-        if (stamp[s] != t) {
-          stamp[s] = t;
-          ++runs;
-        }
-        cnt[s * Q + q]++;
-      }
-      ok = runs <= kStageRuns;
-    }
-    if (!ok) {
-      why = "kernel 8 (staged slices): a tile touches more than " + std::to_string(kStageRuns) + " slices";
-      continue;
-    }
-    std::vector<int64_t> off(P * Q + 1, 0);
-    for (int64_t k = 0; k < P * Q; ++k) off[k + 1] = off[k] + (cnt[k] + 15) / 16 * 16;
-    const int64_t total = off[P * Q];
-    if (total >= (int64_t)INT32_MAX - 16) {
-      why = "kernel 8 (staged slices): staged index exceeds 2^31";
-      continue;
-    }
-    std::vector<uint16_t> colS(std::max<int64_t>(total, 16), 0);
-    std::vector<uint16_t> s16(h->E > 0 ? h->E : 1, 0);
-    std::vector<int32_t> dt((size_t)T * kStageRuns, 0);
-    std::vector<int64_t> cur(off.begin(), off.end() - 1);
-    std::vector<int32_t> ord;
-    for (int t = 0; t < T; ++t) {
-      const int32_t e0 = light[t].z, ne = light[t].w - light[t].z;
-      const int64_t q = part(t);
-      ord.resize(ne);
-      for (int32_t m = 0; m < ne; ++m) ord[m] = m;
-      std::stable_sort(ord.begin(), ord.end(), [&](int32_t x, int32_t y) {
-        return h->h_col[e0 + x] / SN < h->h_col[e0 + y] / SN;
-      });
-      int run = -1;
-      int64_t sprev = -1;
-      for (int32_t m = 0; m < ne; ++m) {
-        const int32_t pos = ord[m];
-        const int32_t c = h->h_col[e0 + pos];
-        const int64_t s = c / SN;
-        const int64_t gidx = cur[s * Q + q]++;
-        colS[gidx] = (uint16_t)(c % SN);
-        if (s != sprev) {
-          ++run;
-          sprev = s;
-          dt[(size_t)t * kStageRuns + run] = (int32_t)(gidx - m);
-        }
-        s16[e0 + m] = (uint16_t)(pos | (run << 10));
-      }
-    }
-    // stage block of region (s, q) at b = 8 (Q (s / 8) + q) + s % 8: the Q blocks of slice s run
-    // on one XCD (blocks are dealt round-robin over the 8 XCDs; placement only, never
-    // correctness), so the slice's Q - 1 re-reads hit that XCD's L2
-    const int64_t NB = 8 * Q * ((P + 7) / 8);
-    std::vector<int4> br(NB, make_int4(0, 0, 0, 0));
-    for (int64_t s2 = 0; s2 < P; ++s2)
-      for (int64_t q = 0; q < Q; ++q) {
-        const int64_t k = s2 * Q + q, b = 8 * (Q * (s2 / 8) + q) + s2 % 8;
-        br[b] = make_int4((int)off[k], (int)off[k + 1], (int)s2, 0);
-      }
-    for (void *p : {(void *)L.brange, (void *)L.colS, (void *)L.sidx16, (void *)L.dtab})
-      if (p) hipFree(p);
-    L = fu_handle::StageLayout{};
-    if (int rc = up(&L.brange, br.data(), br.size())) return rc;
-    if (int rc = up(&L.colS, colS.data(), colS.size())) return rc;
-    if (int rc = up(&L.sidx16, s16.data(), s16.size())) return rc;
-    if (int rc = up(&L.dtab, dt.data(), dt.size())) return rc;
-    L.P = (int)P;
-    L.Q = (int)Q;
-    L.SN = (int)SN;
-    L.NB = (int)NB;
-    gmax = std::max<int64_t>(gmax, total);
-  }
-  bool any = false;
-  for (int li = 0; li < 4; ++li) any |= h->st[li].P > 0;
-  if (!any) {
+  FP::StageLayout L[4];
+  std::string why;
+  if (!FP::build_stage_layouts(plan_graph(h), h->h_light, h->n_cu, L, &why)) {
     h->st_why = why;
     return fail(FU_ERR_GRAPH, why);
+  }
+  int64_t gmax = 16;
+  for (int li = 0; li < 4; ++li) {
+    auto &D = h->st[li];
+    for (void *p : {(void *)D.brange, (void *)D.colS, (void *)D.sidx16, (void *)D.dtab})
+      if (p) hipFree(p);
+    D = fu_handle::StageLayout{};
+    if (!L[li].P) continue;
+    if (int rc = upload(&D.brange, L[li].brange)) return rc;
+    if (int rc = upload(&D.colS, L[li].colS)) return rc;
+    if (int rc = upload(&D.sidx16, L[li].sidx16)) return rc;
+    if (int rc = upload(&D.dtab, L[li].dtab)) return rc;
+    D.P = L[li].P;
+    D.Q = L[li].Q;
+    D.SN = L[li].SN;
+    D.NB = L[li].NB;
+    gmax = std::max<int64_t>(gmax, L[li].total);
   }
   if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)gmax)) return rc;
   HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long) * (size_t)gmax));
@@ -2907,98 +2524,38 @@ void free_transpose(fu_handle *h) {
 int ensure_transpose(fu_handle *h) {
   if (h->tr_ready) return FU_OK;
   if (!h->tr_why.empty()) return fail(FU_ERR_GRAPH, h->tr_why);
-  const int64_t n = h->n, E = h->E;
-  const int64_t SN = kStageLds / 8;
-  const int64_t P = (n + SN - 1) / SN;
-  if (E == 0 || P > kTrMaxP) {
-    h->tr_why = E == 0 ? "kernel 9 (pregather): no edges" : "kernel 9 (pregather): more than 2^25 nodes";
-    return fail(FU_ERR_GRAPH, h->tr_why);
+  FP::TransPlan tp;
+  std::string why;
+  const int32_t *mrows = h->h_hrows.empty() ? nullptr : h->h_hrows.data() + h->multi_geo[1][0];
+  if (!FP::build_transpose(plan_graph(h), h->mega_hub, h->tr_hot, h->n_cu, mrows, h->multi_geo[1][1], tp, &why)) {
+    h->tr_why = why;
+    return fail(FU_ERR_GRAPH, why);
   }
-  const int64_t B = (E + kTrBE - 1) / kTrBE;
-  // buckets [0, Bh) hold every mega-hub edge: transposed first, so the hub chains can start
-  int64_t hub_end = 0;
-  for (int32_t i = 0; i < h->n; ++i)
-    if (h->h_rowptr[i + 1] - h->h_rowptr[i] > h->mega_hub) hub_end = h->h_rowptr[i + 1];
-  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>, k_transpose_pipe<HOTN>)
-  const int32_t H = (int32_t)std::min<int64_t>(h->tr_hot, std::min<int64_t>(n, kTrHot));
-  std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < E; ++e)
-    if (h->h_col[e] >= H) cnt[h->h_col[e] / SN]++;
-  std::vector<int64_t> reg(P + 1, 0);
-  for (int64_t s2 = 0; s2 < P; ++s2) reg[s2 + 1] = reg[s2] + (cnt[s2] + 15) / 16 * 16;
-  const int64_t total = reg[P];
-  if (total >= (int64_t)INT32_MAX) {
-    h->tr_why = "kernel 9 (pregather): more than 2^31 staged elements";
-    return fail(FU_ERR_GRAPH, h->tr_why);
-  }
-  std::vector<uint16_t> colS(total, 0), pos(total, 0);
-  std::vector<int32_t> offT((size_t)(B + 1) * P);
-  std::vector<int64_t> cur(reg.begin(), reg.end() - 1);
-  std::vector<int32_t> hoff(B + 1, 0);
-  std::vector<uint32_t> hlist;
-  for (int64_t b = 0; b < B; ++b) {
-    for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)b * P + s2] = (int32_t)cur[s2];
-    hoff[b] = (int32_t)hlist.size();
-    const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
-    for (int64_t e = b * kTrBE; e < e1; ++e) {
-      const int32_t c = h->h_col[e];
-      if (c < H) {  // {column, position in the bucket}, edge order
-        hlist.push_back(((uint32_t)c << 16) | (uint32_t)(e - b * kTrBE));
-        continue;
-      }
-      const int64_t g = cur[c / SN]++;
-      colS[g] = (uint16_t)(c % SN);
-      pos[g] = (uint16_t)(e - b * kTrBE);
-    }
-  }
-  hoff[B] = (int32_t)hlist.size();
-  for (int64_t s2 = 0; s2 < P; ++s2) offT[(size_t)B * P + s2] = (int32_t)cur[s2];
-  // stage pieces by element count, not per slice: under the degree layout the hottest slice
-  // holds ~40% of all elements (R-MAT-24), so a slice gets as many blocks as its share
-  // (each re-reads the 128 KB slice, mostly from L2)
-  const int64_t piece = std::max<int64_t>(16384, (total / (4 * (int64_t)h->n_cu) + 15) / 16 * 16);
-  std::vector<int4> br;
-  for (int64_t s2 = 0; s2 < P; ++s2)
-    for (int64_t p0 = reg[s2]; p0 < reg[s2 + 1] || p0 == reg[s2]; p0 += piece)
-      br.push_back(make_int4((int)p0, (int)std::min(reg[s2 + 1], p0 + piece), (int)s2, 0));
-  const int64_t Q = (int64_t)br.size() / P;
   auto &T = h->tr;
-  auto up = [&](auto **dst, const auto *src, size_t count) -> int {
-    if (int rc = dmalloc(dst, std::max<size_t>(1, count))) return rc;
-    if (count) HIP_TRY(hipMemcpy(*dst, src, sizeof(**dst) * count, hipMemcpyHostToDevice));
-    return FU_OK;
-  };
-  if (int rc = up(&T.brange, br.data(), br.size())) return rc;
-  if (int rc = up(&T.colS, colS.data(), colS.size())) return rc;
-  if (int rc = up(&T.pos16, pos.data(), pos.size())) return rc;
-  if (int rc = up(&T.offT, offT.data(), offT.size())) return rc;
-  if (int rc = up(&T.hoff, hoff.data(), hoff.size())) return rc;
-  if (int rc = up(&T.hlist, hlist.data(), hlist.size())) return rc;
-  T.H = H;
-  if (int rc = dmalloc(&T.GA, (size_t)total)) return rc;
+  if (int rc = upload(&T.brange, tp.brange)) return rc;
+  if (int rc = upload(&T.colS, tp.colS)) return rc;
+  if (int rc = upload(&T.pos16, tp.pos)) return rc;
+  if (int rc = upload(&T.offT, tp.offT)) return rc;
+  if (int rc = upload(&T.hoff, tp.hoff)) return rc;
+  if (int rc = upload(&T.hlist, tp.hlist)) return rc;
+  if (int rc = dmalloc(&T.GA, (size_t)tp.total)) return rc;
   // G_B: a ring of three with lag (round r reads G_B of round r - 2 for the lagged rows)
   for (int k = 0; k < 3; ++k) {
     if (k && !h->lag) {
       T.GBr[k] = T.GBr[0];
       continue;
     }
-    if (int rc = dmalloc(&T.GBr[k], (size_t)E)) return rc;
+    if (int rc = dmalloc(&T.GBr[k], (size_t)h->E)) return rc;
   }
   for (int p = 0; p < 2; ++p)
     if (int rc = dmalloc(&T.hist[p], (size_t)(h->multi_geo[1][1] + 1))) return rc;
-  T.P = (int)P;
-  T.Q = (int)Q;
-  T.NB = (int)br.size();
-  T.B = (int)B;
-  T.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
-  {  // the multi-row heavy rows of geometry 1 (contiguous after the hubs under the degree layout)
-    int64_t mend = hub_end;
-    for (int q = 0; q < h->multi_geo[1][1]; ++q) {
-      const int32_t i = h->h_hrows[h->multi_geo[1][0] + q];
-      mend = std::max<int64_t>(mend, h->h_rowptr[i + 1]);
-    }
-    T.Bm = (int)std::max<int64_t>(T.Bh, (mend + kTrBE - 1) / kTrBE);
-  }
+  T.H = tp.H;
+  T.P = tp.P;
+  T.Q = tp.Q;
+  T.NB = tp.NB;
+  T.B = tp.B;
+  T.Bh = tp.Bh;
+  T.Bm = tp.Bm;
   h->tr_ready = true;
   return FU_OK;
 }
@@ -3125,12 +2682,16 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   if (!Gb) return fail(FU_ERR_STATE, "kernel 9: no pre-gather buffer");
   const int r1 = (int)(c.r & 1);
   const void *cp = h->code[(c.r - 1) & 1];
-  const int nmega = h->n_hub, nh = h->nheavy_geo[1];
-  const int niso = h->iso_rows ? h->niso_geo[1] : 0;  // trailing isolated-row tiles: k_isolated
-  const int nl = h->ntiles_geo[1] - nh - niso;
-  // heavy tiles [m0, m1): the register-resident launch (mid_heavy), the others as before
-  const int m0 = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-  const int m1 = h->mid_heavy ? std::max(m0, h->mid_geo[1][1]) : nh;
+  // which launch computes which rows (FP::k9_schedule; tools/plan_check.cpp replays it)
+  FP::K9Opts ko;
+  ko.mid_heavy = h->mid_heavy;
+  ko.multi_mid = h->multi_mid;
+  ko.multi_short = h->multi_short;
+  ko.multi_heavy = h->multi_heavy;
+  ko.wave_heavy = h->wave_heavy;
+  ko.iso_rows = h->iso_rows;
+  const FP::K9Sched ks = FP::k9_schedule(h->tiles1, h->n_hub, ko);
+  const int nmega = ks.nmega, nh = ks.nh, niso = ks.niso, nl = ks.nl, m0 = ks.m0, m1 = ks.m1;
   const int4 *tl = h->tiles_geo[1];
   const bool hubs = nmega > 0;
   StageArgs sa{};
@@ -3151,32 +2712,16 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int bh = hubs ? h->tr.Bh : 0;
   // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
   // multi-row heavy rows
-  const int m0_ = h->mid_heavy ? std::max(nmega, h->mid_geo[1][0]) : nh;
-  // multi_short: the rows of 129-256 edges (heavy tiles [m1, nh)) join the multi-row blocks
-  const int mend = h->multi_mid ? (h->multi_short ? nh : m1) : m0_;
-  const int n_multi = std::min(h->multi_geo[1][1], 4 * (mend - nmega));
-  const bool multi = h->multi_heavy && h->mid_heavy && h->wave_heavy && n_multi > 0;
-  const int m1s = multi && h->multi_mid && h->multi_short ? nh : m1;  // one-row-per-wave tiles [m1s, nh)
+  const int n_multi = ks.n_multi, m1s = ks.m1s;
+  const bool multi = ks.multi;
   const bool lag_multi = h->lag && multi;
   const int p = r1;
   if (h->lagf[p] && h->lag_nmulti[p] != (lag_multi ? n_multi : 0)) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
   }
   const int lagm = lag_multi ? (h->lagf[p] ? 2 : 1) : 0;
-  const bool pipe = h->tr_pipe && h->tr_bpx > 0;
   auto tr_launch = [&](int b0, int nb) {
-    if (pipe && h->tr.H > kTrHotS)
-      hipLaunchKernelGGL(k_transpose_pipe<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
-                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
-                         h->tr.hlist);
-    else if (pipe && h->tr.H)
-      hipLaunchKernelGGL(k_transpose_pipe<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb,
-                         h->tr.P, (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff,
-                         h->tr.hlist);
-    else if (pipe)
-      hipLaunchKernelGGL(k_transpose_pipe<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
-    else if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
+    if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
       hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
@@ -3194,54 +2739,18 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
     HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
-  // split_tr: the buckets of the multi-row heavy rows first, then k_heavy_multi on stream3
-  // beside the remaining (latency-bound) transposes
-  const int bm = std::min(std::max(h->tr.Bm, bh), h->tr.B);
-  const bool split = h->split_tr && bm > bh && bm < h->tr.B;
-  if (split) {
-    tr_launch(bh, bm - bh);
-    HIP_TRY(hipEventRecord(h->ev_htr, h->stream));
-    HIP_TRY(hipStreamWaitEvent(h->stream3, h->ev_htr, 0));
-    tr_launch(bm, h->tr.B - bm);
-  } else if (h->tr.B > bh) {
-    tr_launch(bh, h->tr.B - bh);
-  }
+  if (h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
   const bool chk = c.err != nullptr;
-  // side_tiles: the light tiles (1) and the rows of 129-256 edges (2) run on the side stream
-  // behind the hub path, once every bucket is transposed, beside the heavy rows
-  const int side = hubs ? h->side_tiles : 0;
-  if (side) HIP_TRY(hipEventRecord(h->ev_tr, h->stream));
   if (hubs) {
     auto chains = [&](auto C) {
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
                          0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
-                         h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm, nullptr, nullptr, nullptr,
-                         h->hub_prio);
+                         h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm);
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
     hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
                        (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
-    if (side) {
-      HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_tr, 0));
-      auto st = [&](auto C) {
-        if (side >= 2 && nh > m1s)  // the rows of 129-256 edges (4 per block, in registers)
-          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, kHeavyRL>), dim3(nh - m1s),
-                             dim3(kBlock), 0, h->stream2, tl + m1s, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
-                             h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
-                             c.fm);
-        if (niso)
-          hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream2,
-                             h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
-                             decltype(C)::value ? 1 : 0);
-        if (nl)
-          hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
-                             h->stream2, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err,
-                             cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
-      };
-      if (chk) st(std::true_type{});
-      else st(std::false_type{});
-    }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
   }
@@ -3262,7 +2771,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (multi) {
       auto hm = [&](auto L) {
         hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
-                           dim3(kBlock), 0, split ? h->stream3 : h->stream, h->hrows + h->multi_geo[1][0], n_multi,
+                           dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0], n_multi,
                            h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
                            h->tr.hist[p]);
       };
@@ -3274,12 +2783,12 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
       heavy(C, std::integral_constant<int, kHeavyRL>{}, nmega, m0);
       heavy(C, std::integral_constant<int, kMidRL>{}, m0, m1);
     }
-    if (side < 2) heavy(C, std::integral_constant<int, kHeavyRL>{}, m1s, nh);
-    if (niso && !side)
+    heavy(C, std::integral_constant<int, kHeavyRL>{}, m1s, nh);
+    if (niso)
       hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream,
                          h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
                          decltype(C)::value ? 1 : 0);
-    if (nl && !side)
+    if (nl)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
@@ -3287,10 +2796,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   if (chk) tiles(std::true_type{});
   else tiles(std::false_type{});
   HIP_TRY(hipGetLastError());
-  if (split && multi) {
-    HIP_TRY(hipEventRecord(h->ev_s3, h->stream3));
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_s3, 0));
-  }
   if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
     h->lagf[p] = 1;
@@ -3503,8 +3008,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
     int lo = 0, hi = 0;
     if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
     if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, hi) != hipSuccess ||
-        hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess)
+        hipStreamCreateWithPriority(&h->stream2, hipStreamNonBlocking, hi) != hipSuccess)
       return cleanup(fail(FU_ERR_HIP, "hipStreamCreate failed"));
   }
   {
@@ -3515,10 +3019,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_tr, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_htr, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_s3, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
@@ -3542,39 +3043,12 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipMemset(h->a[0], 0, sizeof(double) * na) != hipSuccess || hipMemset(h->a[1], 0, sizeof(double) * na) != hipSuccess ||
       hipMemset(h->a[2], 0, sizeof(double) * na) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: memset failed"));
-  {  // round 0's per-block rows
-    const int64_t nblk = (e + kR0E - 1) / kR0E;
-    std::vector<int32_t> br(nblk + 1, 0);
-    int32_t i = 0;
-    for (int64_t b = 0; b <= nblk; ++b) {
-      const int64_t k = b < nblk ? b * kR0E : e - 1;
-      while (i + 1 < n && rowptr[i + 1] <= k) ++i;  // last row with rowptr[i] <= k
-      br[b] = i;
-    }
-    if ((rc = dmalloc(&h->blk_row, br.size()))) return cleanup(rc);
-    if (hipMemcpy(h->blk_row, br.data(), sizeof(int32_t) * br.size(), hipMemcpyHostToDevice) != hipSuccess)
-      return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
-    // kernel 4's 2-byte column offsets: block b (edges [1024 b, 1024 b + 1024)) is narrow
-    // when every column lies within 32K ids of the block's first row (graphs with locality:
-    // RGG in cell order); a wide block keeps cbase -1 and its tiles read the 4-byte columns
-    std::vector<uint16_t> c16(std::max<int64_t>(e, 1), 0);
-    h->h_cbase.assign(std::max<int64_t>(nblk, 1), -1);
-    for (int64_t b = 0; b < nblk; ++b) {
-      const int32_t base = br[b];
-      bool ok = true;
-      const int64_t k1 = std::min<int64_t>(e, (b + 1) * kR0E);
-      for (int64_t k = b * kR0E; k < k1 && ok; ++k) {
-        const int64_t d = (int64_t)col[k] - base + 32768;
-        ok = d >= 0 && d <= 65535;
-      }
-      if (!ok) continue;
-      h->h_cbase[b] = base;
-      for (int64_t k = b * kR0E; k < k1; ++k) c16[k] = (uint16_t)((int64_t)col[k] - base + 32768);
-    }
-    if ((rc = dmalloc(&h->col16, c16.size())) || (rc = dmalloc(&h->cbase, h->h_cbase.size()))) return cleanup(rc);
-    if (hipMemcpy(h->col16, c16.data(), sizeof(uint16_t) * c16.size(), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(h->cbase, h->h_cbase.data(), sizeof(int32_t) * h->h_cbase.size(), hipMemcpyHostToDevice) != hipSuccess)
-      return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
+  {  // round 0's per-block rows; kernel 4's 2-byte column offsets (FP::build_blocks)
+    std::vector<int32_t> br;
+    std::vector<uint16_t> c16;
+    FP::build_blocks(n, e, rowptr, col, br, h->h_cbase, c16);
+    if ((rc = upload(&h->blk_row, br)) || (rc = upload(&h->col16, c16)) || (rc = upload(&h->cbase, h->h_cbase)))
+      return cleanup(rc);
   }
   if ((rc = build_tiles(h))) return cleanup(rc);
   if ((rc = dmalloc(&h->pctl, 3)) || (rc = dmalloc(&h->code[0], 4 * (size_t)na)) ||
@@ -3716,10 +3190,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->staged_lo = value != 0;
     return FU_OK;
   }
-  if (!std::strcmp(key, "tr_pipe")) {  // kernel 9: software-pipelined transpose (1)
-    h->tr_pipe = value != 0;
-    return FU_OK;
-  }
   if (!std::strcmp(key, "tr_hot")) {  // kernel 9: neighbours of id < value served from LDS (0: none)
     if (value < 0 || value > kTrHot) return fail(FU_ERR_ARG, "fu_set_option: tr_hot must be in [0, 10240]");
     if (value != h->tr_hot) {
@@ -3754,19 +3224,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "iso_rows")) {  // kernel 9: trailing isolated rows one thread each (1) or as tiles (0)
     h->iso_rows = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "split_tr")) {  // kernel 9: heavy rows start once their buckets are transposed (1)
-    h->split_tr = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "side_tiles")) {  // kernel 9: light tiles (1), and rows of 129-256 edges (2), on the side stream
-    if (value < 0 || value > 2) return fail(FU_ERR_ARG, "fu_set_option: side_tiles must be 0, 1 or 2");
-    h->side_tiles = (int)value;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_prio")) {  // kernel 9: hub chain waves issue first on their SIMD (1)
-    h->hub_prio = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "multi_heavy")) {  // kernel 9: rows > 256 edges with many rows per chain wave (1)
@@ -4232,7 +3689,6 @@ int fu_destroy(fu_handle *h) {
   hipSetDevice(h->device);
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
-  if (h->stream3) hipStreamSynchronize(h->stream3);
   if (h->dist) fu__dist_free(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
@@ -4248,14 +3704,13 @@ int fu_destroy(fu_handle *h) {
   }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_tr, h->ev_htr, h->ev_s3})
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);
   if (h->h_pw) hipHostFree(h->h_pw);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
-  if (h->stream3) hipStreamDestroy(h->stream3);
   delete h;
   return FU_OK;
 }

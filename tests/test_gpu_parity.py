@@ -141,10 +141,11 @@ def test_option_errors():
     for k in (1, 2, 3, 5, 6, 7, 10, 11):  # removed variants / out of range
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
-    for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse"):
+    for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse",
+                "tr_pipe", "hub_prio", "side_tiles", "split_tr"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
-    for key, val in (("side_tiles", 3), ("side_tiles", -1), ("tr_nt", 2)):
+    for key, val in (("tr_nt", 2), ("tr_nt", -1)):
         with pytest.raises(fu.FuError):
             eng.set_option(key, val)
     with pytest.raises(fu.FuError):
@@ -534,14 +535,14 @@ def test_packed_gather_long_run_bitwise(kind, kernel):
 
 
 @pytest.mark.parametrize("opts", [{"staged_lo": 0}, {"staged_lo": 0, "pack": 0}, {"tr_bpx": 0},
-                                  {"tr_pipe": 1}, {"tr_pipe": 1, "tr_bpx": 3}])
+                                  {"tr_bpx": 3}, {"tr_bpx": 3, "tr_nt": 0}])
 def test_load_order_and_transpose_options_bitwise(opts):
     """The A/B options of this round (kernel 8's interleaved load order; kernel 9's
     one-block-per-bucket transpose) give the C oracle's bits over a 300-round run with packing
     and escapes."""
     g, v = _er_with_outlier_pairs(100_000, 400_000, 64, seed=5)
     rounds = 300
-    eng = fu.CollectAll(g, v, kernel="pregather" if {"tr_bpx", "tr_pipe"} & set(opts) else "stage",
+    eng = fu.CollectAll(g, v, kernel="pregather" if "tr_bpx" in opts else "stage",
                         hub_threshold=16)
     eng.set_option("pack_every", 4)
     for k, val in opts.items():
@@ -629,8 +630,8 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0", "pipe", "nolag", "hot", "hot_nolag", "hot_pipe", "hot4k", "prio",
-                                   "side1", "side2_hot_pipe", "split", "split_side1_hot", "iso0", "short0", "short_side2_nolag", "trnt0", "trnt_pipe"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "nolag", "hot", "hot_nolag", "hot4k", "iso0", "short0",
+                                   "short_nolag", "trnt0"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -645,8 +646,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     eng.set_option("mega_hub", mega)
     if multi == "mid0":
         eng.set_option("multi_mid", 0)
-    elif multi == "pipe":
-        eng.set_option("tr_pipe", 1)
     elif multi == "nolag":  # the two-pass heavy rows (lag is the default)
         eng.set_option("lag", 0)
     elif multi == "hot":  # neighbours of id < 10240 served from the transpose's LDS
@@ -654,34 +653,16 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     elif multi == "hot_nolag":
         eng.set_option("tr_hot", 3000)
         eng.set_option("lag", 0)
-    elif multi == "hot_pipe":  # the pipelined transpose with the hot table
-        eng.set_option("tr_hot", 10240)
-        eng.set_option("tr_pipe", 1)
     elif multi == "hot4k":  # the small (32 KB) hot table
         eng.set_option("tr_hot", 4096)
-    elif multi == "prio":  # the hub chain waves at issue priority 3
-        eng.set_option("hub_prio", 1)
-    elif multi == "side1":  # light tiles on the side stream behind the hub path
-        eng.set_option("side_tiles", 1)
-    elif multi == "side2_hot_pipe":  # ... and the rows of 129-256 edges
-        for key, val in (("side_tiles", 2), ("tr_hot", 5000), ("tr_pipe", 1), ("hub_prio", 1)):
-            eng.set_option(key, val)
-    elif multi == "split":  # the heavy rows on a third stream once their buckets are transposed
-        eng.set_option("split_tr", 1)
-    elif multi == "split_side1_hot":
-        for key, val in (("split_tr", 1), ("side_tiles", 1), ("tr_hot", 3000), ("hub_prio", 1)):
-            eng.set_option(key, val)
     elif multi == "iso0":  # the trailing isolated rows as light tiles (k_isolated is the default)
         eng.set_option("iso_rows", 0)
     elif multi == "trnt0":  # plain G_A loads / G_B stores in the transposes (tr_nt is the default)
         eng.set_option("tr_nt", 0)
-    elif multi == "trnt_pipe":  # (the pipelined transpose keeps its plain loads and stores)
-        eng.set_option("tr_nt", 1)
-        eng.set_option("tr_pipe", 1)
     elif multi == "short0":  # the rows of 129-256 edges one per wave (multi_short is the default)
         eng.set_option("multi_short", 0)
-    elif multi == "short_side2_nolag":
-        for key, val in (("multi_short", 1), ("side_tiles", 2), ("lag", 0)):
+    elif multi == "short_nolag":
+        for key, val in (("multi_short", 1), ("lag", 0)):
             eng.set_option(key, val)
     else:
         eng.set_option("multi_heavy", multi)
@@ -1050,11 +1031,56 @@ def _class_edge_graph(seed):
     return g
 
 
+def _isolated_then_heavy_graph(tail):
+    """Layout "given" with runs of isolated rows right before a heavy row and a mega hub:
+    tail = "heavy_hub" puts [..., isolated x 700, heavy (300 edges), mega hub (9000 edges)] at
+    the end, "hub_iso_heavy" [..., mega hub, isolated x 700, heavy], "iso_end" keeps the
+    isolated run last (the k_isolated case)."""
+    rng = np.random.default_rng(21)
+    n_leaf, n_iso = 12000, 700
+    base = rng.integers(0, n_leaf, size=(3 * n_leaf, 2))
+    src, dst = [base[:, 0]], [base[:, 1]]
+    if tail == "heavy_hub":
+        iso0, heavy, hub = n_leaf, n_leaf + n_iso, n_leaf + n_iso + 1
+    elif tail == "hub_iso_heavy":
+        hub, iso0, heavy = n_leaf, n_leaf + 1, n_leaf + 1 + n_iso
+    else:
+        heavy, hub, iso0 = n_leaf, n_leaf + 1, n_leaf + 2
+    n = n_leaf + n_iso + 2
+    src += [np.full(300, heavy), np.full(9000, hub)]
+    dst += [rng.choice(n_leaf, 300, replace=False), rng.choice(n_leaf, 9000, replace=False)]
+    g = fu.Graph.from_edges(n, np.concatenate(src), np.concatenate(dst))
+    deg = g.degrees
+    assert deg[heavy] == 300 and deg[hub] == 9000 and not deg[iso0:iso0 + n_iso].any()
+    return g
+
+
+@pytest.mark.parametrize("tail", ["heavy_hub", "hub_iso_heavy", "iso_end"])
+@pytest.mark.parametrize("opts", [{}, {"lag": 0}, {"iso_rows": 0}, {"tr_hot": 64}])
+def test_isolated_rows_before_heavy_rows_given_layout_bitwise(tail, opts):
+    """Kernel 9's k_isolated must not cover a heavy row or a mega hub that follows the
+    trailing run of edge-less light tiles (layout "given", CollectAll's default): every row
+    computed by exactly one launch, bitwise against the C oracle (CA:106-113)."""
+    g = _isolated_then_heavy_graph(tail)
+    v = fu.uniform_values(g.n, seed=8)
+    eng = fu.CollectAll(g, v, kernel="pregather", layout="given")
+    for key, val in opts.items():
+        eng.set_option(key, val)
+    done = 0
+    for k in (1, 2, 4, 9):
+        eng.run(k)
+        done += k
+        a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, done, nthreads=16)
+        assert np.array_equal(eng.estimates(), a_ref), done
+        assert np.array_equal(eng.flows(), f_ref), done
+    eng.close()
+
+
 @pytest.mark.parametrize("layout", ["given", "degree"])
 @pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
                                          ("pregather", {}), ("pregather", {"lag": 0}),
                                          ("pregather", {"multi_mid": 0, "tr_hot": 64}),
-                                         ("pregather", {"iso_rows": 0}), ("pregather", {"side_tiles": 2}),
+                                         ("pregather", {"iso_rows": 0}), ("pregather", {"tr_hot": 4096, "lag": 0}),
                                          ("pregather", {"multi_short": 0}),
                                          ("pregather", {"multi_short": 1, "multi_heavy": 0})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):

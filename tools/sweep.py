@@ -30,36 +30,17 @@ VARIANTS = {
     "pre_mid0": ("pregather", {"layout": "degree", "pack": 0, "mid_heavy": 0}),
     "pre_multi0": ("pregather", {"layout": "degree", "pack": 0, "multi_heavy": 0}),
     "pre_multimid0": ("pregather", {"layout": "degree", "pack": 0, "multi_mid": 0}),
-    "pre_trpipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
     "pre_lag": ("pregather", {"layout": "degree", "pack": 0, "lag": 1}),
     "pre_hot": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240}),
     "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1}),
     "pre_hot4k_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096, "lag": 1}),
     "pre_hot4k": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096}),
-    "pre_prio": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1}),
-    "pre_prio_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1}),
-    "pre_prio_side2": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 2}),
-    "pre_prio_side1_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1, "lag": 1}),
-    "pre_prio_side1_hot_pipe": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "side_tiles": 1,
-                                              "tr_hot": 10240, "tr_pipe": 1}),
-    "pre_pipe": ("pregather", {"layout": "degree", "pack": 0, "tr_pipe": 1}),
-    "pre_prio_split": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1}),
-    "pre_prio_split_side1": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1, "side_tiles": 1}),
-    "pre_prio_split_side1_hot": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "split_tr": 1,
-                                               "side_tiles": 1, "tr_hot": 10240}),
-    "pre_prio_lag": ("pregather", {"layout": "degree", "pack": 0, "hub_prio": 1, "lag": 1}),
     "pre_iso0": ("pregather", {"layout": "degree", "pack": 0, "iso_rows": 0}),
     "pre_short": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1}),
     "pre_trnt": ("pregather", {"layout": "degree", "pack": 0, "tr_nt": 1}),
     "pre_trnt0": ("pregather", {"layout": "degree", "pack": 0, "tr_nt": 0}),
-    "pre_short_side1": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "side_tiles": 1}),
     "pre_short_ht64": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "hub_threshold": 64}),
     "pre_short_ht96": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "hub_threshold": 96}),
-    "pre_short_split": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1, "split_tr": 1}),
-    "pre_side1": ("pregather", {"layout": "degree", "pack": 0, "side_tiles": 1}),
-    "pre_side2": ("pregather", {"layout": "degree", "pack": 0, "side_tiles": 2}),
-    "pre_split": ("pregather", {"layout": "degree", "pack": 0, "split_tr": 1}),
-    "pre_split_side1": ("pregather", {"layout": "degree", "pack": 0, "split_tr": 1, "side_tiles": 1}),
     "pre_mega4k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 4096}),
     "pre_mega16k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 16384}),
     "pre_mega32k": ("pregather", {"layout": "degree", "pack": 0, "mega_hub": 32768}),
