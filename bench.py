@@ -207,62 +207,96 @@ def pmc_traffic(n, E, kernel_selected, steps, per_gpu=False):
     return None
 
 
+def make_graph(wl, n_arg, m_arg):
+    """The single-GPU workloads' graphs (seeded): (graph, description)."""
+    import fu
+
+    if wl == "er":
+        n = n_arg or 1_000_000
+        return fu.Graph.erdos_renyi(n, m_arg, seed=1), f"er:n={n},m={m_arg} collect-all generation-synchronous rounds"
+    if wl == "rgg":
+        n = n_arg or (1 << 20)
+        return fu.Graph.random_geometric(n, avg_deg=8.0, seed=1), f"rgg:n={n},deg=8 collect-all generation-synchronous rounds"
+    if wl == "rmat":
+        scale = n_arg or 24
+        return fu.Graph.rmat(scale, 16, seed=1), f"rmat:scale={scale},ef=16 collect-all generation-synchronous rounds"
+    n = n_arg or 65536
+    return fu.Graph.random_regular(n, 8, seed=1), f"rr:n={n},d=8 collect-all generation-synchronous rounds"
+
+
+def prepare(eng, kernel, warmup, widths=None):
+    """Untimed setup: one autotune pass (kernel auto), `warmup` rounds in chunks of 64 (the
+    host sees each packing plan's width between calls, so the autotuner also covers every
+    width the warmup reaches; winners are kept across fu_reset), fu_reset. widths: a list
+    that receives (rounds done, packing plan width) after each chunk."""
+    if kernel == "auto":
+        eng.tune()
+    done = 0
+    for w0 in range(0, warmup, 64):
+        eng.run(min(64, warmup - w0))
+        done += min(64, warmup - w0)
+        eng.synchronize()
+        if widths is not None:
+            widths.append((done, eng.pack_widths()[2]))
+    eng.reset()
+
+
+def measure_window(eng, g, steps):
+    """The timed region (rounds 0..steps-1 from the zero state) of an engine already tuned and
+    reset: wall time, per-chunk device times, the roofline of rounds 1..steps-1, the kernel
+    that ran them."""
+    wall, dev_ms, b = timed_rounds(eng, steps)
+    kinfo = eng.info()
+    kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
+    phases = [{"rounds": [b[k], b[k + 1]], "us_per_round": dev_ms[k] * 1e3 / max(1, b[k + 1] - b[k])}
+              for k in range(len(b) - 1)]
+    alg_bytes = 24 * g.E + 28 * g.n
+    roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, steps), round_kernels(kinfo))
+    ws = window_stats(g.n, g.E, kname, steps)
+    if ws:
+        roof["window_stats"] = ws
+    value_r1 = g.E * (steps - 1) / (sum(dev_ms[1:]) * 1e-3) if steps > 1 else None
+    return wall, phases, roof, value_r1, kinfo, kname
+
+
 def run_single(args, wl):
     import fu
 
     t_gen = time.perf_counter()
-    if wl == "er":
-        n = args.n or 1_000_000
-        g = fu.Graph.erdos_renyi(n, args.m, seed=1)
-        desc = f"er:n={n},m={args.m} collect-all generation-synchronous rounds"
-    elif wl == "rgg":
-        n = args.n or (1 << 20)
-        g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
-        desc = f"rgg:n={n},deg=8 collect-all generation-synchronous rounds"
-    elif wl == "rmat":
-        scale = args.n or 24
-        g = fu.Graph.rmat(scale, 16, seed=1)
-        desc = f"rmat:scale={scale},ef=16 collect-all generation-synchronous rounds"
-    else:
-        n = args.n or 65536
-        g = fu.Graph.random_regular(n, 8, seed=1)
-        desc = f"rr:n={n},d=8 collect-all generation-synchronous rounds"
+    g, desc = make_graph(wl, args.n, args.m)
     v = fu.uniform_values(g.n, seed=0)
     t_gen = time.perf_counter() - t_gen
     print(f"[bench] graph {desc}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
     layout = args.layout if args.layout != "auto" else ("degree" if wl == "rmat" else "given")
-    eng = fu.CollectAll(g, v, device=0, kernel=args.kernel, layout=layout)
+    device = 0
+    eng = fu.CollectAll(g, v, device=device, kernel=args.kernel, layout=layout)
     t_setup = time.perf_counter()
-    if args.kernel == "auto":
-        eng.tune()  # untimed: one pass over the candidates at the unpacked width
-    # warmup in chunks: the host sees each packing plan's width between calls, so the
-    # autotuner also covers every width the warmup reaches (winners kept across fu_reset)
-    for w0 in range(0, args.warmup, 64):
-        eng.run(min(64, args.warmup - w0))
-        eng.synchronize()
-    eng.reset()
+    prepare(eng, args.kernel, args.warmup)
     t_setup = time.perf_counter() - t_setup
 
-    wall, dev_ms, b = timed_rounds(eng, args.steps)
-    kinfo = eng.info()
-    phases = [{"rounds": [b[k], b[k + 1]], "us_per_round": dev_ms[k] * 1e3 / max(1, b[k + 1] - b[k])}
-              for k in range(len(b) - 1)]
+    wall, phases, roof, value_r1, kinfo, kname = measure_window(eng, g, args.steps)
     pack_after = eng.pack_widths()[2]
     value = g.E * args.steps / wall
-    # rounds 1..K-1 alone (round 0 writes no flows, §4.8): E (K-1) / their device time
-    value_r1 = g.E * (args.steps - 1) / (sum(dev_ms[1:]) * 1e-3) if args.steps > 1 else None
-    alg_bytes = 24 * g.E + 28 * g.n
-    kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
-    roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, args.steps), round_kernels(kinfo))
-    # the box's own streaming rate, measured in this run (untimed, after the timed region):
-    # a float4 copy of 1 GB, so a slow box shows as a slow copy as well as a slow round
-    roof["copy_GBs"] = fu.copy_bandwidth(0, 1 << 30, 5)
-    roof["frac_of_copy"] = roof["achieved"] / roof["copy_GBs"]
+    companions = args.workload == "auto" and not args.no_unit
+    extra = {}
+    if companions and args.steps != 1000:  # BASELINE config 2 as written, on the same engine
+        extra["config2_1000"] = guarded("config2_1000", config2_1000, eng, g, args.kernel)
 
     conv = {"rounds_to_1e-9": None, "err_after_conv_rounds": None, "conv_rounds": None,
             "components": None}
     if not args.no_conv:  # rounds to 1e-9 vs the per-component means (untimed)
         conv = convergence(eng, g.rowptr, g.col, v, args.conv_rounds)
+    eng.close()
+    # the box's own streaming rate, measured in this run (untimed, after the timed region and
+    # with the engine freed): a float4 copy of 1 GB, so a slow box shows as a slow copy as well
+    # as a slow round
+    try:
+        roof["copy_GBs"] = fu.copy_bandwidth(device, 1 << 30, 5)
+        roof["frac_of_copy"] = roof["achieved"] / roof["copy_GBs"]
+    except Exception as ex:  # noqa: BLE001  (the headline line must survive)
+        print(f"[bench] copy_bandwidth failed: {ex!r}", file=sys.stderr, flush=True)
+        roof["copy_GBs"] = None
+        roof["copy_error"] = repr(ex)
     cpu = cpu_baseline(g, v, args.cpu_seconds) if args.cpu_seconds > 0 else None
     out = {
         "metric": METRIC, "value": value, "unit": "edge-updates/s", "n_gpus": 1,
@@ -283,14 +317,85 @@ def run_single(args, wl):
         "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen,
     }
     out.update(conv)
-    eng.close()
-    if args.workload == "auto" and not args.no_unit:
-        try:  # a failure of the companion measurement must not lose the headline line
-            out["weak_scaling_unit"] = weak_unit(args)
-        except Exception as ex:  # noqa: BLE001
-            print(f"[bench] weak_scaling_unit failed: {ex!r}", file=sys.stderr, flush=True)
-            out["weak_scaling_unit"] = {"error": repr(ex)}
+    del g
+    if companions:
+        # BASELINE configs 5, 4 and 3 measured live beside the headline (each guarded: a
+        # failure of a companion measurement must not lose the headline line)
+        out["weak_scaling_unit"] = guarded("weak_scaling_unit", weak_unit, args)
+        out["rmat24_unit"] = guarded("rmat24_unit", rmat24_unit, args)
+        out["pairwise_unit"] = guarded("pairwise_unit", pairwise_unit, args)
+    out.update(extra)
     print(json.dumps(out), flush=True)
+
+
+def guarded(name, fn, *a):
+    t = time.perf_counter()
+    try:
+        r = fn(*a)
+    except Exception as ex:  # noqa: BLE001
+        print(f"[bench] {name} failed: {ex!r}", file=sys.stderr, flush=True)
+        return {"error": repr(ex)}
+    r["wall_s"] = time.perf_counter() - t
+    print(f"[bench] {name}: {r.get('wall_s'):.1f} s", file=sys.stderr, flush=True)
+    return r
+
+
+def config2_1000(eng, g, kernel):
+    """BASELINE config 2 as written (ER-1M, 1000 rounds) on the headline's engine: an untimed
+    400-round pass in chunks (the autotuner sees the 32-, 16- and 8-bit packing widths; the
+    width schedule is recorded), fu_reset, then rounds 0-999 timed from the zero state
+    without any error check, HIP events around round 0 and ten chunks."""
+    widths = []
+    eng.reset()  # the width schedule is counted from the zero state, as in the timed run
+    prepare(eng, kernel, 400, widths)
+    wall, phases, roof, value_r1, info, kname = measure_window(eng, g, 1000)
+    sched, last = [], None
+    for r, w in widths:  # rounds at which the plan's width changed (deterministic: the same
+        if w != last:    # rounds and values give the same plans in the timed run)
+            sched.append({"from_round_le": r, "width": w})
+            last = w
+    return {"workload": "er:n=%d,m=%d, rounds 0-999 from the zero state (BASELINE config 2)" % (g.n, g.E // 2),
+            "value": g.E * 1000 / wall, "unit": "edge-updates/s", "ms_total": wall * 1e3,
+            "value_rounds_1_on": value_r1, "avg_round_us": roof["avg_launch_us"], "frac": roof["frac"],
+            "roofline": roof, "phases": phases, "pack_width_schedule": sched,
+            "autotune_winner_by_width": info["tune_winner_by_width"],
+            "note": "measured in this run; the 20-round headline window is rounds 0-19 of this job"}
+
+
+def rmat24_unit(args):
+    """BASELINE config 4 (R-MAT scale 24, ef 16, degree layout) beside the headline: kernel
+    auto tuned outside the window (kernel 9 wins), 20 rounds timed from the zero state."""
+    import fu
+
+    steps = 20
+    t = time.perf_counter()
+    g, desc = make_graph("rmat", 24, 0)
+    v = fu.uniform_values(g.n, seed=0)
+    t_gen = time.perf_counter() - t
+    eng = fu.CollectAll(g, v, device=0, kernel="auto", layout="degree")
+    try:
+        prepare(eng, "auto", 2)
+        wall, phases, roof, value_r1, kinfo, kname = measure_window(eng, g, steps)
+    finally:
+        eng.close()
+    return {"workload": desc + ", degree layout (BASELINE config 4)", "n": g.n, "E_directed": g.E,
+            "max_deg": g.max_deg, "value": g.E * steps / wall, "unit": "edge-updates/s",
+            "value_rounds_1_on": value_r1, "steps": steps, "ms_per_step": wall * 1e3 / steps,
+            "kernel_selected": kname, "autotune_us_per_round": kinfo["tune_us_per_round"],
+            "avg_round_us": roof["avg_launch_us"], "frac": roof["frac"], "traffic": roof["traffic"],
+            "roofline": roof, "phases": phases, "graph_gen_s": t_gen}
+
+
+def pairwise_unit(args):
+    """BASELINE config 3 beside the headline: RR-64K pairwise tick replay, ticks 101-500."""
+    a = argparse.Namespace(**vars(args))
+    a.n, a.steps, a.warmup, a.cpu_seconds = 0, 400, 50, 0
+    line = pairwise_line(a)
+    return {"workload": line["config"]["workload"], "value": line["value"], "unit": line["unit"],
+            "ms_per_step": line["ms_per_step"],
+            "us_per_tick": line["roofline"]["avg_launch_us"] / a.steps,  # device time (HIP events)
+            "frac": line["roofline"]["frac"], "traffic": line["roofline"]["traffic"],
+            "roofline": line["roofline"], "pairwise_updates": line["config"]["pairwise_updates"]}
 
 
 def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_total, per, kinfo,
@@ -341,6 +446,27 @@ def dist_line(*, world, steps, warmup, wall, dev1_ms, e_tot, n_tot, halo, n_tota
     }
     line.update(conv)
     return line
+
+
+def window_stats(n, E, kernel_selected, steps):
+    """The kernel-trace record of this exact window (tools/window_stats.py over a rocprofv3
+    --kernel-trace of the same command, committed under profiles/), when one matches: the
+    per-kernel mean durations and the window's round time, from which the roofline fraction
+    can be recomputed."""
+    import glob
+
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "*window_stats.json")), reverse=True):
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if rec.get("n") == n and rec.get("E") == E and rec.get("kernel_selected") == kernel_selected \
+                and rec.get("rounds_timed") == steps:
+            return {"file": os.path.relpath(path, ROOT), "avg_round_us": rec.get("avg_round_us"),
+                    "frac": rec.get("frac"), "per_kernel": rec.get("per_kernel_per_round"),
+                    "box_copy_GBs": rec.get("copy_GBs")}
+    return None
 
 
 def run_dist(args, world, rank, local, dist):
@@ -560,6 +686,10 @@ def pairwise_bytes(events, rowptr, tasks):
 
 
 def run_pairwise(args):
+    print(json.dumps(pairwise_line(args)), flush=True)
+
+
+def pairwise_line(args):
     """BASELINE config 3: pairwise mode on a 64K-node random regular graph (d = 8), the
     SimGrid event order (Peer.loop, mailbox rendez-vous; App. B) replayed on the GPU by the
     persistent dataflow kernel. A step = one tick (PW:69-84 for every actor); the timed ticks
@@ -597,7 +727,7 @@ def run_pairwise(args):
         upd_all = int(np.sum(ev[:, 0] == 2))
         cpu = {"value": upd_all / dt, "unit": "flow-updates/s", "cores": 1, "kind": "port",
                "sample": f"oracle/fu_oracle.c replay of the same trace, all {ticks} ticks ({dt:.2f} s, 1 thread)"}
-    print(json.dumps({
+    return {
         "metric": METRIC, "value": upd / wall, "unit": "flow-updates/s", "n_gpus": 1,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
@@ -612,7 +742,7 @@ def run_pairwise(args):
                      "traffic": pmc_traffic(g.n, g.E, "pairwise", args.steps) if args.warmup == 50 else None,
                      "alg_bytes_per_launch": alg, "kernel": "k_replay_persist_reg",
                      "avg_launch_us": ms * 1e3, "launch_window": f"one launch, {args.steps} ticks"},
-        "cpu_baseline": cpu}), flush=True)
+        "cpu_baseline": cpu}
 
 
 def cpu_baseline(g, v, seconds):

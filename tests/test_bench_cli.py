@@ -152,3 +152,117 @@ def test_pmc_traffic_per_gpu_record(tmp_path, monkeypatch):
     assert bench.pmc_traffic(8388608, None, "rgg-dist", 20, per_gpu=True) == 1.8e9
     assert bench.pmc_traffic(8388608, None, "rgg-dist", 21, per_gpu=True) is None
     assert bench.pmc_traffic(8388608, 5, "rgg-dist", 20) is None
+
+
+class _FakeGraph:
+    def __init__(self, n, E):
+        self.n, self.E, self.max_deg = n, E, 8
+        self.rowptr = np.zeros(n + 1, dtype=np.int64)
+        self.col = np.zeros(0, dtype=np.int32)
+
+
+class _FakeEngine:
+    """A CollectAll stand-in for the bench's control flow on the CPU: rounds advance a
+    counter, every round 'takes' 50 us, the packing plan narrows at rounds 110/150/200."""
+    def __init__(self, g, v, device=0, kernel="auto", layout="given"):
+        self.r, self.marks, self.kernel = 0, {}, kernel
+
+    def tune(self):
+        pass
+
+    def run(self, k, err_every=0):
+        self.r += k
+        return np.zeros(max(k // err_every, 1)) if err_every else None
+
+    def synchronize(self):
+        pass
+
+    def pack_widths(self):
+        w = 8 if self.r >= 200 else 16 if self.r >= 150 else 32 if self.r >= 110 else 0
+        return (w, w, w)
+
+    def reset(self):
+        self.r = 0
+
+    def mark(self, slot):
+        self.marks[slot] = self.r
+
+    def elapsed(self, a, b):
+        return (self.marks[b] - self.marks[a]) * 0.05
+
+    def info(self):
+        return {"kernel": "stage", "nt": 0, "tile": (1024, 128), "tune_passes": 1,
+                "tune_us_per_round": {"stage": 50.0}, "tune_winner_by_width": {0: "stage"}}
+
+    def close(self):
+        pass
+
+
+class _FakeReplay:
+    def __init__(self, tr, v, persistent=False):
+        self.tr = tr
+
+    def run(self, tick_end, snapshot_ticks=()):
+        return {}
+
+    def run_timed(self, tick_end):
+        return 0.5
+
+    def close(self):
+        pass
+
+
+def test_n1_line_carries_config2_rmat24_pairwise_units(monkeypatch, capsys):
+    """The driver's N = 1 command (--steps 20 --warmup 5) measures BASELINE configs 2 (as
+    written: 1000 rounds), 4 (R-MAT-24) and 3 (pairwise RR-64K, ticks 101-500) beside the
+    headline, each guarded so that a failure keeps the headline line (CPU: fake engines)."""
+    import json
+
+    import fu
+
+    graphs = {"er": _FakeGraph(1_000_000, 7_999_972), "rmat": _FakeGraph(1 << 24, 520_761_504)}
+    monkeypatch.setattr(bench, "make_graph", lambda wl, n, m: (graphs[wl], f"{wl} fake"))
+    monkeypatch.setattr(fu, "CollectAll", _FakeEngine)
+    monkeypatch.setattr(fu, "Replay", _FakeReplay)
+    monkeypatch.setattr(fu, "uniform_values", lambda n, seed=0: np.zeros(n))
+    monkeypatch.setattr(fu, "copy_bandwidth", lambda *a: 5500.0)
+    monkeypatch.setattr(bench, "measure_dist", lambda *a: {
+        "config": {"workload": "rgg", "E_directed": 1, "kernel_selected": "recon", "tile_selected": (1024, 128)},
+        "value": 1.0, "unit": "edge-updates/s", "ms_per_step": 1.0,
+        "roofline": {"frac": 0.7, "avg_launch_us": 300.0}})
+    args = bench.parse(["--steps", "20", "--warmup", "5", "--no-conv", "--cpu-seconds", "0"])
+    bench.run_single(args, "er")
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert line["steps"] == 20 and line["roofline"]["copy_GBs"] == 5500.0
+    c2 = line["config2_1000"]
+    assert "error" not in c2, c2
+    assert abs(c2["avg_round_us"] - 50.0) < 1e-9 and len(c2["phases"]) == 11
+    assert abs(c2["frac"] - (24 * 7_999_972 + 28 * 1_000_000) / 50e-6 / 1e9 / 8000.0) < 1e-9
+    assert [p["width"] for p in c2["pack_width_schedule"]] == [0, 32, 16, 8]
+    rm = line["rmat24_unit"]
+    assert "error" not in rm, rm
+    assert rm["E_directed"] == 520_761_504 and rm["steps"] == 20
+    assert abs(rm["frac"] - (24 * 520_761_504 + 28 * (1 << 24)) / 50e-6 / 1e9 / 8000.0) < 1e-9
+    pw = line["pairwise_unit"]
+    assert "error" not in pw, pw
+    assert "ticks 101-500" in pw["workload"] and abs(pw["us_per_tick"] - 0.5e3 / 400) < 1e-3
+    assert line["weak_scaling_unit"]["roofline_frac"] == 0.7
+    # a failing companion keeps the headline
+    monkeypatch.setattr(bench, "rmat24_unit", lambda a: 1 / 0)
+    bench.run_single(args, "er")
+    line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert "ZeroDivisionError" in line["rmat24_unit"]["error"] and line["value"] > 0
+
+
+def test_window_stats_lookup(tmp_path, monkeypatch):
+    import json
+
+    d = tmp_path / "profiles" / "r05"
+    d.mkdir(parents=True)
+    rec = {"n": 10, "E": 40, "kernel_selected": "stage", "rounds_timed": 20, "avg_round_us": 60.0, "frac": 0.45,
+           "per_kernel_per_round": {"k_stage": 17.0}}
+    (d / "x_window_stats.json").write_text(json.dumps(rec))
+    monkeypatch.setattr(bench, "ROOT", str(tmp_path))
+    ws = bench.window_stats(10, 40, "stage", 20)
+    assert ws["file"] == os.path.join("profiles", "r05", "x_window_stats.json") and ws["frac"] == 0.45
+    assert bench.window_stats(10, 40, "stage", 21) is None
