@@ -2934,11 +2934,10 @@ int launch_round(fu_handle *h, unsigned long long *err_slot) {
 }
 
 // Autotune candidates, fixed order (fu_get_info reports per index). Kernel 8 is single-GPU.
-struct TuneCand {
-  int kernel, geo;
-};
-constexpr TuneCand kCands[] = {{4, 0}, {4, 3}, {8, 1}, {4, 1}, {9, 1}};
-constexpr int kNCands = (int)(sizeof(kCands) / sizeof(kCands[0]));
+using FP::kCands;
+using FP::kNCands;
+using FP::kTimed;
+using FP::TuneCand;
 static int width_class(int w) { return w == 8 ? 1 : w == 16 ? 2 : w == 32 ? 3 : 0; }
 static void use_cand(fu_handle *h, const TuneCand &c) {
   h->kernel = c.kernel;
@@ -3312,25 +3311,35 @@ int fu__err_slots(fu_handle *h, int count) {
 // when the packing plan changes width (the packed gather shifts the balance between the
 // candidates), at most kMaxTunes times; fu_tune runs one pass on demand.
 constexpr int kMaxTunes = 4;
-constexpr int kTimed = 8;
 
 static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
-  // multi-GPU: every rank must run the same rounds (each one is a halo exchange), so no
-  // candidate is dropped and none stops early on rank-local timings
-  auto active = [&](int c) { return (h->dist || h->tune_out[c] < 2) && !(h->dist && kCands[c].kernel == 9); };
-  // kernel 9 stages the doubles whatever the packing: a candidate of the unpacked table only
-  auto active9 = [&](int c) { return active(c) && !(kCands[c].kernel == 9 && width != 0); };
-  int32_t need = 0;
-  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 3 + kTimed : 0;  // warm + a confirmation pair + timed
-  if (*budget < need) return FU_OK;  // not enough rounds in this call: try again later
+  // which candidate runs (FP::tune_steps): multi-GPU, every rank must run the same rounds
+  // (each one is a halo exchange), so no candidate is dropped and none stops early on
+  // rank-local timings (tools/plan_check --tune checks the count is rank-independent)
+  FP::TuneRank tr;
+  tr.dist = h->dist != nullptr;
+  tr.width = width;
+  for (int c = 0; c < kNCands; ++c) tr.tune_out[c] = h->tune_out[c];
+  if (FP::tune_need(tr) > *budget) return FU_OK;  // not enough rounds in this call: try again later
   // the pass runs at the table's current width: the host's copy of it is exact once the stream
   // is idle, and no plan runs until the pass ends (h->tuning)
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->pw_pending = false;
   h->seen_width = width = *h->h_pw;
-  need = 0;
-  for (int c = 0; c < kNCands; ++c) need += active9(c) ? 3 + kTimed : 0;
-  if (*budget < need) return FU_OK;
+  tr.width = width;
+  if (FP::tune_need(tr) > *budget) return FU_OK;
+  int steps[kNCands];
+  FP::tune_steps(tr, steps);
+  if (steps[2] != FP::kTuneSkip && ensure_stage(h) != FU_OK) {  // no slice layout fits this graph
+    set_error("");
+    tr.k8_ok = false;
+  }
+  if (steps[4] != FP::kTuneSkip && ensure_transpose(h) != FU_OK) {  // too many nodes for the slices
+    set_error("");
+    tr.k9_ok = false;
+  }
+  FP::tune_steps(tr, steps);
+  const int32_t budget0 = *budget;
   h->tuning = true;
   struct Untune {
     fu_handle *h;
@@ -3341,10 +3350,8 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   for (int c = 0; c < kNCands; ++c) {
     if (!h->dist && h->tune_out[c] >= 2) continue;  // its last ns per round stays reported
     h->tune_ms[c] = 0.f;
-    if (!active9(c)) continue;
-    if (kCands[c].kernel == 8 && ensure_stage(h) != FU_OK) {  // no slice layout fits this graph
-      set_error("");
-      if (!h->dist) continue;
+    if (steps[c] == FP::kTuneSkip) continue;
+    if (steps[c] == FP::kTuneStandIn) {
       // multi-GPU: this rank still runs the candidate's rounds (kernel 4), so that every
       // rank runs the same rounds (each is a halo exchange); its time is never the best
       use_cand(h, kCands[0]);
@@ -3352,10 +3359,6 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
         if (int rc = launch_round(h, nullptr)) return rc;
       *budget -= 1 + kTimed;
       h->tune_ms[c] = 1e30f;
-      continue;
-    }
-    if (kCands[c].kernel == 9 && ensure_transpose(h) != FU_OK) {  // too many nodes for the slices
-      set_error("");
       continue;
     }
     use_cand(h, kCands[c]);
@@ -3402,6 +3405,9 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
     }
   }
   if (bi < 0) return fail(FU_ERR_STATE, "autotune: no candidate ran");
+  if (h->dist && budget0 - *budget != FP::tune_rounds_fixed(tr))
+    return fail(FU_ERR_STATE, "autotune: a multi-GPU pass ran " + std::to_string(budget0 - *budget) + " rounds, not " +
+                                  std::to_string(FP::tune_rounds_fixed(tr)) + " (the ranks would diverge)");
   for (int c = 0; c < kNCands; ++c)
     if (h->tune_ms[c] > 1.3f * h->tune_ms[bi]) h->tune_out[c]++;
   use_cand(h, kCands[bi]);

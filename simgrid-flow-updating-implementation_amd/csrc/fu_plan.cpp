@@ -380,5 +380,37 @@ K9Sched k9_schedule(const Tiles &t1, int n_hub, const K9Opts &o) {
   return s;
 }
 
+// multi-GPU: no candidate is dropped (tune_out) and none stops early on rank-local timings;
+// kernel 9 is single-GPU. Kernel 9 stages the doubles whatever the packing: a candidate of the
+// unpacked table only.
+static bool tune_active(const TuneRank &r, int c) {
+  const bool on = (r.dist || r.tune_out[c] < 2) && !(r.dist && kCands[c].kernel == 9);
+  return on && !(kCands[c].kernel == 9 && r.width != 0);
+}
+
+void tune_steps(const TuneRank &r, int steps[kNCands]) {
+  for (int c = 0; c < kNCands; ++c) {
+    steps[c] = kTuneSkip;
+    if (!tune_active(r, c)) continue;
+    if (kCands[c].kernel == 8 && !r.k8_ok) steps[c] = r.dist ? kTuneStandIn : kTuneSkip;
+    else if (kCands[c].kernel == 9 && !r.k9_ok) steps[c] = kTuneSkip;
+    else steps[c] = kTuneRun;
+  }
+}
+
+int tune_need(const TuneRank &r) {
+  int need = 0;
+  for (int c = 0; c < kNCands; ++c) need += tune_active(r, c) ? 3 + kTimed : 0;  // warm + a confirmation pair + timed
+  return need;
+}
+
+int tune_rounds_fixed(const TuneRank &r) {
+  int st[kNCands];
+  tune_steps(r, st);
+  int n = 0;
+  for (int c = 0; c < kNCands; ++c) n += st[c] != kTuneSkip ? 1 + kTimed : 0;
+  return n;
+}
+
 }  // namespace plan
 }  // namespace fu

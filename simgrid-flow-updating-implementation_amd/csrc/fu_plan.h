@@ -140,5 +140,28 @@ struct K9Sched {
 };
 K9Sched k9_schedule(const Tiles &t1, int n_hub, const K9Opts &o);
 
+// Autotune candidates (fixed order: fu_get_info reports per index) and one pass's steps
+// (autotune_kernel). Per candidate: skipped, run (a warm round + kTimed timed rounds; on one
+// GPU a slow warm round may end the candidate early), or stand-in: a multi-GPU rank on which
+// kernel 8 has no slice layout runs kernel 4 rounds in its place, so that every rank runs the
+// same rounds (each is a halo exchange: a rank running fewer would hang RCCL, not fail).
+struct TuneCand {
+  int kernel, geo;
+};
+constexpr TuneCand kCands[] = {{4, 0}, {4, 3}, {8, 1}, {4, 1}, {9, 1}};
+constexpr int kNCands = (int)(sizeof(kCands) / sizeof(kCands[0]));
+constexpr int kTimed = 8;  // timed rounds per candidate
+enum TuneStep : int { kTuneSkip = 0, kTuneRun = 1, kTuneStandIn = 2 };
+struct TuneRank {
+  bool dist = false;           // a partitioned (multi-GPU) handle
+  int width = 0;               // packing width of the pass (multi-GPU handles never pack)
+  int tune_out[kNCands] = {};  // passes in which the candidate was > 1.3x the best (rank-local)
+  bool k8_ok = true;           // kernel 8 has a slice layout on this rank's graph
+  bool k9_ok = true;           // kernel 9 has a staging layout
+};
+void tune_steps(const TuneRank &r, int steps[kNCands]);
+int tune_need(const TuneRank &r);          // rounds a pass may take (the budget it waits for)
+int tune_rounds_fixed(const TuneRank &r);  // rounds of a pass without warm-round drops (multi-GPU)
+
 }  // namespace plan
 }  // namespace fu

@@ -116,3 +116,12 @@ def test_tiny_graph_plans(plan_check, tmp_path, case):
     for layout in ("given", "degree"):
         _run(plan_check, ["--csr", f, "--layout", layout, "--ht", "128", "--ht", "3", "--hot", "0", "--hot", "64"]
              + MEGAS)
+
+
+def test_autotune_pass_rounds_rank_independent(plan_check):
+    """Multi-GPU: an autotune pass runs the same number of rounds on every rank whatever the
+    rank-local state (forced candidate drops from its own timings, kernel 8 / 9 layouts missing
+    on its graph): each round is a halo exchange, so a mismatch would hang RCCL at N > 1
+    instead of failing (CA:74, CA:124). The engine asserts the same count at run time."""
+    out = _run(plan_check, ["--tune"])
+    assert "4096 rank states, 36 rounds per multi-GPU pass" in out

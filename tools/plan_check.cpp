@@ -572,6 +572,49 @@ void check_all(const Csr &g, int mega, int ht, int hot) {
   check_k8(g, pg, ht);
 }
 
+// ---- the autotune pass (--tune) -----------------------------------------------------------
+// Multi-GPU: every rank runs the same rounds in a pass whatever its rank-local state (tune_out
+// from its own timings, whether kernel 8 / 9 have layouts on its graph): each round is a halo
+// exchange, so a rank running fewer would hang RCCL. Every combination of forced candidate
+// drops (tune_out 0..3 per candidate) and missing layouts, per width.
+void check_tune() {
+  g_ctx = "tune";
+  for (int width : {0, 8, 16, 32}) {
+    int want_rounds = -1, want_need = -1;
+    long combos = 0;
+    for (int code = 0; code < (1 << (2 * FP::kNCands)); ++code)
+      for (int k8 : {1, 0})
+        for (int k9 : {1, 0}) {
+          FP::TuneRank r;
+          r.dist = true;
+          r.width = width;
+          r.k8_ok = k8;
+          r.k9_ok = k9;
+          for (int c = 0; c < FP::kNCands; ++c) r.tune_out[c] = (code >> (2 * c)) & 3;
+          const int rounds = FP::tune_rounds_fixed(r), need = FP::tune_need(r);
+          if (want_rounds < 0) want_rounds = rounds, want_need = need;
+          CHECK(rounds == want_rounds && need == want_need, "width %d tune_out code %d k8 %d k9 %d: %d rounds / need %d, "
+                "other ranks %d / %d", width, code, k8, k9, rounds, need, want_rounds, want_need);
+          CHECK(rounds <= need, "a pass runs more rounds (%d) than it waits for (%d)", rounds, need);
+          int st[FP::kNCands];
+          FP::tune_steps(r, st);
+          CHECK(st[4] == FP::kTuneSkip, "multi-GPU pass runs kernel 9");
+          ++combos;
+        }
+    std::printf("plan_check --tune: width %d, %ld rank states, %d rounds per multi-GPU pass\n", width, combos,
+                want_rounds);
+  }
+  // one GPU: a dropped candidate (tune_out >= 2) is skipped, kernel 9 only at width 0
+  FP::TuneRank r;
+  r.tune_out[1] = 2;
+  int st[FP::kNCands];
+  FP::tune_steps(r, st);
+  CHECK(st[1] == FP::kTuneSkip && st[0] == FP::kTuneRun && st[4] == FP::kTuneRun, "single-GPU steps");
+  r.width = 8;
+  FP::tune_steps(r, st);
+  CHECK(st[4] == FP::kTuneSkip, "kernel 9 at a packed width");
+}
+
 bool read_csr(const char *path, Csr &g) {
   FILE *f = std::fopen(path, "rb");
   if (!f) return false;
@@ -609,6 +652,12 @@ int main(int argc, char **argv) {
   std::string layout = "given";
   std::vector<int> megas, hts, hots;
   fu_graph *gh = nullptr;
+  for (int a = 1; a < argc; ++a)
+    if (!std::strcmp(argv[a], "--tune")) {
+      check_tune();
+      std::printf("plan_check --tune: %ld checks, %ld failed\n", g_checks, g_fail);
+      return g_fail ? 1 : 0;
+    }
   for (int a = 1; a < argc; ++a) {
     const std::string k = argv[a];
     auto need = [&](int cnt) {

@@ -5,6 +5,7 @@ a rocprofv3 --kernel-trace CSV of the same command, as the record bench.py quote
 
     python tools/window_stats.py TRACE.csv --n N --E E --kernel KNAME --steps K [--which I]
                                  [--copy-GBs C] [--out profiles/r05/NAME_window_stats.json]
+                                 [--dump profiles/r05/NAME_window_trace.csv]
 
 The window starts at the (I+1)-th k_round0 launch of the process (I = 1 by default: the first
 k_round0 is the autotune / warmup run, the second the timed run; the R-MAT unit of the N = 1
@@ -33,6 +34,8 @@ def main():
     ap.add_argument("--which", type=int, default=1, help="index of the k_round0 launch that starts the window")
     ap.add_argument("--copy-GBs", type=float, default=None, help="the same run's roofline.copy_GBs")
     ap.add_argument("--out")
+    ap.add_argument("--dump", help="write the window's launches (name, start, end ns) as CSV, so that the "
+                                   "record can be recomputed from a tracked file")
     a = ap.parse_args()
     rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
     seq = []
@@ -79,6 +82,12 @@ def main():
                            "max_us": round(max(v), 3)} for k, v in per.items()},
         "copy_GBs": a.copy_GBs,
     }
+    if a.dump:
+        with open(a.dump, "w") as f:
+            f.write("kernel,start_ns,end_ns\n")
+            for nm, s0, s1 in w[:r0_end] + win:
+                f.write(f'"{nm}",{s0},{s1}\n')
+        rec["window_trace"] = a.dump
     print(json.dumps(rec, indent=1))
     if a.out:
         with open(a.out, "w") as f:
