@@ -233,11 +233,16 @@ int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *
 /* Same, with link sharing (parity-unpinned against SimGrid): the
  * platform's links (bandwidth B/s, latency s, shared = 0 for FATPIPE) and every route
  * (route_links[route_off[src * n + dst] .. route_off[src * n + dst + 1]), n * n + 1 offsets;
- * an empty route = same host). A message matched at tick t starts a transfer at time t:
- * lat_factor * sum(latency) with no bandwidth, then msg_bytes at the max-min fair share of
- * bw_factor * bandwidth on every shared link it crosses (capped by its FATPIPE links); it
- * is consumed at the first tick after its end. Alone, a transfer takes the per-route time
- * above (SimGrid LV08: lat_factor 13.01, bw_factor 0.97, 154-byte messages). */
+ * an empty route = same host, or a pair the platform does not route: delivery within one
+ * tick). A message matched at tick t starts a transfer at time t: lat_factor * sum(latency)
+ * with no bandwidth, then msg_bytes at the max-min fair share of bw_factor * bandwidth on
+ * every shared link it crosses (capped by its FATPIPE links); it is consumed at the first tick
+ * after its end. Alone, a transfer takes the per-route time above (SimGrid LV08: lat_factor
+ * 13.01, bw_factor 0.97, 154-byte messages). Deviation from LV08: every flow on a link gets an
+ * EQUAL max-min share; SimGrid weights each flow's share by its sharing penalty (route latency
+ * plus weight_S / bandwidth per link), so two flows of different routes on one link get
+ * different rates here than in SimGrid. The reference platform's 154-byte transfers all end
+ * within one tick, where the two agree (the plain schedule); no TCP-window bound either. */
 int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
                          int32_t ticks, const char *order, const char *faults, int32_t n_links,
                          const double *link_bw, const double *link_lat, const int32_t *link_shared,

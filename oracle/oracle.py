@@ -197,7 +197,9 @@ class LinkNet:
     operation for operation so both give the same doubles: a transfer matched at tick t has
     a latency phase of lat_factor * sum(latency), then `bytes` at its max-min fair share of
     bw_factor * bandwidth on the shared links it crosses, capped by its FATPIPE links.
-    Parity-unpinned against SimGrid (not installable offline)."""
+    Every flow on a link gets an equal share (plain max-min); SimGrid's LV08 weights shares by
+    each flow's sharing penalty -- a documented deviation (fu.h). Parity-unpinned against
+    SimGrid (not installable offline)."""
 
     def __init__(self, net):
         self.n = int(net["n"])

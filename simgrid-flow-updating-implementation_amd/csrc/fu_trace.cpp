@@ -109,7 +109,10 @@ struct LinkNet {
     }
     active.push_back(id);
   }
-  // progressive filling over the data-phase transfers
+  // progressive filling over the data-phase transfers, every flow on a link with an EQUAL
+  // share (plain max-min). SimGrid's LV08 weights a flow's share by its sharing penalty (route
+  // latency + weight_S / bandwidth per link): a documented deviation (fu.h), parity-unpinned;
+  // it changes nothing while every transfer ends within its tick (the reference platform)
   void rates() {
     std::vector<double> crem(n_links, 0.0);
     std::vector<int32_t> cnt(n_links, 0);

@@ -60,3 +60,32 @@ def test_deployment_errors(tmp_path):
     write_deployment_xml(p, [("a", "1.5", "b,b"), ("b", "2", "")])
     names, values, nbrs = load_deployment(str(p)).peers()
     assert nbrs == [["b"], []]  # dict keys collapse duplicates (CA:38-40)
+
+
+def test_link_net_missing_route_is_one_tick(tmp_path):
+    """A platform that routes only some host pairs still runs: a neighbouring pair without a
+    route gets an empty route (delivery within one tick, the plain schedule, CA:76), as the
+    per-route model treated it; the trace equals the plain one when no route is slow."""
+    import fu
+
+    d = load_json("tick_small_platform_ca_fwd.json")
+    hosts = [a[0] for a in d["actors"]]
+    lines = ["<?xml version='1.0'?>", '<platform version="4.1">', '  <zone id="z" routing="Full">']
+    lines += [f'    <host id="{h}" speed="1Gf"/>' for h in hosts]
+    lines.append('    <link id="fast" bandwidth="1GBps" latency="1us"/>')
+    lines += [f'    <route src="{hosts[0]}" dst="{hosts[1]}">', '      <link_ctn id="fast"/>', "    </route>"]
+    lines += ["  </zone>", "</platform>"]
+    pf = tmp_path / "partial.xml"
+    pf.write_text("\n".join(lines) + "\n")
+    plat = load_platform(str(pf))
+    names = [a[0] for a in d["actors"]]
+    nbrs = [a[2].split(",") if a[2] else [] for a in d["actors"]]
+    rp, col = declared_csr(names, nbrs)
+    net = plat.link_net(names)
+    n = len(names)
+    assert net["route_off"][-1] == 2  # only the routed pair (both directions) holds a link
+    plain = fu.Trace(rp, col, "collectall", 300, "fwd").arrays()
+    linked = fu.Trace(rp, col, "collectall", 300, "fwd", net=net).arrays()
+    for k in ("events", "tasks", "tick_task_off"):
+        assert np.array_equal(plain[k], linked[k]), k
+    assert n == 6
