@@ -5,7 +5,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 AB_SPEC="rmat:scale=24,ef=16" AB_ARGS="--warm=3 --timed=20 --reps=3" AB_ROUNDS=1 \
-  AB_VARIANTS="deg_np_pre pre_hot_cu32 pre_hot_cu32s pre_hot_cu16s pre_hot_cu64s pre_cu32s pre_hot deg_np_pre pre_hot_cu16 pre_hot_cu64" \
+  AB_VARIANTS="deg_np_pre pre_hot_cu32 pre_hot_cu32s pre_hot_cu16s pre_hot_cu64s pre_cu32s pre_hot deg_np_pre pre_hot_cu16 pre_hot_cu64"  # (variants removed with the option after this session) \
   bash tools/ab_proc.sh || exit $?
 mkdir -p gpurun_out/b
 timeout -k 10 300 python -u -m pytest -s -x -v --timeout 200 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "hub_cus" > gpurun_out/b/pytest_hubcus.log 2>&1 || exit $?

@@ -2263,10 +2263,6 @@ struct fu_handle {
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
   int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
-  int hub_cus = 0;            // kernel 9: CUs reserved for the hub path (chains, k_hub_flows); 0 = shared
-  int hub_cu_stride = 0;      // ... their mask bits: 0 = the lowest hub_cus bits, 1 = spread evenly
-  hipStream_t cu_main = nullptr, cu_hub = nullptr;  // the CU-masked streams of hub_cus
-  hipEvent_t ev_cu[2] = {nullptr, nullptr};
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -2682,34 +2678,6 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
 // Kernel 9: k_stage -> k_transpose (the mega-hub buckets first) -> kernel 4's tiles reading
 // the pre-gathered estimates; the mega hubs' chains and k_hub_flows on the side stream beside
 // the remaining buckets and tiles.
-// hub_cus: two streams with complementary CU masks (hipExtStreamCreateWithCUMask), the hub
-// path's hub_cus CUs either the lowest mask bits or spread over the mask (the bit -> CU order
-// is the runtime's: both are measured)
-void free_cu_streams(fu_handle *h) {
-  if (h->cu_main) hipStreamSynchronize(h->cu_main);
-  if (h->cu_hub) hipStreamSynchronize(h->cu_hub);
-  for (hipStream_t s : {h->cu_main, h->cu_hub})
-    if (s) hipStreamDestroy(s);
-  for (hipEvent_t e : h->ev_cu)
-    if (e) hipEventDestroy(e);
-  h->cu_main = h->cu_hub = nullptr;
-  h->ev_cu[0] = h->ev_cu[1] = nullptr;
-}
-int ensure_cu_streams(fu_handle *h) {
-  if (h->cu_main) return FU_OK;
-  const int ncu = h->n_cu, k = std::min(h->hub_cus, ncu - 8);
-  if (k < 1) return fail(FU_ERR_ARG, "hub_cus: at least 8 CUs must stay on the main stream");
-  std::vector<uint32_t> hub((ncu + 31) / 32, 0u), mainm((ncu + 31) / 32, 0u);
-  std::vector<char> sel(ncu, 0);
-  for (int q = 0; q < k; ++q) sel[h->hub_cu_stride ? (int)((int64_t)q * ncu / k) : q] = 1;
-  for (int i = 0; i < ncu; ++i) (sel[i] ? hub : mainm)[i / 32] |= 1u << (i % 32);
-  HIP_TRY(hipExtStreamCreateWithCUMask(&h->cu_main, (uint32_t)mainm.size(), mainm.data()));
-  HIP_TRY(hipExtStreamCreateWithCUMask(&h->cu_hub, (uint32_t)hub.size(), hub.data()));
-  HIP_TRY(hipEventCreateWithFlags(&h->ev_cu[0], hipEventDisableTiming));
-  HIP_TRY(hipEventCreateWithFlags(&h->ev_cu[1], hipEventDisableTiming));
-  return FU_OK;
-}
-
 int launch_k9(fu_handle *h, RoundCtx &c) {
   if (int rc = ensure_transpose(h)) return rc;  // rebuilt after a tile option changed
   double *Gb = h->tr.GBr[c.r % 3];
@@ -2729,9 +2697,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int nmega = ks.nmega, nh = ks.nh, niso = ks.niso, nl = ks.nl, m0 = ks.m0, m1 = ks.m1;
   const int4 *tl = h->tiles_geo[1];
   const bool hubs = nmega > 0;
-  // hub_cus: the round on two CU-masked streams, the hub path (chains, k_hub_flows) on
-  // hub_cus CUs of its own and every other launch on the rest, so that the chains' dependent
-  // adds do not share SIMDs with the transposes and the heavy rows
   // lag: the rows this round leaves their flows to round r + 2 (k_heavy_multi<LAG>): the
   // multi-row heavy rows
   const int n_multi = ks.n_multi, m1s = ks.m1s;
@@ -2742,15 +2707,6 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (int rc = lag_finalize(h, p)) return rc;  // the lagged set changed: write its flows first
   }
   const int lagm = lag_multi ? (h->lagf[p] ? 2 : 1) : 0;
-  hipStream_t ms = h->stream, hs2 = h->stream2;
-  const bool masked = h->hub_cus > 0 && hubs;
-  if (masked) {  // the masked main stream continues the handle's stream
-    if (int rc = ensure_cu_streams(h)) return rc;
-    ms = h->cu_main;
-    hs2 = h->cu_hub;
-    HIP_TRY(hipEventRecord(h->ev_cu[0], h->stream));
-    HIP_TRY(hipStreamWaitEvent(ms, h->ev_cu[0], 0));
-  }
   StageArgs sa{};
   for (int li = 0; li < 4; ++li) sa.sel[li] = 3;
   sa.P[3] = h->tr.P;
@@ -2761,7 +2717,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   sa.colS[3] = h->tr.colS;
   sa.f64 = 1;
   {
-    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, ms, sa, h->n, c.ap,
+    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap,
                        cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
@@ -2769,43 +2725,43 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const int bh = hubs ? h->tr.Bh : 0;
   auto tr_launch = [&](int b0, int nb) {
     if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
-      hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, ms, b0, nb, h->tr.P,
+      hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
-      hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, ms, b0, nb, h->tr.P,
+      hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
     else if (h->tr_nt)
-      hipLaunchKernelGGL((k_transpose<0, true>), dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, ms, b0, nb, h->tr.P,
+      hipLaunchKernelGGL((k_transpose<0, true>), dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
     else
-      hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, ms, b0, nb, h->tr.P,
+      hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
                          (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
   };
   if (bh) tr_launch(0, bh);
   if (hubs) {
-    HIP_TRY(hipEventRecord(h->ev_fork, ms));
-    HIP_TRY(hipStreamWaitEvent(hs2, h->ev_fork, 0));
+    HIP_TRY(hipEventRecord(h->ev_fork, h->stream));
+    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_fork, 0));
   }
   if (h->tr.B > bh) tr_launch(bh, h->tr.B - bh);
   const bool chk = c.err != nullptr;
   if (hubs) {
     auto chains = [&](auto C) {
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
-                         0, hs2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm);
     };
     if (chk) chains(std::true_type{});
     else chains(std::false_type{});
-    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs2, h->n_hub, h->hub_rows,
+    hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, h->stream2, h->n_hub, h->hub_rows,
                        (long long)h->hub_total, nullptr, c.an, c.F, Gb, c.ap2, c.fm, h->hub_blk);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(h->ev_join, hs2));
+    HIP_TRY(hipEventRecord(h->ev_join, h->stream2));
   }
   // heavy tiles [t0, t1) with RL register elements per lane
   auto heavy = [&](auto C, auto RL, int t0, int t1) {
     if (t1 > t0)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, decltype(RL)::value>),
-                         dim3(t1 - t0), dim3(kBlock), 0, ms, tl + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
+                         dim3(t1 - t0), dim3(kBlock), 0, h->stream, tl + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                          c.fm);
   };
@@ -2818,7 +2774,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     if (multi) {
       auto hm = [&](auto L) {
         hipLaunchKernelGGL((k_heavy_multi<decltype(C)::value, decltype(L)::value>), dim3((n_multi + kMR - 1) / kMR),
-                           dim3(kBlock), 0, ms, h->hrows + h->multi_geo[1][0], n_multi,
+                           dim3(kBlock), 0, h->stream, h->hrows + h->multi_geo[1][0], n_multi,
                            h->rowptr, h->v, c.F, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, Gb, c.fm, Gb_old,
                            h->tr.hist[p]);
       };
@@ -2832,22 +2788,18 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
     }
     heavy(C, std::integral_constant<int, kHeavyRL>{}, m1s, nh);
     if (niso)
-      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, ms,
+      hipLaunchKernelGGL(k_isolated, dim3(grid_for(h->n - h->iso0_geo[1])), dim3(kBlock), 0, h->stream,
                          h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
                          decltype(C)::value ? 1 : 0);
     if (nl)
       hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
-                         ms, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
+                         h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
   };
   if (chk) tiles(std::true_type{});
   else tiles(std::false_type{});
   HIP_TRY(hipGetLastError());
-  if (hubs) HIP_TRY(hipStreamWaitEvent(ms, h->ev_join, 0));
-  if (masked) {  // the handle's stream continues after the round
-    HIP_TRY(hipEventRecord(h->ev_cu[1], ms));
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_cu[1], 0));
-  }
+  if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
   if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
     h->lagf[p] = 1;
     h->lag_round[p] = c.r;
@@ -3266,17 +3218,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose streams G_A / G_B non-temporally (1)
     if (value != 0 && value != 1) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0 or 1");
     h->tr_nt = (int)value;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_cus")) {  // kernel 9: CUs reserved for the hub path (0 = shared)
-    if (value < 0 || value > 248) return fail(FU_ERR_ARG, "fu_set_option: hub_cus must be in [0, 248]");
-    free_cu_streams(h);
-    h->hub_cus = (int)value;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "hub_cu_stride")) {  // kernel 9: hub_cus as the lowest mask bits (0) or spread (1)
-    free_cu_streams(h);
-    h->hub_cu_stride = value != 0;
     return FU_OK;
   }
   if (!std::strcmp(key, "multi_short")) {  // kernel 9: rows of 129-256 edges as multi-row blocks (1)
@@ -3758,7 +3699,6 @@ int fu_destroy(fu_handle *h) {
   if (h->stream) hipStreamSynchronize(h->stream);
   if (h->stream2) hipStreamSynchronize(h->stream2);
   if (h->dist) fu__dist_free(h);
-  free_cu_streams(h);
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
                               h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,

@@ -142,7 +142,7 @@ def test_option_errors():
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse",
-                "tr_pipe", "hub_prio", "side_tiles", "split_tr"):
+                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
     for key, val in (("tr_nt", 2), ("tr_nt", -1)):
@@ -674,37 +674,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     assert np.max(np.abs(a_ref - tgt)) == tr[-1]
-
-
-@pytest.mark.parametrize("cus,stride,hot", [(32, 0, 0), (16, 1, 10240), (64, 1, 0)])
-def test_pregather_hub_cus_bitwise(cus, stride, hot):
-    """Kernel 9 with the hub path on CU-masked streams (option hub_cus: the chains and
-    k_hub_flows on reserved CUs, every other launch on the rest, the handle's stream joined
-    after each round): bitwise against the C oracle with the error check, packing and
-    fu_get_flows between runs; switching the option mid-run rebuilds the streams."""
-    g = fu.Graph.rmat(15, 16, seed=34)
-    v = fu.uniform_values(g.n, seed=34)
-    eng = fu.CollectAll(g, v, kernel="pregather", layout="degree")
-    eng.set_option("mega_hub", 500)
-    eng.set_option("hub_cus", cus)
-    eng.set_option("hub_cu_stride", stride)
-    if hot:
-        eng.set_option("tr_hot", hot)
-    eng.set_option("pack_every", 4)
-    tgt, _ = fu.component_means(g.rowptr, g.col, v)
-    eng.set_targets(tgt)
-    done = 0
-    for k, cu in ((7, cus), (9, 0), (14, cus)):
-        eng.set_option("hub_cus", cu)
-        tr = eng.run(k, err_every=1)
-        done += k
-        a_ref, f_ref = coracle.ca_sync(*g.arrays(), v, done, nthreads=16)
-        assert np.array_equal(eng.estimates(), a_ref), done
-        assert np.array_equal(eng.flows(), f_ref), done
-        assert np.max(np.abs(a_ref - tgt)) == tr[-1]
-    with pytest.raises(fu.FuError):
-        eng.set_option("hub_cus", 300)
-    eng.close()
 
 
 @pytest.mark.parametrize("mega", [100, 1000])

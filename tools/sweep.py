@@ -60,13 +60,6 @@ VARIANTS = {
     "deg_np_ht128": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 128}),
     "deg_np_ht256": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
-    "pre_hot_cu16": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 16}),
-    "pre_hot_cu32": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 32}),
-    "pre_hot_cu64": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 64}),
-    "pre_hot_cu16s": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 16, "hub_cu_stride": 1}),
-    "pre_hot_cu32s": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 32, "hub_cu_stride": 1}),
-    "pre_hot_cu64s": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "hub_cus": 64, "hub_cu_stride": 1}),
-    "pre_cu32s": ("pregather", {"layout": "degree", "pack": 0, "hub_cus": 32, "hub_cu_stride": 1}),
     "stage": ("stage", {}),
     "stage_nopack": ("stage", {"pack": 0}),
     "stage_lo0": ("stage", {"staged_lo": 0}),
