@@ -73,6 +73,8 @@ def parse(argv=None):
     ap.add_argument("--no-conv", action="store_true")
     ap.add_argument("--strong", action="store_true",
                     help="rgg-dist: strong scaling, --n nodes in all (2^26 by default) split over the ranks")
+    ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
+                    help="engine option for the headline engine (fu_set_option; A/B runs)")
     ap.add_argument("--no-unit", action="store_true",
                     help="N = 1 default line without its weak_scaling_unit (config 5's per-GPU RGG)")
     return ap.parse_args(argv)
@@ -270,6 +272,9 @@ def run_single(args, wl):
     layout = args.layout if args.layout != "auto" else ("degree" if wl == "rmat" else "given")
     device = 0
     eng = fu.CollectAll(g, v, device=device, kernel=args.kernel, layout=layout)
+    for kv in args.opt:
+        k, val = kv.split("=", 1)
+        eng.set_option(k, int(val))
     t_setup = time.perf_counter()
     prepare(eng, args.kernel, args.warmup)
     t_setup = time.perf_counter() - t_setup
@@ -312,6 +317,7 @@ def run_single(args, wl):
             "autotune_us_per_round": kinfo["tune_us_per_round"],
             "autotune_winner_by_width": kinfo["tune_winner_by_width"],
             "pack_width_after": pack_after, "setup_s": t_setup, "phases": phases,
+            "options": args.opt,
             "parallelism": "single GPU",
         },
         "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen,
