@@ -141,7 +141,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "staged_lo"     kernel 8: staged indices loaded ahead of the flows (1, default) or
  *                 interleaved with them (0; the round-1 order, kept for A/B and tests).
  * Removed after measurement (FU_ERR_ARG): "tr_pipe", "hub_prio", "side_tiles", "split_tr",
- * "hub_cus" / "hub_cu_stride" (the hub path on CU-masked streams: round 5, profiles/r05/b)
+ * "hub_cus" / "hub_cu_stride" (the hub path on CU-masked streams: round 5, profiles/r05/b),
+ * "st_split" (kernel 8's next stage overlapping this round's tiles: profiles/r05/c)
  * (DESIGN.md §4.12), "hub_multi", "hub_blocks", "fuse", "light_geo". */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */

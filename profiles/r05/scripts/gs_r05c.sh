@@ -1,4 +1,5 @@
 # round 5, session c: kernel 8 option st_split (the next round's stage on a second stream in
+# (the st_split option was removed after this session: profiles/r05/c)
 # two slice groups, each behind the tiles of its rows; G double-buffered) on ER-1M: the
 # parity test, then the driver's command with and without it, alternating in separate
 # processes (x3), and a kernel trace of the split window.

@@ -881,7 +881,6 @@ struct StageArgs {
   const int *dtab[4];                  // per light tile: kStageRuns x (G index - m) of each run
   int sel[4];                          // layout used for tables of width 8, 16, 32, 0
   int f64;                             // kernel 9: always stage the doubles (layout 3)
-  int B1[4];                           // st_split: stage blocks of the first slice group (part 1)
 };
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
@@ -1006,7 +1005,7 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         const void *__restrict__ code_prev,
                                                         PackCtl *ctl, int rslot,
                                                         void *__restrict__ G, const int *__restrict__ psample,
-                                                        int *pw_host, int part = 0) {
+                                                        int *pw_host) {
   __shared__ __align__(16) unsigned char s_tab[kStageLds];
   // the packing plan from a_{r-1} (the table staged here; due after round r-1) rides on the
   // stage launch: k_round_staged, the plan's first reader, starts after this launch, so the
@@ -1023,9 +1022,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
   // bytes per element of the table gathered (kernel 9 stages the doubles, always written)
   const int wb = (pp.width && !sa.f64) ? pp.width / 8 : 8;
   const int li = sa.f64 ? 3 : sa.sel[width_index(pp.width)];
-  // st_split: part 1 = the stage blocks of the first slice group, part 2 = the rest (0 = all)
-  if (part == 1 && bid >= sa.B1[li]) return;
-  if (part == 2) bid += sa.B1[li];
   if (bid >= sa.NB[li]) return;
   const int4 rg = sa.brange[li][bid];
   if (rg.x >= rg.y) return;  // no slice here (grid rounded to whole XCD rows) or empty region
@@ -2299,16 +2295,6 @@ struct fu_handle {
   void *stG = nullptr;                    // staged estimates, 8 B per G element
   int seen_width = 0;                     // packing width the host last saw
   int st_force = -1;                      // tests: force layout 0..3 (element bytes 1, 2, 4, 8)
-  // option st_split: round r + 1's stage launch in two parts on stream2, part 1 (the slices of
-  // rows [0, st_row1)) behind round r's tiles of those rows (ev_t1), part 2 behind the rest
-  // (ev_t2), so that the stage of the next round overlaps the tail of this round's tiles; G
-  // double-buffered (stGb[r & 1])
-  int st_split = 0;
-  int st_row1 = 0, st_T1 = 0;             // the split row (a multiple of 2^19) and the tiles below it
-  void *stGb[2] = {nullptr, nullptr};     // stGb[0] = stG
-  int64_t st_gmax = 0;
-  int64_t st_prev = -1;                   // last round whose tile parts recorded ev_t1 / ev_t2
-  hipEvent_t ev_t1 = nullptr, ev_t2 = nullptr, ev_st = nullptr;
   std::vector<FP::I4> h_light;            // host copy (layout construction)
   // kernel 9 (pregather): slice-major G_A, per-bucket run starts, edge-order Gb
   struct TransLayout {
@@ -2484,18 +2470,6 @@ int ensure_stage(fu_handle *h) {
   }
   if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stG), (size_t)gmax)) return rc;
   HIP_TRY(hipMemset(h->stG, 0, sizeof(unsigned long long) * (size_t)gmax));
-  h->stGb[0] = h->stG;
-  h->st_gmax = gmax;
-  // st_split's row: a multiple of 8 x 65536 (so that it ends a whole XCD row of stage blocks in
-  // every layout), the one nearest half of the rows; the light tiles below it (row order, one GPU)
-  {
-    const int64_t q = std::max<int64_t>(1, std::llround(h->n / 2.0 / 524288.0)) * 524288;
-    h->st_row1 = h->dist || q >= h->n ? 0 : (int)q;
-  }
-  h->st_T1 = 0;
-  if (h->st_row1 > 0)
-    while (h->st_T1 < (int)h->h_light.size() && h->h_light[h->st_T1].y <= h->st_row1) ++h->st_T1;
-  if (h->st_T1 >= (int)h->h_light.size()) h->st_T1 = 0;
   h->st_ready = true;
   return FU_OK;
 }
@@ -2516,7 +2490,6 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
     sa.colS[li] = L.colS;
     sa.sidx16[li] = L.sidx16;
     sa.dtab[li] = L.dtab;
-    sa.B1[li] = L.P && h->st_row1 ? 8 * L.Q * (h->st_row1 / L.SN / 8) : 0;
     if (L.P) g = std::max<unsigned>(g, (unsigned)L.NB);
   }
   for (int want = 0; want < 4; ++want) {
@@ -2635,7 +2608,6 @@ void plan_alone(fu_handle *h, RoundCtx &c) {
 int launch_round0(fu_handle *h, RoundCtx &c) {
   static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
   h->lagf[0] = h->lagf[1] = 0;  // zero state: no lagged flows
-  h->st_prev = -1;               // round 1's stage runs in order
   hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
                      h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
   if (c.err)
@@ -2656,37 +2628,9 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   unsigned sgrid = 1;
   const StageArgs sa = stage_args(h, &sgrid);
   const void *cp = h->code[(c.r - 1) & 1];
-  // st_split (one GPU): G double-buffered, this round's stage on stream2 in two parts behind the
-  // previous round's two tile parts (when the previous round split its tiles), the tiles in two
-  // parts recording ev_t1 / ev_t2 for the next round's stage
-  const bool split = h->st_split && h->st_T1 > 0 && !h->dist && h->st_ntiles > 0;
-  if (split && !h->stGb[1]) {
-    if (int rc = dmalloc(reinterpret_cast<unsigned long long **>(&h->stGb[1]), (size_t)h->st_gmax)) return rc;
-    HIP_TRY(hipMemset(h->stGb[1], 0, sizeof(unsigned long long) * (size_t)h->st_gmax));
-  }
-  void *G = split ? h->stGb[r1] : h->stG;
-  if (split && h->st_prev == c.r - 1) {
-    unsigned g1 = 1, g2 = 1;
-    for (int li = 0; li < 4; ++li)
-      if (h->st[li].P) {
-        g1 = std::max<unsigned>(g1, (unsigned)sa.B1[li]);
-        g2 = std::max<unsigned>(g2, (unsigned)(h->st[li].NB - sa.B1[li]));
-      }
-    // part 1 reads a_{r-1} of rows [0, st_row1): done once the previous round's first tile part
-    // (and its heavy rows, launched before it) retired; part 2 carries the packing plan, which
-    // samples the whole table and rewrites the plan the previous round's tiles encode with
-    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_t1, 0));
-    hipLaunchKernelGGL(k_stage, dim3(g1), dim3(kStageThreads), 0, h->stream2, sa, h->na, c.ap, cp, h->pctl, r1, G,
-                       nullptr, h->pw_dev, 1);
-    HIP_TRY(hipStreamWaitEvent(h->stream2, h->ev_t2, 0));
-    hipLaunchKernelGGL(k_stage, dim3(g2 + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream2, sa, h->na, c.ap, cp,
-                       h->pctl, r1, G, c.plan ? h->psample : nullptr, h->pw_dev, 2);
-    HIP_TRY(hipEventRecord(h->ev_st, h->stream2));
-    HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_st, 0));
-    c.plan = false;
-  } else if (h->st_ntiles) {
+  if (h->st_ntiles) {
     hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap, cp,
-                       h->pctl, r1, G, c.plan ? h->psample : nullptr, h->pw_dev, 0);
+                       h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
   plan_alone(h, c);
@@ -2703,22 +2647,20 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   // multi-GPU: the boundary tiles [0, st_nbound), then the halo goes out on the comm stream
   // beside the interior tiles
   auto light = [&](auto chk, auto rf, auto lo) -> int {
-    // multi-GPU: [0, st_nbound) then the rest; st_split: [0, st_T1) then the rest
-    const int nb = h->dist ? h->st_nbound : split ? h->st_T1 : 0;
+    // multi-GPU: the boundary tiles [0, st_nbound), then the rest
+    const int nb = h->dist ? h->st_nbound : 0;
     for (int part = 0; part < 2; ++part) {
       const int t0 = part ? nb : 0, cnt = part ? h->st_ntiles - nb : nb;
       if (cnt)
         hipLaunchKernelGGL((k_round_staged<decltype(chk)::value, kStageTE, kStageTN, decltype(rf)::value,
                                            decltype(lo)::value>),
                            dim3(cnt), dim3(kBlock), 0, h->stream, h->st_tiles, t0, cnt, h->rowptr, h->col, sa,
-                           G, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
+                           h->stG, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, h->code[r1], h->pctl, r1, c.fm);
       if (!part && h->dist) {  // boundary rows (and the heavy rows) done
         h->halo_a = c.an;
         if (int rc = fu__dist_round_hook(h, 2)) return rc;
       }
-      if (split) HIP_TRY(hipEventRecord(part ? h->ev_t2 : h->ev_t1, h->stream));
     }
-    if (split) h->st_prev = c.r;
     return FU_OK;
   };
   auto light_lo = [&](auto chk, auto rf) {
@@ -3080,10 +3022,7 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipEventCreate(&h->ev2) != hipSuccess || hipEventCreate(&h->ev3) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_pw, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_t1, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_t2, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&h->ev_st, hipEventDisableTiming) != hipSuccess)
+      hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
@@ -3248,11 +3187,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "split_hubs")) {  // kernel 4: mega-hub tiles alone on the side stream (1)
     h->split_hubs = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "st_split")) {  // kernel 8: the next round's stage overlaps this round's tiles (1)
-    h->st_split = value != 0;
-    h->st_prev = -1;
     return FU_OK;
   }
   if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
@@ -3769,7 +3703,7 @@ int fu_destroy(fu_handle *h) {
   std::vector<void *> ptrs = {h->rowptr, h->col, h->blk_row, h->v, h->f[0], h->f[1], h->a[0], h->a[1], h->a[2], h->target,
                               h->err, h->ftmp, h->tiles_geo[0], h->tiles_geo[1], h->tiles_geo[2], h->tiles_geo[3],
                               h->hrows, h->hub_rows, h->hub_off, h->hubxy, h->hub_blk, h->code[0], h->code[1], h->pctl,
-                              h->psample, h->st_tiles, h->st_heavy, h->stG, h->stGb[1], h->col16, h->cbase,
+                              h->psample, h->st_tiles, h->st_heavy, h->stG, h->col16, h->cbase,
                               h->tnar_geo[0], h->tnar_geo[1], h->tnar_geo[2], h->tnar_geo[3]};
   free_transpose(h);
   for (const auto &L : h->st) {
@@ -3780,7 +3714,7 @@ int fu_destroy(fu_handle *h) {
   }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_t1, h->ev_t2, h->ev_st})
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);

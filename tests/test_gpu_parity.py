@@ -142,7 +142,7 @@ def test_option_errors():
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse",
-                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride"):
+                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride", "st_split"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
     for key, val in (("tr_nt", 2), ("tr_nt", -1)):
@@ -674,29 +674,6 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
     assert np.max(np.abs(a_ref - tgt)) == tr[-1]
-
-
-def test_stage_split_er1m_bitwise():
-    """Kernel 8 with st_split (the next round's stage on a second stream in two slice groups,
-    each behind the tiles of its rows, G double-buffered) on ER-1M: bitwise against the C oracle
-    through 300 rounds with packing every 4 rounds (every stage layout width), the option
-    toggled mid-run and the estimates / flows read between runs (CA:105-128)."""
-    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
-    v = fu.uniform_values(g.n, seed=0)
-    eng = fu.CollectAll(g, v, kernel="stage")
-    eng.set_option("st_split", 1)
-    eng.set_option("pack_every", 4)
-    done = 0
-    for k, sp in ((25, 1), (10, 0), (165, 1), (100, 1)):
-        eng.set_option("st_split", sp)
-        eng.run(k)
-        done += k
-        if done in (25, 200, 300):
-            a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, done, nthreads=16)
-            assert np.array_equal(eng.estimates(), a_ref), done
-            assert np.array_equal(eng.flows(), f_ref), done
-    assert eng.pack_widths()[2] in (8, 16, 32)
-    eng.close()
 
 
 @pytest.mark.parametrize("mega", [100, 1000])

@@ -61,8 +61,6 @@ VARIANTS = {
     "deg_np_ht256": ("recon", {"layout": "degree", "pack": 0, "hub_threshold": 256}),
     "deg_np_nosplit": ("recon", {"layout": "degree", "pack": 0, "split_hubs": 0}),
     "stage": ("stage", {}),
-    "stage_split": ("stage", {"st_split": 1}),
-    "stage_split_nopack": ("stage", {"st_split": 1, "pack": 0}),
     "stage_nopack": ("stage", {"pack": 0}),
     "stage_lo0": ("stage", {"staged_lo": 0}),
     "stage_pe64": ("stage", {"pack_every": 64}),
