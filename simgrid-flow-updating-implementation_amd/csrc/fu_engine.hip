@@ -2718,7 +2718,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   sa.colS[3] = h->tr.colS;
   sa.f64 = 1;
   {
-    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->n, c.ap,
+    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap,
                        cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
@@ -2801,6 +2801,10 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   else tiles(std::false_type{});
   HIP_TRY(hipGetLastError());
   if (hubs) HIP_TRY(hipStreamWaitEvent(h->stream, h->ev_join, 0));
+  if (h->dist) {  // multi-GPU: boundary rows sit in every row class, so a_r goes out after the round
+    h->halo_a = c.an;
+    if (int rc = fu__dist_round_hook(h, 2)) return rc;
+  }
   if (lagm) {  // F[p] now holds f_{r-2} on the lagged rows; round r + 2 (or lag_finalize) writes f_r
     h->lagf[p] = 1;
     h->lag_round[p] = c.r;
@@ -3133,7 +3137,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   if (!std::strcmp(key, "kernel")) {
     if (value != 0 && value != 4 && value != 8 && value != 9)
       return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon), 8 (stage) or 9 (pregather)");
-    if (h->dist && value == 9) return fail(FU_ERR_ARG, "fu_set_option: multi-GPU supports kernels 4 (recon) and 8 (stage)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
     if (value == 8) {
       if (int rc = ensure_stage(h)) return rc;

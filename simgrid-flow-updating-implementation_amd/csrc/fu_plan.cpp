@@ -298,7 +298,7 @@ bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const i
   out = TransPlan{};
   const int64_t n = g.n, E = g.E;
   const int64_t SN = kStageLds / 8;
-  const int64_t P = (n + SN - 1) / SN;
+  const int64_t P = ((int64_t)g.na + SN - 1) / SN;  // multi-GPU: the ghost slots are slices too
   if (E == 0 || P > kTrMaxP) {
     if (why) *why = E == 0 ? "kernel 9 (pregather): no edges" : "kernel 9 (pregather): more than 2^25 nodes";
     return false;

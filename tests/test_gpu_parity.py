@@ -345,6 +345,41 @@ def test_dist_rmat_heavy_rows_and_hubs_with_ghosts_bitwise(world, geo):
         e.close()
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_kernel9_rmat_ghosts_bitwise(world):
+    """Kernel 9 on a partitioned R-MAT (in-process transport): the staging slices cover the
+    ghost estimate slots, the transposes deliver halo estimates to heavy rows, mega hubs and
+    light tiles, and the halo goes out after the round (boundary rows sit in every row class).
+    60 rounds with lag, bitwise against the C oracle; then a switch to kernel 4 after a reset."""
+    from fu.dist import DistCollectAll, partition, run_local
+
+    g = fu.Graph.rmat(14, 16, seed=5)
+    v = fu.uniform_values(g.n, seed=6)
+    plans = [partition(g.rowptr, g.col, g.rev, world, r) for r in range(world)]
+    engs = []
+    for p in plans:
+        e = DistCollectAll(p, v[p.lo:p.hi], None, kernel="pregather")
+        for key, val in (("hub_threshold", 32), ("mega_hub", 256)):
+            fu._lib.call("fu_set_option", e._h, key.encode(), val)
+        engs.append(e)
+    assert all(e.info()["kernel"] == "pregather" and e.info()["mega_hubs"] > 0 for e in engs)
+    for rounds in (7, 60):
+        run_local(engs, rounds - (7 if rounds == 60 else 0))
+        a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, rounds, nthreads=16)
+        for p, e in zip(plans, engs):
+            assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), (p.rank, rounds)
+            assert np.array_equal(e.flows(), f_ref[g.rowptr[p.lo]:g.rowptr[p.hi]]), (p.rank, rounds)
+    for e in engs:
+        e.reset()
+        fu._lib.call("fu_set_option", e._h, b"kernel", 4)
+    run_local(engs, 5)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 5, nthreads=16)
+    for p, e in zip(plans, engs):
+        assert np.array_equal(e.estimates(), a_ref[p.lo:p.hi]), p.rank
+    for e in engs:
+        e.close()
+
+
 def test_dist_exchange_local_checks_round_counts():
     """fu_dist_exchange_local refuses ranks that ran different numbers of rounds, no round,
     or a round whose halo was already exchanged (it would copy into the wrong generation)."""

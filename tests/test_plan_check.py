@@ -125,3 +125,14 @@ def test_autotune_pass_rounds_rank_independent(plan_check):
     instead of failing (CA:74, CA:124). The engine asserts the same count at run time."""
     out = _run(plan_check, ["--tune"])
     assert "4096 rank states, 36 rounds per multi-GPU pass" in out
+
+
+@pytest.mark.parametrize("args", [["--rmat", "12", "16", "3", "--ghosts", "1000"],
+                                  ["--rmat", "14", "16", "3", "--ghosts", "4000", "--ht", "32", "--mega", "256"],
+                                  ["--er", "100000", "400000", "5", "--ghosts", "20000"]])
+def test_rank_view_plans(plan_check, args):
+    """A multi-GPU rank's view (the last ids as ghost estimate slots, na > n): the boundary light
+    tiles lead, the staging slices cover the ghost slots, kernel 9's transposes deliver ghost
+    estimates to their edges (kernels 4, 8 and 9 all run partitioned)."""
+    extra = [] if "--mega" in args else MEGAS
+    _run(plan_check, args + extra + ["--hot", "0", "--hot", "64"])

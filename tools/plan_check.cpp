@@ -57,6 +57,7 @@ std::string g_ctx;
 
 struct Csr {
   int32_t n = 0;
+  int32_t na = 0;  // estimate slots (n + ghosts); 0 = n
   int64_t E = 0;
   std::vector<int64_t> rowptr;
   std::vector<int32_t> col;
@@ -157,7 +158,7 @@ void light_tile_loads(const Csr &g, const FP::Tiles &t, const std::vector<int32_
                 (long long)ci, (long long)c, g.col[ci]);
         }
       }
-      if (q < ne) CHECK(g.col[ci] >= 0 && g.col[ci] < g.n, "gather index");
+      if (q < ne) CHECK(g.col[ci] >= 0 && g.col[ci] < (g.na ? g.na : g.n), "gather index");
     }
     const int64_t fi = q < ne ? e0 + q : 0;
     CHECK(fi < fe, "light tile %zu: flow index %lld", k, (long long)fi);
@@ -483,7 +484,7 @@ void check_k9_tables(const Csr &g, const FP::Graph &pg, const FP::Tiles &t1, con
   std::snprintf(what, sizeof what, "kernel 9 stage (hot %d)", hot);
   const int SN = FP::kStageLds / 8;
   std::vector<int32_t> slice_of;
-  check_stage_blocks(T.brange, T.NB, T.P, SN, g.n, T.total, slice_of, what);  // k_stage reads a_{r-1}[0, n)
+  check_stage_blocks(T.brange, T.NB, T.P, SN, pg.na, T.total, slice_of, what);  // k_stage reads a_{r-1}[0, na)
   CHECK(T.H <= FP::kTrHot && T.H <= g.n, "H %d", T.H);
   CHECK((int64_t)T.offT.size() == (int64_t)(T.B + 1) * T.P && (int64_t)T.hoff.size() == T.B + 1, "offT / hoff sizes");
   std::vector<int64_t> ga_val(T.total, -1);
@@ -492,7 +493,7 @@ void check_k9_tables(const Csr &g, const FP::Graph &pg, const FP::Tiles &t1, con
     CHECK(used >= T.reg[s] && used <= T.reg[s + 1], "slice %d end %lld", s, (long long)used);
     for (int64_t q = T.reg[s]; q < T.reg[s + 1]; ++q) {
       CHECK(slice_of[q] == s, "%s: G_A element %lld not staged by its slice (%d)", what, (long long)q, slice_of[q]);
-      const int64_t cnt = std::min<int64_t>(SN, g.n - (int64_t)s * SN);
+      const int64_t cnt = std::min<int64_t>(SN, pg.na - (int64_t)s * SN);
       CHECK(T.colS[q] < cnt, "%s: element %lld LDS offset %u of %lld", what, (long long)q, T.colS[q], (long long)cnt);
       ga_val[q] = (int64_t)s * SN + T.colS[q];  // the stage writes a_{r-1}[s SN + colS]: here the node id
     }
@@ -518,16 +519,20 @@ void check_k9_tables(const Csr &g, const FP::Graph &pg, const FP::Tiles &t1, con
 }
 
 // ---- one option set ----------------------------------------------------------------------
-void check_all(const Csr &g, int mega, int ht, int hot) {
-  char ctx[96];
-  std::snprintf(ctx, sizeof ctx, "n=%d E=%lld mega=%d ht=%d hot=%d", g.n, (long long)g.E, mega, ht, hot);
+// ghosts > 0: a multi-GPU rank's view: the last `ghosts` node ids become ghost estimate slots
+// (rows [0, n - ghosts) local, na = n), as fu_part.cpp numbers them
+void check_all(const Csr &g, int mega, int ht, int hot, int ghosts = 0) {
+  char ctx[112];
+  std::snprintf(ctx, sizeof ctx, "n=%d E=%lld mega=%d ht=%d hot=%d ghosts=%d", g.n, (long long)g.E, mega, ht, hot,
+                ghosts);
   g_ctx = ctx;
   std::vector<int32_t> blk_row, cbase;
   std::vector<uint16_t> col16;
   FP::build_blocks(g.n, g.E, g.rowptr.data(), g.col.data(), blk_row, cbase, col16);
   check_round0(g, blk_row);
   FP::Graph pg;
-  pg.n = pg.na = g.n;
+  pg.n = g.n;
+  pg.na = g.n + ghosts;
   pg.E = g.E;
   pg.rowptr = g.rowptr.data();
   pg.col = g.col.data();
@@ -568,8 +573,26 @@ void check_all(const Csr &g, int mega, int ht, int hot) {
               check_k9_schedule(g, tg[1], hrows, hb, ko);
             }
     if (wave) check_k9_tables(g, pg, tg[1], hrows, mega, hot, !hb.rows.empty());
+    if (ghosts)  // the boundary light tiles (a ghost neighbour) lead the light ones
+      for (int geo = 0; geo < 4; ++geo)
+        for (size_t k = tg[geo].nheavy; k < tg[geo].all.size(); ++k) {
+          bool gh = false;
+          for (int32_t e = tg[geo].all[k].z; e < tg[geo].all[k].w; ++e) gh |= g.col[e] >= g.n;
+          CHECK(gh == ((int)k < tg[geo].nheavy + tg[geo].nbound), "geometry %d tile %zu: boundary order", geo, k);
+        }
   }
   check_k8(g, pg, ht);
+}
+
+// the rank view of a graph: rows [0, n - ghosts), columns kept (ids >= n - ghosts are ghosts)
+Csr local_view(const Csr &g, int ghosts) {
+  Csr l;
+  l.n = g.n - ghosts;
+  l.na = g.n;
+  l.rowptr.assign(g.rowptr.begin(), g.rowptr.begin() + l.n + 1);
+  l.E = l.rowptr[l.n];
+  l.col.assign(g.col.begin(), g.col.begin() + l.E);
+  return l;
 }
 
 // ---- the autotune pass (--tune) -----------------------------------------------------------
@@ -651,6 +674,7 @@ int main(int argc, char **argv) {
   Csr g;
   std::string layout = "given";
   std::vector<int> megas, hts, hots;
+  int ghosts = 0;
   fu_graph *gh = nullptr;
   for (int a = 1; a < argc; ++a)
     if (!std::strcmp(argv[a], "--tune")) {
@@ -697,6 +721,9 @@ int main(int argc, char **argv) {
     } else if (k == "--hot") {
       need(1);
       hots.push_back(std::atoi(argv[++a]));
+    } else if (k == "--ghosts") {
+      need(1);
+      ghosts = std::atoi(argv[++a]);
     } else {
       std::fprintf(stderr, "plan_check: unknown argument %s\n", k.c_str());
       return 2;
@@ -717,9 +744,14 @@ int main(int argc, char **argv) {
   if (megas.empty()) megas = {8192};
   if (hts.empty()) hts = {128};
   if (hots.empty()) hots = {0};
+  if (ghosts < 0 || ghosts >= g.n) {
+    std::fprintf(stderr, "plan_check: --ghosts must be in [0, n)\n");
+    return 2;
+  }
+  const Csr lv = ghosts ? local_view(g, ghosts) : Csr{};
   for (int mega : megas)
     for (int ht : hts)
-      for (int hot : hots) check_all(g, mega, ht, hot);
+      for (int hot : hots) check_all(ghosts ? lv : g, mega, ht, hot, ghosts);
   if (gh) fu_graph_free(gh);
   std::printf("plan_check: n=%d E=%lld layout=%s: %ld checks, %ld failed\n", g.n, (long long)g.E, layout.c_str(),
               g_checks, g_fail);
