@@ -184,7 +184,7 @@ def round_kernels(kinfo):
     """The launches one round of the selected kernel consists of (the roofline's unit)."""
     k = kinfo["kernel"]
     if k == "recon":
-        return "k_round_recon %dx%d%s" % (kinfo["tile"][0], kinfo["tile"][1], "+nt" if kinfo["nt"] else "")
+        return "k_round_recon %dx%d" % (kinfo["tile"][0], kinfo["tile"][1])
     if k == "stage":
         return "k_stage + k_round_staged 1024x128"
     if k == "pregather":
@@ -249,7 +249,7 @@ def measure_window(eng, g, steps):
     that ran them."""
     wall, dev_ms, b = timed_rounds(eng, steps)
     kinfo = eng.info()
-    kname = kinfo["kernel"] + ("+nt" if kinfo["nt"] else "")
+    kname = kinfo["kernel"]
     phases = [{"rounds": [b[k], b[k + 1]], "us_per_round": dev_ms[k] * 1e3 / max(1, b[k + 1] - b[k])}
               for k in range(len(b) - 1)]
     alg_bytes = 24 * g.E + 28 * g.n

@@ -125,8 +125,6 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "lag"           kernel 9: the multi-row heavy rows leave f_r unwritten and write f_{r-2}
  *                 from f_{r-4} and their kept a_{r-4}, two rounds later (default 1); the
  *                 lagged flows are finalized before fu_get_flows, other kernels and rebuilds.
- * "tr_hot"        kernel 9: neighbours of id < value served from an LDS table in the
- *                 transpose instead of staged (default 0; <= 10240).
  * "iso_rows"      kernel 9: the trailing run of degree-0 rows (the degree layout's last rows)
  *                 runs as one thread per row (k_isolated, 1, default) or as light tiles (0).
  * "multi_short"   kernel 9: the rows of 129-256 edges run in the multi-row blocks too (default 1;
@@ -134,7 +132,6 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "tr_nt"         kernel 9: k_transpose's G_A loads and G_B stores non-temporal (default 1).
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
- * "nt"            kernel 4: non-temporal loads of the streamed column indices (default 0).
  * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster
  *                 (default 1); "pack_every" rounds between encoding plans (default 16).
  * "stage_layout"  kernel 8, tests: -1 = by packing width, 0..3 = the 1/2/4/8-byte layout.
@@ -142,7 +139,9 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 interleaved with them (0; the round-1 order, kept for A/B and tests).
  * Removed after measurement (FU_ERR_ARG): "tr_pipe", "hub_prio", "side_tiles", "split_tr",
  * "hub_cus" / "hub_cu_stride" (the hub path on CU-masked streams: round 5, profiles/r05/b),
- * "st_split" (kernel 8's next stage overlapping this round's tiles: profiles/r05/c)
+ * "st_split" (kernel 8's next stage overlapping this round's tiles: profiles/r05/c), "tr_hot"
+ * (kernel 9's hot-estimate table in the transposes: DESIGN §4.12), "nt" (kernel 4's
+ * non-temporal column loads: DESIGN §4.11)
  * (DESIGN.md §4.12), "hub_multi", "hub_blocks", "fuse", "light_geo". */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */

@@ -45,7 +45,6 @@ using FP::kStageRuns;
 using FP::kStageTE;
 using FP::kStageTN;
 using FP::kTrBE;
-using FP::kTrHot;
 using FP::kTrMaxP;
 
 constexpr int kBlock = 256;      // threads per block (4 waves of 64)
@@ -418,10 +417,6 @@ __device__ __forceinline__ void chain_sum(const double *xs, const double *es, in
   T = __shfl(acc, 1);
 }
 
-template <typename T>
-__device__ inline T ld_stream(const T *p) {
-  return __builtin_nontemporal_load(p);
-}
 
 // Heavy rows (one per wave) up to 64 x max(kHeavyRL, chunk / 64) edges keep their operands
 // in registers (measured on R-MAT-24: 8 or 16 per lane cost more in occupancy than the
@@ -432,7 +427,7 @@ __device__ inline T ld_stream(const T *p) {
 
 // PRE (kernel 9): every edge's estimate a_{r-1}[col e] was pre-gathered into Gb[e] (edge
 // order) by the two staging passes; the tile reads it coalesced instead of col + gather.
-template <bool CHECK, bool NT, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
+template <bool CHECK, int TE = kTileEdges, int TN = kTileNodes, int PART = 0,
           bool PRE = false, int HRL = kHeavyRL, bool RF = true>
 __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_recon(
     const int4 *__restrict__ tiles, const int *__restrict__ rowptr,
@@ -763,7 +758,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
       for (int k = 0; k < kPer; ++k) {
         const int q = t + k * kBlock;
         const int ci = q < ne ? e0 + q : (ne > 0 ? e0 : 0);
-        cw[k] = NT ? ld_stream(col + ci) : col[ci];
+        cw[k] = col[ci];
         bs[k] = 32768;
       }
     }
@@ -1062,12 +1057,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
 // col 4 + one random 8-byte gather).
 // ------------------------------------------------------------------------------------
 constexpr int kTrThreads = 1024;
-// Hot estimates (option tr_hot): the neighbours of id < H (H <= kTrHot; under the degree
-// layout the H highest-degree nodes: R-MAT-24's first 10K take 23 % of all gathers) never
-// pass through the staging launch. Each transpose block keeps a_{r-1}[0, H) in LDS beside
-// its bucket and serves a bucket's hot edges from a per-bucket list {column, position} in
-// edge order: 4 B per hot edge read instead of 2 + 8 staged, 8 + 2 transposed.
-constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 
 // Persistent over its buckets: grid = 8 x (blocks per XCD); XCD x owns the contiguous
 // bucket range [x per, (x + 1) per) and its blocks take every nj-th bucket of it. The next
@@ -1077,18 +1066,13 @@ constexpr int kTrHotS = 4096;  // the small table: 32 KB (tr_hot <= 4096)
 #ifndef FU_TR_WAVES
 #define FU_TR_WAVES 1
 #endif
-template <int HOTN, bool NT = false>  // HOTN: LDS capacity of the hot table (0: none); NT: streamed G_A / G_B non-temporal
+template <bool NT>  // NT: streamed G_A loads / G_B stores non-temporal
 __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
-                                                        double *__restrict__ GB,
-                                                        const double *__restrict__ a_prev, int H,
-                                                        const int *__restrict__ hoff,
-                                                        const unsigned *__restrict__ hlist) {
+                                                        double *__restrict__ GB) {
   __shared__ double s_v[kTrBE];
-  constexpr bool HOT = HOTN > 0;
-  __shared__ double s_hot[HOT ? HOTN : 1];
   __shared__ unsigned short s_m[kTrMaxP + 1];  // first element (bucket order) of each slice's run
   __shared__ int s_o[kTrMaxP];      // G_A index of each run
   __shared__ int s_c[kTrBE / 64 + 1];
@@ -1101,8 +1085,6 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   int bk = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
   const int bend = min((int)(blockIdx.x & 7) * per + per, nbk);
   if (bk >= bend) return;
-  if (HOT)  // a_{r-1} of the hot nodes, once per block (visible after the first table barrier)
-    for (int q = t; q < H; q += kTrThreads) s_hot[q] = a_prev[q];
   // runs: thread t owns slices 2t, 2t + 1
   int o[2], len[2];
   auto load_runs = [&](int bkk, int (&oo)[2], int (&ll)[2]) {
@@ -1185,31 +1167,11 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
     else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
-  unsigned hx[HOT ? 2 : 1];  // the bucket's hot edges: at most 2 per thread in one pass
-  int h0 = 0, h1 = 0;
-  if (HOT) {
-    h0 = hoff[bb];
-    h1 = hoff[bb + 1];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int q = h0 + t + k * kTrThreads;
-      hx[k] = q < h1 ? hlist[q] : 0u;
-    }
-  }
   const int next = bk + nj;
   if (next < bend) load_runs(next, o, len);  // in flight beside this bucket's loads
 #pragma unroll
   for (int k = 0; k < kPerT; ++k)
     if (g[k] >= 0) s_v[pos[k]] = val[k];
-  if (HOT) {
-#pragma unroll
-    for (int k = 0; k < 2; ++k)
-      if (h0 + t + k * kTrThreads < h1) s_v[hx[k] & 0xFFFFu] = s_hot[hx[k] >> 16];
-    for (int q = h0 + t + 2 * kTrThreads; q < h1; q += kTrThreads) {  // buckets of > 2048 hot edges
-      const unsigned x = hlist[q];
-      s_v[x & 0xFFFFu] = s_hot[x >> 16];
-    }
-  }
   __syncthreads();
   for (int q = t; q < ne; q += kTrThreads) {
     if constexpr (NT) __builtin_nontemporal_store(s_v[q], GB + e0 + q);
@@ -2219,13 +2181,11 @@ struct fu_handle {
   int wave_heavy = 1;    // kernel 4: heavy rows one per wave
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
-  int tr_hot = 0;        // kernel 9: neighbours of id < tr_hot (<= kTrHot) served from the transpose's LDS
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
   int c16 = 1;           // kernel 4: narrow light tiles read 2-byte column offsets
   int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
-  int nt = 0;            // non-temporal loads of the streamed arrays (kernel 4)
   bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
   bool tuned = false;
   bool tuning = false;     // inside an autotune pass: packing plans wait until it ends
@@ -2306,9 +2266,6 @@ struct fu_handle {
     unsigned short *pos16 = nullptr;      // per G_A element: position in its bucket
     int *offT = nullptr;                  // (B + 1) x P: G_A index where bucket b's run of slice s starts
     double *GA = nullptr;
-    int H = 0;                            // hot neighbours: id < H (tr_hot), served from LDS
-    int *hoff = nullptr;                  // B + 1: per bucket, its range of hlist
-    unsigned *hlist = nullptr;            // per hot edge: column << 16 | position in its bucket
     double *GBr[3] = {nullptr, nullptr, nullptr};  // G_B of round r in GBr[r % 3] (one buffer without lag)
     double *hist[2] = {nullptr, nullptr};          // lag: per parity, a_{r-2} of every lagged row
   };
@@ -2513,7 +2470,7 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
 void free_transpose(fu_handle *h) {
   auto &T = h->tr;
   for (void *p : {(void *)T.brange, (void *)T.colS, (void *)T.pos16, (void *)T.offT, (void *)T.GA,
-                  (void *)T.GBr[0], (void *)T.hist[0], (void *)T.hist[1], (void *)T.hoff, (void *)T.hlist})
+                  (void *)T.GBr[0], (void *)T.hist[0], (void *)T.hist[1]})
     if (p) hipFree(p);
   if (T.GBr[1] != T.GBr[0]) hipFree(T.GBr[1]);
   if (T.GBr[2] != T.GBr[0]) hipFree(T.GBr[2]);
@@ -2527,7 +2484,7 @@ int ensure_transpose(fu_handle *h) {
   FP::TransPlan tp;
   std::string why;
   const int32_t *mrows = h->h_hrows.empty() ? nullptr : h->h_hrows.data() + h->multi_geo[1][0];
-  if (!FP::build_transpose(plan_graph(h), h->mega_hub, h->tr_hot, h->n_cu, mrows, h->multi_geo[1][1], tp, &why)) {
+  if (!FP::build_transpose(plan_graph(h), h->mega_hub, h->n_cu, mrows, h->multi_geo[1][1], tp, &why)) {
     h->tr_why = why;
     return fail(FU_ERR_GRAPH, why);
   }
@@ -2536,8 +2493,6 @@ int ensure_transpose(fu_handle *h) {
   if (int rc = upload(&T.colS, tp.colS)) return rc;
   if (int rc = upload(&T.pos16, tp.pos)) return rc;
   if (int rc = upload(&T.offT, tp.offT)) return rc;
-  if (int rc = upload(&T.hoff, tp.hoff)) return rc;
-  if (int rc = upload(&T.hlist, tp.hlist)) return rc;
   if (int rc = dmalloc(&T.GA, (size_t)tp.total)) return rc;
   // G_B: a ring of three with lag (round r reads G_B of round r - 2 for the lagged rows)
   for (int k = 0; k < 3; ++k) {
@@ -2549,7 +2504,6 @@ int ensure_transpose(fu_handle *h) {
   }
   for (int p = 0; p < 2; ++p)
     if (int rc = dmalloc(&T.hist[p], (size_t)(h->multi_geo[1][1] + 1))) return rc;
-  T.H = tp.H;
   T.P = tp.P;
   T.Q = tp.Q;
   T.NB = tp.NB;
@@ -2635,7 +2589,7 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   }
   plan_alone(h, c);
   auto heavy = [&](auto chk) {
-    hipLaunchKernelGGL((k_round_recon<decltype(chk)::value, false, kStageTE, kStageTN>), dim3(h->st_nheavy),
+    hipLaunchKernelGGL((k_round_recon<decltype(chk)::value, kStageTE, kStageTN>), dim3(h->st_nheavy),
                        dim3(kBlock), 0, h->stream, h->st_heavy, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an,
                        h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr, c.fm);
   };
@@ -2725,18 +2679,12 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   plan_alone(h, c);
   const int bh = hubs ? h->tr.Bh : 0;
   auto tr_launch = [&](int b0, int nb) {
-    if (h->tr.H > kTrHotS)  // 80 KB table: the whole LDS of a CU with the bucket's
-      hipLaunchKernelGGL(k_transpose<kTrHot>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
-    else if (h->tr.H)  // 32 KB table: room for a hub chain block beside it
-      hipLaunchKernelGGL(k_transpose<kTrHotS>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, c.ap, h->tr.H, h->tr.hoff, h->tr.hlist);
-    else if (h->tr_nt)
-      hipLaunchKernelGGL((k_transpose<0, true>), dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
+    if (h->tr_nt)
+      hipLaunchKernelGGL(k_transpose<true>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb);
     else
-      hipLaunchKernelGGL(k_transpose<0>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
-                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb, nullptr, 0, nullptr, nullptr);
+      hipLaunchKernelGGL(k_transpose<false>, dim3(tr_grid(h, nb)), dim3(kTrThreads), 0, h->stream, b0, nb, h->tr.P,
+                         (long long)h->E, h->tr.offT, h->tr.GA, h->tr.pos16, Gb);
   };
   if (bh) tr_launch(0, bh);
   if (hubs) {
@@ -2747,7 +2695,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   const bool chk = c.err != nullptr;
   if (hubs) {
     auto chains = [&](auto C) {
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, 1024, 128, 2, true>), dim3(nmega), dim3(kBlock),
                          0, h->stream2, tl, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, h->hrows, 1, Gb, c.fm);
     };
@@ -2761,7 +2709,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   // heavy tiles [t0, t1) with RL register elements per lane
   auto heavy = [&](auto C, auto RL, int t0, int t1) {
     if (t1 > t0)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 2, true, decltype(RL)::value>),
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, 1024, 128, 2, true, decltype(RL)::value>),
                          dim3(t1 - t0), dim3(kBlock), 0, h->stream, tl + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, h->hubxy, h->hub_off, h->hrows, 1, Gb,
                          c.fm);
@@ -2793,7 +2741,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
                          h->iso0_geo[1], h->n, h->v, c.an, h->target, c.err, h->code[r1], h->pctl, r1,
                          decltype(C)::value ? 1 : 0);
     if (nl)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, 1024, 128, 1, true>), dim3(nl), dim3(kBlock), 0,
                          h->stream, tl + nh, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp,
                          h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, Gb, c.fm);
   };
@@ -2839,37 +2787,37 @@ int launch_k4_geo(fu_handle *h, RoundCtx &c) {
                        (long long)h->hub_total, h->col, c.F, c.ap, c.ap2, cp, h->pctl, r1, h->hubxy, c.fm, h->hub_blk);
   auto heavy = [&](auto C, hipStream_t st, int t0, int cnt) {
     if (cnt)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, false, TE, TN, 2>), dim3(cnt), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, TE, TN, 2>), dim3(cnt), dim3(kBlock), 0, st,
                          tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2, c.an, h->target, c.err, cp, h->code[r1],
                          h->pctl, r1, h->hubxy, h->hub_off, h->hrows, hub_sep, nullptr, c.fm);
   };
   // light tiles: rounds 1 and 2 (fm) read no flows (RF = false)
-  auto light = [&](auto C, auto NT, auto RF, int t0, int cnt) {
+  auto light = [&](auto C, auto RF, int t0, int cnt) {
     if (cnt)
-      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, decltype(NT)::value, TE, TN, 1, false, kHeavyRL,
+      hipLaunchKernelGGL((k_round_recon<decltype(C)::value, TE, TN, 1, false, kHeavyRL,
                                         decltype(RF)::value>),
                          dim3(cnt), dim3(kBlock), 0, h->stream, tiles + t0, h->rowptr, h->col, h->v, c.F, c.ap, c.ap2,
                          c.an, h->target, c.err, cp, h->code[r1], h->pctl, r1, nullptr, nullptr, nullptr, 0, nullptr,
                          c.fm, h->col16, h->cbase, h->c16 ? h->tnar_geo[h->geo] + t0 : nullptr);
   };
-  auto light_rf = [&](auto C, auto NT, int t0, int cnt) {
-    if (c.fm) light(C, NT, std::false_type{}, t0, cnt);
-    else light(C, NT, std::true_type{}, t0, cnt);
+  auto light_rf = [&](auto C, int t0, int cnt) {
+    if (c.fm) light(C, std::false_type{}, t0, cnt);
+    else light(C, std::true_type{}, t0, cnt);
   };
-  auto body = [&](auto C, auto NT) -> int {
+  auto body = [&](auto C) -> int {
     heavy(C, hs, 0, nmh);             // mega hubs (or every heavy tile) on the side stream
     heavy(C, h->stream, nmh, nh - nmh);  // the other heavy tiles ahead of the light ones
-    light_rf(C, NT, nh, nb);
+    light_rf(C, nh, nb);
     if (h->dist) {  // boundary rows done: their estimates go out beside the interior tiles
       h->halo_a = c.an;
       if (int rc = fu__dist_round_hook(h, 2)) return rc;
     }
-    light_rf(C, NT, nh + nb, nl - nb);
+    light_rf(C, nh + nb, nl - nb);
     return FU_OK;
   };
   int rc;
-  if (c.err) rc = h->nt ? body(std::true_type{}, std::true_type{}) : body(std::true_type{}, std::false_type{});
-  else rc = h->nt ? body(std::false_type{}, std::true_type{}) : body(std::false_type{}, std::false_type{});
+  if (c.err) rc = body(std::true_type{});
+  else rc = body(std::false_type{});
   if (rc) return rc;
   if (hub_sep)
     hipLaunchKernelGGL(k_hub_flows, dim3(grid_for(h->hub_total)), dim3(kBlock), 0, hs, h->n_hub, h->hub_rows,
@@ -3155,10 +3103,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->st_force = (int)value;
     return FU_OK;
   }
-  if (!std::strcmp(key, "nt")) {
-    h->nt = value != 0;
-    return FU_OK;
-  }
   if (!std::strcmp(key, "pack")) {
     h->pack = value != 0;
     if (!h->pack) {  // stop encoding (and drop a plan still due)
@@ -3194,15 +3138,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
     h->staged_lo = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "tr_hot")) {  // kernel 9: neighbours of id < value served from LDS (0: none)
-    if (value < 0 || value > kTrHot) return fail(FU_ERR_ARG, "fu_set_option: tr_hot must be in [0, 10240]");
-    if (value != h->tr_hot) {
-      if (int rc = lag_finalize_all(h)) return rc;
-      free_transpose(h);  // the staging layout leaves the hot neighbours out
-    }
-    h->tr_hot = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_bpx")) {  // kernel 9: transpose blocks per XCD (0 = one per bucket)
@@ -3610,7 +3545,7 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
   if (!h || !info) return fail(FU_ERR_ARG, "fu_get_info: NULL argument");
   for (int k = 0; k < 32; ++k) info[k] = 0;
   info[0] = h->kernel;
-  info[1] = h->nt;
+  info[1] = 0;  // (reserved: kernel 4's removed "nt" option)
   info[2] = h->autotune ? (h->tuned ? 2 : 1) : 0;
   info[3] = h->rounds;
   info[4] = kGeoEdges[h->geo];

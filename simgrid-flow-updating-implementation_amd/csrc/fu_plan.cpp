@@ -293,10 +293,10 @@ int build_stage_layouts(const Graph &g, const std::vector<I4> &light, int n_cu, 
 // of 16 (the stage launch stores 16 bytes per lane); offT[b * P + s] = where bucket b's run of
 // slice s starts (offT[B * P + s]: the end of slice s's elements); stage blocks cut each
 // slice's region into pieces of about equal element count.
-bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const int32_t *multi_rows, int n_multi_rows,
+bool build_transpose(const Graph &g, int mega_hub, int n_cu, const int32_t *multi_rows, int n_multi_rows,
                      TransPlan &out, std::string *why) {
   out = TransPlan{};
-  const int64_t n = g.n, E = g.E;
+  const int64_t E = g.E;
   const int64_t SN = kStageLds / 8;
   const int64_t P = ((int64_t)g.na + SN - 1) / SN;  // multi-GPU: the ghost slots are slices too
   if (E == 0 || P > kTrMaxP) {
@@ -308,11 +308,8 @@ bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const i
   int64_t hub_end = 0;
   for (int32_t i = 0; i < g.n; ++i)
     if (g.deg(i) > mega_hub) hub_end = g.rowptr[i + 1];
-  // hot neighbours (id < H) bypass the staging launch (k_transpose<HOTN>)
-  const int32_t H = (int32_t)std::min<int64_t>(tr_hot, std::min<int64_t>(n, kTrHot));
   std::vector<int64_t> cnt(P, 0);
-  for (int64_t e = 0; e < E; ++e)
-    if (g.col[e] >= H) cnt[g.col[e] / SN]++;
+  for (int64_t e = 0; e < E; ++e) cnt[g.col[e] / SN]++;
   out.reg.assign(P + 1, 0);
   for (int64_t s2 = 0; s2 < P; ++s2) out.reg[s2 + 1] = out.reg[s2] + (cnt[s2] + 15) / 16 * 16;
   const int64_t total = out.reg[P];
@@ -324,23 +321,16 @@ bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const i
   out.pos.assign(total, 0);
   out.offT.assign((size_t)(B + 1) * P, 0);
   std::vector<int64_t> cur(out.reg.begin(), out.reg.end() - 1);
-  out.hoff.assign(B + 1, 0);
   for (int64_t b = 0; b < B; ++b) {
     for (int64_t s2 = 0; s2 < P; ++s2) out.offT[(size_t)b * P + s2] = (int32_t)cur[s2];
-    out.hoff[b] = (int32_t)out.hlist.size();
     const int64_t e1 = std::min<int64_t>(E, (b + 1) * kTrBE);
     for (int64_t e = b * kTrBE; e < e1; ++e) {
       const int32_t c = g.col[e];
-      if (c < H) {  // {column, position in the bucket}, edge order
-        out.hlist.push_back(((uint32_t)c << 16) | (uint32_t)(e - b * kTrBE));
-        continue;
-      }
       const int64_t gi = cur[c / SN]++;
       out.colS[gi] = (uint16_t)(c % SN);
       out.pos[gi] = (uint16_t)(e - b * kTrBE);
     }
   }
-  out.hoff[B] = (int32_t)out.hlist.size();
   for (int64_t s2 = 0; s2 < P; ++s2) out.offT[(size_t)B * P + s2] = (int32_t)cur[s2];
   // stage pieces by element count, not per slice: under the degree layout the hottest slice
   // holds ~40% of all elements (R-MAT-24), so a slice gets as many blocks as its share
@@ -353,7 +343,6 @@ bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const i
   out.Q = (int)((int64_t)out.brange.size() / P);
   out.NB = (int)out.brange.size();
   out.B = (int)B;
-  out.H = H;
   out.total = total;
   out.Bh = (int)((hub_end + kTrBE - 1) / kTrBE);
   // the multi-row heavy rows of geometry 1 (contiguous after the hubs under the degree layout)

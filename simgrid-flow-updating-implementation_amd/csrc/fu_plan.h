@@ -36,7 +36,6 @@ constexpr int kStageMaxP = 512;                  // slices per kernel 8 layout
 constexpr int kTrBE = FU_TR_BE;                  // kernel 9: edges per transpose bucket
 static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 positions, coarse table");
 constexpr int kTrMaxP = 2048;                    // kernel 9: slices of 16K nodes (n <= 2^25)
-constexpr int kTrHot = 10240;                    // kernel 9: hot table capacity (tr_hot)
 #ifndef FU_HEAVY_RL
 #define FU_HEAVY_RL 4
 #endif
@@ -113,18 +112,16 @@ int build_stage_layouts(const Graph &g, const std::vector<I4> &light, int n_cu, 
 
 // Kernel 9 (pregather): slices of kStageLds / 8 nodes, buckets of kTrBE edges.
 struct TransPlan {
-  int P = 0, Q = 0, NB = 0, B = 0, Bh = 0, Bm = 0, H = 0;
+  int P = 0, Q = 0, NB = 0, B = 0, Bh = 0, Bm = 0;
   int64_t total = 0;              // G_A elements (each slice's region padded to 16)
   std::vector<int64_t> reg;       // P + 1: slice regions in G_A
   std::vector<I4> brange;         // stage blocks: {begin, end} in G_A, slice, 0
   std::vector<uint16_t> colS;     // per G_A element: column offset in its slice
   std::vector<uint16_t> pos;      // per G_A element: position in its bucket
   std::vector<int32_t> offT;      // (B + 1) x P: G_A index where bucket b's run of slice s starts
-  std::vector<int32_t> hoff;      // B + 1: per bucket, its range of hlist
-  std::vector<uint32_t> hlist;    // per hot edge: column << 16 | position in its bucket
 };
 // multi_rows: the k_heavy_multi rows of geometry 1 (hrows + multi[0], multi[1] of them).
-bool build_transpose(const Graph &g, int mega_hub, int tr_hot, int n_cu, const int32_t *multi_rows, int n_multi_rows,
+bool build_transpose(const Graph &g, int mega_hub, int n_cu, const int32_t *multi_rows, int n_multi_rows,
                      TransPlan &out, std::string *why);
 
 // Which launch of a kernel-9 round computes which rows (launch_k9): mega-hub chains

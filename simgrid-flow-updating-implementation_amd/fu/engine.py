@@ -26,7 +26,7 @@ def handle_info(h) -> dict:
     a = np.zeros(32, dtype=np.int64)
     L.call("fu_get_info", h, L.ptr(a))
     names = {4: "recon", 8: "stage", 9: "pregather"}
-    return {"kernel": names.get(int(a[0]), int(a[0])), "nt": int(a[1]),
+    return {"kernel": names.get(int(a[0]), int(a[0])),
             "autotune": ["off", "pending", "done"][int(a[2])], "rounds": int(a[3]),
             "tile": (int(a[4]), int(a[5])), "tune_passes": int(a[6]),
             "tuned_pack_width": int(a[7]), "mega_hubs": int(a[20]),

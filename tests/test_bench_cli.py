@@ -191,7 +191,7 @@ class _FakeEngine:
         return (self.marks[b] - self.marks[a]) * 0.05
 
     def info(self):
-        return {"kernel": "stage", "nt": 0, "tile": (1024, 128), "tune_passes": 1,
+        return {"kernel": "stage", "tile": (1024, 128), "tune_passes": 1,
                 "tune_us_per_round": {"stage": 50.0}, "tune_winner_by_width": {0: "stage"}}
 
     def close(self):

@@ -142,7 +142,7 @@ def test_option_errors():
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse",
-                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride", "st_split"):
+                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride", "st_split", "tr_hot", "nt"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
     for key, val in (("tr_nt", 2), ("tr_nt", -1)):
@@ -665,8 +665,7 @@ def test_pregather_heavy_rows_and_mega_hubs_bitwise(mega):
     assert np.array_equal(eng.flows(), f_ref)
 
 
-@pytest.mark.parametrize("multi", [1, 0, "mid0", "nolag", "hot", "hot_nolag", "hot4k", "iso0", "short0",
-                                   "short_nolag", "trnt0"])
+@pytest.mark.parametrize("multi", [1, 0, "mid0", "nolag", "iso0", "short0", "short_nolag", "trnt0", "bpx3"])
 @pytest.mark.parametrize("ht,mega", [(16, 8192), (4, 700), (64, 100000)])
 def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
     """Kernel 9's heavy rows of more than 256 edges as k_heavy_multi blocks (16 rows per
@@ -683,13 +682,8 @@ def test_pregather_multi_row_chains_bitwise(multi, ht, mega):
         eng.set_option("multi_mid", 0)
     elif multi == "nolag":  # the two-pass heavy rows (lag is the default)
         eng.set_option("lag", 0)
-    elif multi == "hot":  # neighbours of id < 10240 served from the transpose's LDS
-        eng.set_option("tr_hot", 10240)
-    elif multi == "hot_nolag":
-        eng.set_option("tr_hot", 3000)
-        eng.set_option("lag", 0)
-    elif multi == "hot4k":  # the small (32 KB) hot table
-        eng.set_option("tr_hot", 4096)
+    elif multi == "bpx3":  # three transpose blocks per XCD, each looping over many buckets
+        eng.set_option("tr_bpx", 3)
     elif multi == "iso0":  # the trailing isolated rows as light tiles (k_isolated is the default)
         eng.set_option("iso_rows", 0)
     elif multi == "trnt0":  # plain G_A loads / G_B stores in the transposes (tr_nt is the default)
@@ -1010,7 +1004,7 @@ def test_lag_flows_every_round_and_switches():
         assert np.array_equal(eng.estimates(), a_ref), r
         assert np.array_equal(eng.flows(), f_ref), r
     eng.run(5)
-    eng.set_option("tr_hot", 500)  # the staging layout is rebuilt: the lagged flows are written first
+    eng.set_option("mega_hub", 700)  # tiles and staging layout rebuilt: the lagged flows are written first
     eng.run(4)
     eng.set_option("lag", 0)
     eng.run(3)
@@ -1091,7 +1085,7 @@ def _isolated_then_heavy_graph(tail):
 
 
 @pytest.mark.parametrize("tail", ["heavy_hub", "hub_iso_heavy", "iso_end"])
-@pytest.mark.parametrize("opts", [{}, {"lag": 0}, {"iso_rows": 0}, {"tr_hot": 64}])
+@pytest.mark.parametrize("opts", [{}, {"lag": 0}, {"iso_rows": 0}, {"multi_short": 0}])
 def test_isolated_rows_before_heavy_rows_given_layout_bitwise(tail, opts):
     """Kernel 9's k_isolated must not cover a heavy row or a mega hub that follows the
     trailing run of edge-less light tiles (layout "given", CollectAll's default): every row
@@ -1114,8 +1108,8 @@ def test_isolated_rows_before_heavy_rows_given_layout_bitwise(tail, opts):
 @pytest.mark.parametrize("layout", ["given", "degree"])
 @pytest.mark.parametrize("kernel,opts", [("recon", {}), ("recon", {"wave_heavy": 0}), ("stage", {}),
                                          ("pregather", {}), ("pregather", {"lag": 0}),
-                                         ("pregather", {"multi_mid": 0, "tr_hot": 64}),
-                                         ("pregather", {"iso_rows": 0}), ("pregather", {"tr_hot": 4096, "lag": 0}),
+                                         ("pregather", {"multi_mid": 0}),
+                                         ("pregather", {"iso_rows": 0}), ("pregather", {"tr_nt": 0, "lag": 0}),
                                          ("pregather", {"multi_short": 0}),
                                          ("pregather", {"multi_short": 1, "multi_heavy": 0})])
 def test_row_class_boundaries_bitwise(kernel, opts, layout):

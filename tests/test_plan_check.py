@@ -5,7 +5,7 @@ and UndefinedBehaviorSanitizer. No GPU: this runs in the CPU suite.
 
 Covers every golden fixture graph (CA:105-128 on those graphs is pinned bitwise by the GPU
 suite) and R-MAT scales 9-15, both node numberings, mega-hub thresholds 64 / 300 / 8192, the
-forced heavy path and the hot-estimate tables: each table index in range, each row computed
+forced heavy path and a rank's view with ghost slots: each table index in range, each row computed
 by exactly one launch, each flow written once, each edge's pre-gathered estimate its own
 neighbour's."""
 import os
@@ -49,21 +49,20 @@ def test_fixture_graph_plans(plan_check, tmp_path, name, meta, layout):
     d = load_npz(meta["file"])
     f = str(tmp_path / "g.bin")
     _write_csr(f, d["rowptr"], d["col"])
-    _run(plan_check, ["--csr", f, "--layout", layout, "--ht", "128", "--ht", "3", "--hot", "0", "--hot", "64"]
+    _run(plan_check, ["--csr", f, "--layout", layout, "--ht", "128", "--ht", "3"]
          + MEGAS)
 
 
 @pytest.mark.parametrize("layout", ["given", "degree"])
 @pytest.mark.parametrize("scale,ef", [(9, 8), (10, 16), (11, 16), (12, 16), (13, 16), (14, 16), (15, 16)])
 def test_rmat_plans(plan_check, scale, ef, layout):
-    hots = ["--hot", "0", "--hot", "4096"] if scale >= 14 else ["--hot", "0", "--hot", "64", "--hot", "10240"]
     hts = ["--ht", "128"] if scale >= 14 else ["--ht", "128", "--ht", "16"]
-    _run(plan_check, ["--rmat", str(scale), str(ef), str(scale), "--layout", layout] + MEGAS + hots + hts)
+    _run(plan_check, ["--rmat", str(scale), str(ef), str(scale), "--layout", layout] + MEGAS + hts)
 
 
 def test_er_plans(plan_check):
     """ER with > 64 slices per kernel 8 layout width (kernel 8 then builds only some layouts)."""
-    _run(plan_check, ["--er", "200000", "800000", "5", "--hot", "0", "--hot", "10240"])
+    _run(plan_check, ["--er", "200000", "800000", "5"])
 
 
 def _edges_graph(n, src, dst):
@@ -114,7 +113,7 @@ def test_tiny_graph_plans(plan_check, tmp_path, case):
     f = str(tmp_path / "g.bin")
     _write_csr(f, rp, col)
     for layout in ("given", "degree"):
-        _run(plan_check, ["--csr", f, "--layout", layout, "--ht", "128", "--ht", "3", "--hot", "0", "--hot", "64"]
+        _run(plan_check, ["--csr", f, "--layout", layout, "--ht", "128", "--ht", "3"]
              + MEGAS)
 
 
@@ -135,4 +134,4 @@ def test_rank_view_plans(plan_check, args):
     tiles lead, the staging slices cover the ghost slots, kernel 9's transposes deliver ghost
     estimates to their edges (kernels 4, 8 and 9 all run partitioned)."""
     extra = [] if "--mega" in args else MEGAS
-    _run(plan_check, args + extra + ["--hot", "0", "--hot", "64"])
+    _run(plan_check, args + extra)

@@ -15,14 +15,14 @@
 //     tiles' u16 {position, run} and run offsets: every edge's staged element is its neighbour;
 //   * kernel 9: the staging launch (as kernel 8), every transpose bucket through the block's
 //     own run scan / coarse table / binary search (u16 run starts, nst <= kTrBE), positions
-//     written exactly once (staged and hot edges), the transposed value of edge e equal to
+//     written exactly once, the transposed value of edge e equal to
 //     col[e] for every e (values = node ids), every bucket visited once per grid (tr_bpx);
 //     the launch partition of a round (FP::k9_schedule) for every option combination: each row
 //     computed once, each flow written once, k_heavy_multi's rows and history slots in range;
 //   * the mega-hub tables: every hub edge's thread finds its hub.
 //
 //   plan_check --csr FILE | --rmat SCALE EF SEED | --er N M SEED
-//              [--layout given|degree] [--mega M]... [--ht T]... [--hot H]...
+//              [--layout given|degree] [--mega M]... [--ht T]... [--ghosts K]
 // FILE: int64 n, int64 E, int64 rowptr[n + 1], int32 col[E]. Exit 0 = every check passed.
 #include <cstdio>
 #include <cstdlib>
@@ -66,7 +66,6 @@ struct Csr {
 
 constexpr int kBlock = 256;
 constexpr int kTrThreads = 1024;
-constexpr int kTrHotS = 4096;
 
 int64_t fe_of(int64_t E) { return std::max<int64_t>(32, (E + 31) / 32 * 32); }  // split-word flow slots
 
@@ -452,19 +451,6 @@ void run_transpose(const Csr &g, const FP::TransPlan &T, const std::vector<int64
         s_v[pos] = ga_val[gi];
         s_hit[pos]++;
       }
-      if (T.H) {
-        CHECK((size_t)bb + 1 < T.hoff.size(), "hoff index");
-        const int h0 = T.hoff[bb], h1 = T.hoff[bb + 1];
-        CHECK(h0 <= h1 && h1 <= (int)T.hlist.size(), "bucket %d hot list [%d, %d)", bb, h0, h1);
-        for (int q = h0; q < h1; ++q) {
-          const uint32_t x = T.hlist[q];
-          const int pos = (int)(x & 0xFFFFu), c = (int)(x >> 16);
-          CHECK(pos < ne && c < T.H && c < (T.H > kTrHotS ? FP::kTrHot : kTrHotS), "bucket %d hot entry %u", bb, x);
-          if (pos >= ne) continue;
-          s_v[pos] = c;  // s_hot[c] = a_{r-1}[c]: the node id here
-          s_hit[pos]++;
-        }
-      }
       for (int q = 0; q < ne; ++q) {
         CHECK(s_hit[q] == 1, "bucket %d position %d written %d times", bb, q, s_hit[q]);
         CHECK(e0 + q < g.E, "G_B store %lld", (long long)(e0 + q));
@@ -475,18 +461,16 @@ void run_transpose(const Csr &g, const FP::TransPlan &T, const std::vector<int64
 }
 
 void check_k9_tables(const Csr &g, const FP::Graph &pg, const FP::Tiles &t1, const std::vector<int32_t> &hrows,
-                     int mega, int hot, bool hubs) {
+                     int mega, bool hubs) {
   FP::TransPlan T;
   std::string why;
   const int32_t *mrows = hrows.empty() ? nullptr : hrows.data() + t1.multi[0];
-  if (!FP::build_transpose(pg, mega, hot, 256, mrows, t1.multi[1], T, &why)) return;  // kernel 9 unavailable
-  char what[64];
-  std::snprintf(what, sizeof what, "kernel 9 stage (hot %d)", hot);
+  if (!FP::build_transpose(pg, mega, 256, mrows, t1.multi[1], T, &why)) return;  // kernel 9 unavailable
+  const char *what = "kernel 9 stage";
   const int SN = FP::kStageLds / 8;
   std::vector<int32_t> slice_of;
   check_stage_blocks(T.brange, T.NB, T.P, SN, pg.na, T.total, slice_of, what);  // k_stage reads a_{r-1}[0, na)
-  CHECK(T.H <= FP::kTrHot && T.H <= g.n, "H %d", T.H);
-  CHECK((int64_t)T.offT.size() == (int64_t)(T.B + 1) * T.P && (int64_t)T.hoff.size() == T.B + 1, "offT / hoff sizes");
+  CHECK((int64_t)T.offT.size() == (int64_t)(T.B + 1) * T.P, "offT size");
   std::vector<int64_t> ga_val(T.total, -1);
   for (int s = 0; s < T.P; ++s) {
     const int64_t used = T.offT[(size_t)T.B * T.P + s];  // end of slice s's elements
@@ -521,10 +505,9 @@ void check_k9_tables(const Csr &g, const FP::Graph &pg, const FP::Tiles &t1, con
 // ---- one option set ----------------------------------------------------------------------
 // ghosts > 0: a multi-GPU rank's view: the last `ghosts` node ids become ghost estimate slots
 // (rows [0, n - ghosts) local, na = n), as fu_part.cpp numbers them
-void check_all(const Csr &g, int mega, int ht, int hot, int ghosts = 0) {
+void check_all(const Csr &g, int mega, int ht, int ghosts = 0) {
   char ctx[112];
-  std::snprintf(ctx, sizeof ctx, "n=%d E=%lld mega=%d ht=%d hot=%d ghosts=%d", g.n, (long long)g.E, mega, ht, hot,
-                ghosts);
+  std::snprintf(ctx, sizeof ctx, "n=%d E=%lld mega=%d ht=%d ghosts=%d", g.n, (long long)g.E, mega, ht, ghosts);
   g_ctx = ctx;
   std::vector<int32_t> blk_row, cbase;
   std::vector<uint16_t> col16;
@@ -572,7 +555,7 @@ void check_all(const Csr &g, int mega, int ht, int hot, int ghosts = 0) {
               ko.iso_rows = iso;
               check_k9_schedule(g, tg[1], hrows, hb, ko);
             }
-    if (wave) check_k9_tables(g, pg, tg[1], hrows, mega, hot, !hb.rows.empty());
+    if (wave) check_k9_tables(g, pg, tg[1], hrows, mega, !hb.rows.empty());
     if (ghosts)  // the boundary light tiles (a ghost neighbour) lead the light ones
       for (int geo = 0; geo < 4; ++geo)
         for (size_t k = tg[geo].nheavy; k < tg[geo].all.size(); ++k) {
@@ -673,7 +656,7 @@ bool from_handle(fu_graph *h, Csr &g) {
 int main(int argc, char **argv) {
   Csr g;
   std::string layout = "given";
-  std::vector<int> megas, hts, hots;
+  std::vector<int> megas, hts;
   int ghosts = 0;
   fu_graph *gh = nullptr;
   for (int a = 1; a < argc; ++a)
@@ -718,9 +701,6 @@ int main(int argc, char **argv) {
     } else if (k == "--ht") {
       need(1);
       hts.push_back(std::atoi(argv[++a]));
-    } else if (k == "--hot") {
-      need(1);
-      hots.push_back(std::atoi(argv[++a]));
     } else if (k == "--ghosts") {
       need(1);
       ghosts = std::atoi(argv[++a]);
@@ -743,15 +723,13 @@ int main(int argc, char **argv) {
   }
   if (megas.empty()) megas = {8192};
   if (hts.empty()) hts = {128};
-  if (hots.empty()) hots = {0};
   if (ghosts < 0 || ghosts >= g.n) {
     std::fprintf(stderr, "plan_check: --ghosts must be in [0, n)\n");
     return 2;
   }
   const Csr lv = ghosts ? local_view(g, ghosts) : Csr{};
   for (int mega : megas)
-    for (int ht : hts)
-      for (int hot : hots) check_all(ghosts ? lv : g, mega, ht, hot, ghosts);
+    for (int ht : hts) check_all(ghosts ? lv : g, mega, ht, ghosts);
   if (gh) fu_graph_free(gh);
   std::printf("plan_check: n=%d E=%lld layout=%s: %ld checks, %ld failed\n", g.n, (long long)g.E, layout.c_str(),
               g_checks, g_fail);

@@ -15,7 +15,6 @@ ap.add_argument("--spec", default="er:n=1000000,m=4000000")
 ap.add_argument("--kernel", default="auto")
 ap.add_argument("--warm", type=int, default=20)
 ap.add_argument("--rounds", type=int, default=1000)
-ap.add_argument("--nt", type=int, default=-1)
 ap.add_argument("--pack", type=int, default=1)
 ap.add_argument("--tile", type=int, default=0, help="kernel 4 tile edges (2048/1024/512); 0 = default")
 ap.add_argument("--layout", default="given")
@@ -53,8 +52,6 @@ if a.pairwise:
 g = fu.Graph.from_spec(a.spec, seed=1)
 v = fu.uniform_values(g.n, seed=0)
 eng = fu.CollectAll(g, v, kernel=a.kernel, layout=a.layout)
-if a.nt >= 0:
-    eng.set_option("nt", a.nt)
 eng.set_option("pack", a.pack)
 if a.tile:
     eng.set_option("tile_edges", a.tile)

@@ -18,7 +18,6 @@ VARIANTS = {
     "recon_1024_c16off": ("recon", {"tile_edges": 1024, "c16": 0}),
     "recon_1024x256": ("recon", {"tile_edges": 1024, "tile_nodes": 256}),
     "recon_512": ("recon", {"tile_edges": 512}),
-    "recon_nt": ("recon", {"nt": 1}),
     "recon_nopack": ("recon", {"pack": 0}),
     "recon_1024_nopack": ("recon", {"tile_edges": 1024, "pack": 0}),
     "recon_nofork": ("recon", {"fork_heavy": 0}),
@@ -31,10 +30,6 @@ VARIANTS = {
     "pre_multi0": ("pregather", {"layout": "degree", "pack": 0, "multi_heavy": 0}),
     "pre_multimid0": ("pregather", {"layout": "degree", "pack": 0, "multi_mid": 0}),
     "pre_lag": ("pregather", {"layout": "degree", "pack": 0, "lag": 1}),
-    "pre_hot": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240}),
-    "pre_hot_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 10240, "lag": 1}),
-    "pre_hot4k_lag": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096, "lag": 1}),
-    "pre_hot4k": ("pregather", {"layout": "degree", "pack": 0, "tr_hot": 4096}),
     "pre_iso0": ("pregather", {"layout": "degree", "pack": 0, "iso_rows": 0}),
     "pre_short": ("pregather", {"layout": "degree", "pack": 0, "multi_short": 1}),
     "pre_trnt": ("pregather", {"layout": "degree", "pack": 0, "tr_nt": 1}),
