@@ -303,14 +303,30 @@ def test_dist_ghost_slots_local_transport_bitwise(world, kind, kernel):
         e.close()
 
 
-def test_dist_refuses_kernel_9():
-    from fu.dist import DistCollectAll, partition
+def test_dist_autotune_never_runs_kernel_9():
+    """Kernel 9 runs on partitioned handles when asked for (test_dist_kernel9_rmat_ghosts_bitwise),
+    but the autotuner never makes it a candidate there: whether it has a staging layout may
+    differ between ranks, and every rank must run the same rounds (FP::tune_steps). One RCCL
+    rank (a pass needs many rounds in one call; the in-process transport runs one at a time),
+    R-MAT where kernel 9 would win on one GPU; kernel 9 explicitly at one rank, bitwise."""
+    from fu.dist import DistCollectAll, partition, unique_id
 
-    g = fu.Graph.erdos_renyi(20_000, 80_000, seed=2)
-    v = fu.uniform_values(g.n, seed=2)
-    p = partition(g.rowptr, g.col, g.rev, 2, 0)
-    with pytest.raises(fu.FuError, match="kernels 4 .recon. and 8 .stage."):
-        DistCollectAll(p, v[p.lo:p.hi], None, kernel="pregather")
+    g = fu.Graph.rmat(15, 16, seed=12)
+    v = fu.uniform_values(g.n, seed=12)
+    plan = partition(g.rowptr, g.col, g.rev, 1, 0)
+    d = DistCollectAll(plan, v, unique_id(), kernel="auto")
+    d.run(120)
+    info = d.info()
+    assert info["autotune"] == "done" and info["kernel"] in ("recon", "stage"), info
+    assert info["tune_us_per_round"]["pregather"] == 0.0
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 120, nthreads=16)
+    assert np.array_equal(d.estimates(), a_ref) and np.array_equal(d.flows(), f_ref)
+    d.close()
+    d9 = DistCollectAll(plan, v, unique_id(), kernel="pregather")
+    d9.run(40)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 40, nthreads=16)
+    assert np.array_equal(d9.estimates(), a_ref) and np.array_equal(d9.flows(), f_ref)
+    d9.close()
 
 
 @pytest.mark.parametrize("world", [2, 3])
