@@ -141,6 +141,8 @@ def main():
         wl = "er" if world == 1 else "rgg-dist"
     if wl == "rgg-dist":
         return run_dist(args, world, rank, local, dist)
+    if wl == "pairwise" and world > 1:  # the tick replay does not shard: replicas
+        return run_pairwise_replicas(args, world, rank, local, dist)
     if world > 1:
         print(f"[bench] error: workload {wl} is single-GPU (use rgg-dist at N > 1)", file=sys.stderr, flush=True)
         sys.exit(2)
@@ -695,7 +697,30 @@ def run_pairwise(args):
     print(json.dumps(pairwise_line(args)), flush=True)
 
 
-def pairwise_line(args):
+def run_pairwise_replicas(args, world, rank, local, dist):
+    """Pairwise mode at N > 1: "replicas only" (the tick replay is latency-bound
+    and is not sharded): every rank replays the same RR-64K trace on its own GPU, between
+    barriers; value = the updates of all replicas / the slowest rank's wall time."""
+    import torch
+
+    line = pairwise_line(args, device=local, barrier=dist.barrier)
+    t = torch.tensor([line["ms_per_step"] * args.steps * 1e-3, line["roofline"]["avg_launch_us"]],
+                     dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        wall = float(t[0])
+        upd = line["config"]["pairwise_updates"]
+        line.update({"value": upd * world / wall, "n_gpus": world, "ms_per_step": wall * 1e3 / args.steps,
+                     "value_per_gpu": upd / wall, "scaling": "weak", "cpu_baseline": None,
+                     "cpu_baseline_note": "reported on the N = 1 line only"})
+        line["config"]["parallelism"] = f"replicas x{world} (the tick replay does not shard)"
+        line["roofline"]["per_gpu"] = True
+        line["roofline"]["avg_launch_us_max_over_ranks"] = float(t[1])
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+
+
+def pairwise_line(args, device=0, barrier=None):
     """BASELINE config 3: pairwise mode on a 64K-node random regular graph (d = 8), the
     SimGrid event order (Peer.loop, mailbox rendez-vous; App. B) replayed on the GPU by the
     persistent dataflow kernel. A step = one tick (PW:69-84 for every actor); the timed ticks
@@ -716,14 +741,18 @@ def pairwise_line(args):
     win = ev[e0:e1]
     upd = int(np.sum(win[:, 0] == 2))
     alg = pairwise_bytes(win, a["rowptr"], tasks)
-    rep = fu.Replay(tr, v, persistent=True)
+    rep = fu.Replay(tr, v, device=device, persistent=True)
     rep.run(t0_tick)
+    if barrier:
+        barrier()
     t = time.perf_counter()
     ms = rep.run_timed(ticks)
     wall = time.perf_counter() - t
+    if barrier:
+        barrier()
     rep.close()
     cpu = None
-    if args.cpu_seconds > 0:
+    if args.cpu_seconds > 0 and device == 0 and barrier is None:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import coracle
 

@@ -199,7 +199,7 @@ class _FakeEngine:
 
 
 class _FakeReplay:
-    def __init__(self, tr, v, persistent=False):
+    def __init__(self, tr, v, device=0, persistent=False):
         self.tr = tr
 
     def run(self, tick_end, snapshot_ticks=()):
@@ -266,3 +266,40 @@ def test_window_stats_lookup(tmp_path, monkeypatch):
     ws = bench.window_stats(10, 40, "stage", 20)
     assert ws["file"] == os.path.join("profiles", "r05", "x_window_stats.json") and ws["frac"] == 0.45
     assert bench.window_stats(10, 40, "stage", 21) is None
+
+
+def _replica_rank(rank, port, outdir):
+    import contextlib
+    import io
+    import json
+
+    import torch.distributed as dist
+
+    import fu
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", world_size=2, rank=rank)
+    fu.Replay = _FakeReplay
+    args = bench.parse(["--gpus", "2", "--workload", "pairwise", "--steps", "40", "--warmup", "10", "--n", "4096",
+                        "--cpu-seconds", "0"])
+    buf = io.StringIO()
+    with contextlib.redirect_stdout(buf):
+        bench.run_pairwise_replicas(args, 2, rank, rank, dist)
+    with open(os.path.join(outdir, f"r{rank}.txt"), "w") as f:
+        f.write(buf.getvalue())
+
+
+def test_pairwise_replicas_at_two_ranks(tmp_path):
+    """--workload pairwise at N > 1 runs replicas (the replay does not shard):
+    rank 0's line sums the replicas' updates over the slowest rank's wall time (gloo, two
+    processes on the CPU; the trace is real, the replay faked)."""
+    import json
+
+    import torch.multiprocessing as mp
+
+    mp.spawn(_replica_rank, args=(bench._free_port(), str(tmp_path)), nprocs=2, join=True)
+    line = json.loads((tmp_path / "r0.txt").read_text().strip().splitlines()[-1])
+    assert (tmp_path / "r1.txt").read_text().strip() == ""
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and "replicas x2" in line["config"]["parallelism"]
+    assert abs(line["value"] - 2 * line["value_per_gpu"]) < 1e-6 * line["value"]
+    assert line["cpu_baseline"] is None
