@@ -228,12 +228,13 @@ def make_graph(wl, n_arg, m_arg):
     return fu.Graph.random_regular(n, 8, seed=1), f"rr:n={n},d=8 collect-all generation-synchronous rounds"
 
 
-def prepare(eng, kernel, warmup, widths=None):
-    """Untimed setup: one autotune pass (kernel auto), `warmup` rounds in chunks of 64 (the
-    host sees each packing plan's width between calls, so the autotuner also covers every
-    width the warmup reaches; winners are kept across fu_reset), fu_reset. widths: a list
-    that receives (rounds done, packing plan width) after each chunk."""
-    if kernel == "auto":
+def prepare(eng, kernel, warmup, widths=None, tune=True):
+    """Untimed setup: one autotune pass (kernel auto; tune=False: the engine was tuned at this
+    width already), `warmup` rounds in chunks of 64 (the host sees each packing plan's width
+    between calls, so the autotuner also covers every width the warmup reaches; winners are
+    kept across fu_reset; at most four passes per engine), fu_reset. widths: a list that
+    receives (rounds done, packing plan width) after each chunk."""
+    if kernel == "auto" and tune:
         eng.tune()
     done = 0
     for w0 in range(0, warmup, 64):
@@ -355,7 +356,7 @@ def config2_1000(eng, g, kernel):
     without any error check, HIP events around round 0 and ten chunks."""
     widths = []
     eng.reset()  # the width schedule is counted from the zero state, as in the timed run
-    prepare(eng, kernel, 400, widths)
+    prepare(eng, kernel, 400, widths, tune=False)  # the headline's pass covered width 0
     wall, phases, roof, value_r1, info, kname = measure_window(eng, g, 1000)
     sched, last = [], None
     for r, w in widths:  # rounds at which the plan's width changed (deterministic: the same
