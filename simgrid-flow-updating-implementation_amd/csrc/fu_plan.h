@@ -27,7 +27,13 @@ constexpr int kR0E = 1024;                       // round-0 flow blocks; c16 blo
 constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
 constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 constexpr int kStageLds = 131072;                // bytes of estimate table per slice
-constexpr int kStageTE = 1024, kStageTN = 128;   // kernel 8 light tiles
+#ifndef FU_STAGE_TE
+#define FU_STAGE_TE 1024
+#endif
+#ifndef FU_STAGE_TN
+#define FU_STAGE_TN 128
+#endif
+constexpr int kStageTE = FU_STAGE_TE, kStageTN = FU_STAGE_TN;  // kernel 8 light tiles (experiment builds override)
 constexpr int kStageRuns = 64;                   // slice runs per tile the u16 index addresses
 constexpr int kStageMaxP = 512;                  // slices per kernel 8 layout
 #ifndef FU_TR_BE
