@@ -274,7 +274,10 @@ def run_single(args, wl):
     print(f"[bench] graph {desc}: n={g.n} E={g.E} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
     layout = args.layout if args.layout != "auto" else ("degree" if wl == "rmat" else "given")
     device = 0
+    t_create = time.perf_counter()  # host CSR and values -> HBM, the launch plans, the tables
     eng = fu.CollectAll(g, v, device=device, kernel=args.kernel, layout=layout)
+    eng.synchronize()
+    t_create = time.perf_counter() - t_create
     for kv in args.opt:
         k, val = kv.split("=", 1)
         eng.set_option(k, int(val))
@@ -283,8 +286,16 @@ def run_single(args, wl):
     t_setup = time.perf_counter() - t_setup
 
     wall, phases, roof, value_r1, kinfo, kname = measure_window(eng, g, args.steps)
+    t_down = time.perf_counter()  # the K-round job's result back to the host (fu_get_estimates)
+    eng.estimates()
+    t_down = time.perf_counter() - t_down
     pack_after = eng.pack_widths()[2]
     value = g.E * args.steps / wall
+    host_io = {"create_s": t_create, "estimates_to_host_s": t_down,
+               "host_bytes_in": 8 * (g.n + 1) + 4 * g.E + 8 * g.n, "host_bytes_out": 8 * g.n,
+               "value_with_create_and_download": g.E * args.steps / (wall + t_create + t_down),
+               "note": "not the metric: the handle is created once per job (fu_create: the CSR and values "
+                       "cross PCIe, the launch plans are built on the host) and the estimates return once"}
     companions = args.workload == "auto" and not args.no_unit
     extra = {}
     if companions and args.steps != 1000:  # BASELINE config 2 as written, on the same engine
@@ -323,7 +334,7 @@ def run_single(args, wl):
             "options": args.opt,
             "parallelism": "single GPU",
         },
-        "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen,
+        "roofline": roof, "cpu_baseline": cpu, "graph_gen_s": t_gen, "host_io": host_io,
     }
     out.update(conv)
     del g

@@ -177,6 +177,9 @@ class _FakeEngine:
     def synchronize(self):
         pass
 
+    def estimates(self):
+        return np.zeros(4)
+
     def pack_widths(self):
         w = 8 if self.r >= 200 else 16 if self.r >= 150 else 32 if self.r >= 110 else 0
         return (w, w, w)
@@ -234,6 +237,9 @@ def test_n1_line_carries_config2_rmat24_pairwise_units(monkeypatch, capsys):
     bench.run_single(args, "er")
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["steps"] == 20 and line["roofline"]["copy_GBs"] == 5500.0
+    io = line["host_io"]  # the PCIe-inclusive rate, beside (never as) the value
+    assert io["host_bytes_in"] == 8 * 1_000_001 + 4 * 7_999_972 + 8 * 1_000_000
+    assert 0 < io["value_with_create_and_download"] <= line["value"]
     c2 = line["config2_1000"]
     assert "error" not in c2, c2
     assert abs(c2["avg_round_us"] - 50.0) < 1e-9 and len(c2["phases"]) == 11
