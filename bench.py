@@ -289,9 +289,12 @@ def run_single(args, wl):
     t_down = time.perf_counter()  # the K-round job's result back to the host (fu_get_estimates)
     eng.estimates()
     t_down = time.perf_counter() - t_down
+    t_down2 = time.perf_counter()  # again: a snapshot's cost once the bounce buffers exist
+    eng.estimates()
+    t_down2 = time.perf_counter() - t_down2
     pack_after = eng.pack_widths()[2]
     value = g.E * args.steps / wall
-    host_io = {"create_s": t_create, "estimates_to_host_s": t_down,
+    host_io = {"create_s": t_create, "estimates_to_host_s": t_down, "estimates_to_host_again_s": t_down2,
                "host_bytes_in": 8 * (g.n + 1) + 4 * g.E + 8 * g.n, "host_bytes_out": 8 * g.n,
                "value_with_create_and_download": g.E * args.steps / (wall + t_create + t_down),
                "note": "not the metric: the handle is created once per job (fu_create: the CSR and values "

@@ -2195,6 +2195,8 @@ struct fu_handle {
   int tuned_width = 0;    // packing width the last pass ran under
   int tune_cache[4] = {-1, -1, -1, -1};  // winner per packing width (0, 8, 16, 32), kept across fu_reset
   int *h_pw = nullptr;    // pinned copy of the plan's width, refreshed after each plan
+  void *h_xfer[2] = {nullptr, nullptr};           // pinned bounce buffers of copy_out (kXfer bytes each)
+  hipEvent_t ev_xfer[2] = {nullptr, nullptr};
   bool pw_pending = false;
   int *pw_dev = nullptr;      // h_pw as the device sees it (the plan kernels write the width there)
   bool plan_pending = false;  // a packing plan is due before the next round (from its table)
@@ -3489,19 +3491,46 @@ int fu_max_err(fu_handle *h, double *out) {
   return FU_OK;
 }
 
+// Device memory -> the caller's (pageable) host memory through two pinned kXfer-byte
+// buffers: the DMA of chunk k runs while the host copies chunk k-1 out. A pageable
+// hipMemcpyAsync stages through the runtime's own buffers one at a time (ER-1M's 8 MB of
+// estimates: 31 ms on the box, profiles/r05/g/).
+constexpr size_t kXfer = (size_t)4 << 20;
+
+static int copy_out(fu_handle *h, void *dst, const void *src, size_t bytes) {
+  for (int k = 0; k < 2; ++k) {
+    if (!h->h_xfer[k] && hipHostMalloc(&h->h_xfer[k], kXfer, hipHostMallocDefault) != hipSuccess)
+      return fail(FU_ERR_ALLOC, "hipHostMalloc (copy-out buffer) failed");
+    if (!h->ev_xfer[k] && hipEventCreateWithFlags(&h->ev_xfer[k], hipEventDisableTiming) != hipSuccess)
+      return fail(FU_ERR_HIP, "hipEventCreate failed");
+  }
+  const size_t nk = (bytes + kXfer - 1) / kXfer;
+  for (size_t k = 0; k <= nk; ++k) {
+    if (k < nk) {  // chunk k into buffer k & 1 (its previous chunk, k - 2, was copied out at k - 1)
+      const size_t len = std::min(kXfer, bytes - k * kXfer);
+      HIP_TRY(hipMemcpyAsync(h->h_xfer[k & 1], static_cast<const char *>(src) + k * kXfer, len,
+                             hipMemcpyDeviceToHost, h->stream));
+      HIP_TRY(hipEventRecord(h->ev_xfer[k & 1], h->stream));
+    }
+    if (k > 0) {  // chunk k - 1 out while chunk k is in flight
+      const size_t j = k - 1, len = std::min(kXfer, bytes - j * kXfer);
+      HIP_TRY(hipEventSynchronize(h->ev_xfer[j & 1]));
+      std::memcpy(static_cast<char *>(dst) + j * kXfer, h->h_xfer[j & 1], len);
+    }
+  }
+  return FU_OK;
+}
+
 int fu_get_estimates(fu_handle *h, double *a_out) {
   if (!h || !a_out) return fail(FU_ERR_ARG, "fu_get_estimates: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!h->h_new_of_old.empty()) {  // device numbering -> caller numbering
     std::vector<double> a2(h->n);
-    HIP_TRY(hipMemcpyAsync(a2.data(), cur_a(h), sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (int rc = copy_out(h, a2.data(), cur_a(h), sizeof(double) * h->n)) return rc;
     for (int32_t i = 0; i < h->n; ++i) a_out[i] = a2[h->h_new_of_old[i]];
     return FU_OK;
   }
-  HIP_TRY(hipMemcpyAsync(a_out, cur_a(h), sizeof(double) * h->n, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  return FU_OK;
+  return copy_out(h, a_out, cur_a(h), sizeof(double) * h->n);
 }
 
 int fu_get_flows(fu_handle *h, double *f_out) {
@@ -3527,8 +3556,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
   const double *src = h->ftmp;
   if (!h->h_new_of_old.empty()) {  // rows back to the caller's order (blocks, same order inside)
     std::vector<double> f2(h->E);
-    HIP_TRY(hipMemcpyAsync(f2.data(), src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
-    HIP_TRY(hipStreamSynchronize(h->stream));
+    if (int rc = copy_out(h, f2.data(), src, sizeof(double) * h->E)) return rc;
     const auto &orp = h->h_orig_rowptr;
     for (int32_t i = 0; i < h->n; ++i) {
       const int64_t nb = h->h_rowptr[h->h_new_of_old[i]];
@@ -3536,9 +3564,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
     }
     return FU_OK;
   }
-  HIP_TRY(hipMemcpyAsync(f_out, src, sizeof(double) * h->E, hipMemcpyDeviceToHost, h->stream));
-  HIP_TRY(hipStreamSynchronize(h->stream));
-  return FU_OK;
+  return copy_out(h, f_out, src, sizeof(double) * h->E);
 }
 
 int fu_get_info(fu_handle *h, int64_t info[32]) {
@@ -3652,11 +3678,13 @@ int fu_destroy(fu_handle *h) {
   }
   for (void *p : ptrs)
     if (p) hipFree(p);
-  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join})
+  for (hipEvent_t e : {h->ev0, h->ev1, h->ev2, h->ev3, h->ev_pw, h->ev_fork, h->ev_join, h->ev_xfer[0], h->ev_xfer[1]})
     if (e) hipEventDestroy(e);
   for (hipEvent_t e : h->marks)
     if (e) hipEventDestroy(e);
   if (h->h_pw) hipHostFree(h->h_pw);
+  for (void *p : h->h_xfer)
+    if (p) hipHostFree(p);
   if (h->stream) hipStreamDestroy(h->stream);
   if (h->stream2) hipStreamDestroy(h->stream2);
   delete h;
