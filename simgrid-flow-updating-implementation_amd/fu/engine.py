@@ -22,7 +22,7 @@ MODE = {"collectall": 0, "ca": 0, "pairwise": 1, "pw": 1}
 
 
 def handle_info(h) -> dict:
-    """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
+    """Kernel in use (after autotuning), autotune state, rounds done."""
     a = np.zeros(32, dtype=np.int64)
     L.call("fu_get_info", h, L.ptr(a))
     names = {4: "recon", 8: "stage", 9: "pregather"}
@@ -147,7 +147,7 @@ class CollectAll:
         return f[:self.E]
 
     def info(self) -> dict:
-        """Kernel in use (after autotuning), nt policy, autotune state, rounds done."""
+        """Kernel in use (after autotuning), autotune state, rounds done."""
         return handle_info(self._h)
 
     def pack_widths(self) -> tuple:

@@ -244,6 +244,31 @@ def test_full_size_er1m_convergence_and_prefix_parity():
     assert np.all(np.diff(tr[5:]) <= 0) or tr[-1] < 1e-12  # settles monotonically
 
 
+def test_config2_as_written_1000_rounds_bitwise():
+    """BASELINE config 2 as written, the whole job bitwise: ER n=1e6 m=4e6, 1000 rounds from
+    the zero state on the default engine (kernel auto, autotuned at every packing width it
+    reaches; the estimate table packs to 32, 16 and 8 bits on the way), estimates and flows
+    equal to the C oracle's after rounds 150, 400 and 1000 (CA:105-128 every round)."""
+    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    eng = fu.CollectAll(g, v)
+    a_ref, f_ref = None, None
+    widths = set()
+    for done, k in ((150, 150), (400, 250), (1000, 600)):
+        for _ in range(0, k, 50):  # the host sees each plan's width between calls (autotune per width)
+            eng.run(50)
+            widths.add(eng.pack_widths()[2])
+        if a_ref is None:
+            a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, done, nthreads=16)
+        else:
+            coracle.ca_rounds(g.rowptr, g.col, g.rev, v, k, a_ref, f_ref, nthreads=16)
+        assert np.array_equal(eng.estimates(), a_ref), done
+        assert np.array_equal(eng.flows(), f_ref), done
+    assert {32, 16, 8} <= widths, widths  # every packed width ran
+    assert eng.info()["rounds"] == 1000
+    eng.close()
+
+
 def test_dist_single_rank_rccl_matches_engine():
     """fu_dist_create + RCCL communicator at world size 1 (the only size one GPU box can
     run): no ghosts, the per-round halo hook runs with empty send lists. Ghost slots are
