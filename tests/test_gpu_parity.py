@@ -866,14 +866,15 @@ def _check_flow_bookkeeping(g, v, a, f):
 def test_rmat24_degree_layout_bitwise():
     """BASELINE config 4 at full size: R-MAT scale 24 (edge factor 16; E = 5.2e8, max degree
     406,598: mega hubs, heavy rows) with the degree layout and the autotuned kernel on one
-    MI355X. 10 rounds bitwise against the C oracle (16 threads), and the flow bookkeeping."""
+    MI355X. Rounds 0-19 (the window `rmat24_unit` times) bitwise against the C oracle (16
+    threads), and the flow bookkeeping."""
     g = fu.Graph.rmat(24, 16, seed=1)
     v = fu.uniform_values(g.n, seed=0)
     eng = fu.CollectAll(g, v, layout="degree")
-    eng.run(10)
+    eng.run(20)
     a, f = eng.estimates(), eng.flows()
     eng.close()
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 10, nthreads=16)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
     assert np.array_equal(a, a_ref)
     assert np.array_equal(f, f_ref)
     del a_ref, f_ref
@@ -882,16 +883,17 @@ def test_rmat24_degree_layout_bitwise():
 
 def test_rgg_2pow23_partition_unit_bitwise():
     """BASELINE config 5's weak-scaling unit: RggPart(2^23) at world size 1 (native slab
-    generator, RCCL communicator), 5 rounds bitwise against the C oracle on the same graph."""
+    generator, RCCL communicator), rounds 0-19 (the window `weak_scaling_unit` times) bitwise
+    against the C oracle on the same graph."""
     from fu.dist import DistCollectAll, RggPart, unique_id
 
     n = 1 << 23
     part = RggPart(n, avg_deg=8.0, seed=1, nparts=1, part=0)
     v = part.values(seed=0)
     d = DistCollectAll(part.to_plan(), v, unique_id())
-    d.run(5)
+    d.run(20)
     g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 5, nthreads=16)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
     assert np.array_equal(d.estimates(), a_ref)
     assert np.array_equal(d.flows(), f_ref)
     d.close()
