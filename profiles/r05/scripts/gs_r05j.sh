@@ -1,8 +1,10 @@
 # round 5, session j: R-MAT-24 (config 4) and the RGG 2^23 partitioned unit (config 5) bitwise
-# over rounds 0-19, the windows rmat24_unit and weak_scaling_unit time.
+# over rounds 0-19, the windows rmat24_unit and weak_scaling_unit time. (First run: bitwise
+# passed, the flow-bookkeeping property's flat 1e-12 failed at 1.8e-12 on a long row; the
+# property now bounds per node by the row length.)
 set -o pipefail
 O=gpurun_out/j
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 500 python -u -m pytest -s -x -v --durations=0 --timeout 400 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "rmat24_degree_layout_bitwise or rgg_2pow23_partition_unit_bitwise" > $O/pytest.log 2>&1 || exit $?
+timeout -k 10 500 python -u -m pytest -s -x -v --durations=0 --timeout 400 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "rmat24_degree_layout_bitwise or rgg_2pow23_partition_unit_bitwise or rgg64m" > $O/pytest.log 2>&1 || exit $?
 exit 0

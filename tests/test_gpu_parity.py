@@ -849,15 +849,20 @@ def test_stage_layout_slices_and_unbuildable_graphs():
 def _check_flow_bookkeeping(g, v, a, f):
     """Each node's estimate after its average equals its value minus its outgoing flows
     (CA:107 with CA:117: Σ_j f_new = Σ fr + d·a - Σ er = v - a), so Σ a + Σ f = Σ v: the
-    mass in flight is the flow sum. Both hold to rounding."""
+    mass in flight is the flow sum. Both hold to rounding: per node within 4 (d + 2) u of
+    |v| + Σ|f| + (d + 1)|a| + 1 (u = 2^-53; d + 2 roundings of the row's flows, its average
+    and numpy's sum; the C oracle's R-MAT 18-20 outputs reach 0.44 of (d + 2) u of it, so
+    the test holds at any row length, where a flat 1e-12 failed on R-MAT-24's 20th round at
+    1.8e-12, a row of ~10^5 edges)."""
     idx = np.minimum(g.rowptr[:-1], g.E - 1)  # reduceat needs indices < len; empty rows -> 0
-    empty = np.diff(g.rowptr) == 0
+    d = np.diff(g.rowptr)
+    empty = d == 0
     out = np.add.reduceat(f, idx)
     out[empty] = 0.0
     absout = np.add.reduceat(np.abs(f), idx)
     absout[empty] = 0.0
-    scale = np.abs(v) + absout + 1.0
-    assert np.max(np.abs(a - (v - out)) / scale) < 1e-12
+    scale = np.abs(v) + absout + (d + 1) * np.abs(a) + 1.0
+    assert np.max(np.abs(a - (v - out)) / ((d + 2) * 2.0 ** -53 * scale)) < 4.0
     tot = np.sum(np.abs(v)) + np.sum(np.abs(f))
     assert abs(np.sum(a) + np.sum(f) - np.sum(v)) / tot < 1e-12
 
