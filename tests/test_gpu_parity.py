@@ -201,6 +201,51 @@ def test_replay_rr64k_vs_c_oracle(mode, persistent):
         assert np.array_equal(snaps[t], s_ref[t])
 
 
+def test_headline_window_bitwise():
+    """The driver's N = 1 headline exactly as bench.py runs it: ER-1M, bench.prepare (one
+    autotune pass, 5 warmup rounds, fu_reset), then bench.timed_rounds (rounds 0-19 with
+    the HIP event marks); estimates and flows equal the C oracle's after 20 rounds, then
+    config2_1000's prefix (reset, the 400-round untimed pass, reset, 1000 timed rounds)."""
+    import bench
+
+    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    eng = fu.CollectAll(g, v)
+    bench.prepare(eng, "auto", 5)
+    bench.timed_rounds(eng, 20)
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 20, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    eng.reset()
+    bench.prepare(eng, "auto", 400, [], tune=False)
+    bench.timed_rounds(eng, 1000)
+    coracle.ca_rounds(g.rowptr, g.col, g.rev, v, 980, a_ref, f_ref, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    eng.close()
+
+
+def test_pairwise_unit_window_bitwise():
+    """BASELINE config 3 exactly as `pairwise_unit` times it: RR-64K pairwise, tie order
+    rand:3, the default persistent register kernel run to tick 101, then ticks 101-500
+    through fu_replay_run_timed; the final last_avg, flows and estimate caches equal the C
+    oracle's replay of ticks 0-500 (PW:93-117 every event)."""
+    g = fu.Graph.random_regular(65536, 8, seed=1)
+    v = fu.uniform_values(g.n, seed=0)
+    tr = fu.Trace(g.rowptr, g.col, "pairwise", 501, "rand:3")
+    a = tr.arrays()
+    rep = fu.Replay(tr, v, persistent=True)
+    rep.run(101)
+    assert rep.run_timed(501) > 0
+    last, flows, est = rep.state()
+    rep.close()
+    l_ref, f_ref, e_ref, _ = coracle.replay(a["rowptr"], v, a["tick_task_off"], a["tasks"], a["events"],
+                                            a["out_ids"], tr.n_msgs)
+    assert np.array_equal(last, l_ref)
+    assert np.array_equal(flows, f_ref)
+    assert np.array_equal(est, e_ref)
+
+
 @pytest.mark.parametrize("mode,tag", [("ca", "fwd"), ("pw", "fwd"), ("ca", "rev"), ("pw", "rand7")])
 def test_engine_small_platform_watcher_lines(tmp_path, mode, tag):
     """The drop-in Engine on the reference inputs prints the watcher's lines (CA:134-142)
