@@ -3082,6 +3082,7 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
 }
 
 int fu_set_option(fu_handle *h, const char *key, int64_t value) {
+  FU_TRY_BEGIN
   if (!h || !key) return fail(FU_ERR_ARG, "fu_set_option: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!std::strcmp(key, "kernel")) {
@@ -3201,9 +3202,11 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     return build_tiles(h);
   }
   return fail(FU_ERR_ARG, std::string("fu_set_option: unknown key '") + key + "'");
+  FU_TRY_END
 }
 
 int fu_reset(fu_handle *h) {
+  FU_TRY_BEGIN
   if (!h) return fail(FU_ERR_ARG, "fu_reset: NULL handle");
   if (int rc = set_device(h)) return rc;
   if (h->dist) {  // phase 1: wait for the last halo, drain the comm stream, forget its rounds
@@ -3221,9 +3224,11 @@ int fu_reset(fu_handle *h) {
     h->tuned_width = 0;
   }
   return FU_OK;
+  FU_TRY_END
 }
 
 int fu_set_targets(fu_handle *h, const double *target) {
+  FU_TRY_BEGIN
   if (!h || !target) return fail(FU_ERR_ARG, "fu_set_targets: NULL argument");
   if (int rc = set_device(h)) return rc;
   std::vector<double> t2;
@@ -3236,6 +3241,7 @@ int fu_set_targets(fu_handle *h, const double *target) {
   HIP_TRY(hipStreamSynchronize(h->stream));
   h->has_target = true;
   return FU_OK;
+  FU_TRY_END
 }
 
 int fu__err_slots(fu_handle *h, int count) {
@@ -3474,6 +3480,7 @@ int fu_mark_elapsed(fu_handle *h, int32_t from, int32_t to, float *ms) {
 }
 
 int fu_max_err(fu_handle *h, double *out) {
+  FU_TRY_BEGIN
   if (!h || !out) return fail(FU_ERR_ARG, "fu_max_err: NULL argument");
   if (!h->has_target) return fail(FU_ERR_STATE, "fu_max_err: call fu_set_targets first");
   if (int rc = set_device(h)) return rc;
@@ -3489,6 +3496,7 @@ int fu_max_err(fu_handle *h, double *out) {
   HIP_TRY(hipStreamSynchronize(h->stream));
   std::memcpy(out, &bits, sizeof(double));
   return FU_OK;
+  FU_TRY_END
 }
 
 // Device memory -> the caller's (pageable) host memory through two pinned kXfer-byte
@@ -3522,6 +3530,7 @@ static int copy_out(fu_handle *h, void *dst, const void *src, size_t bytes) {
 }
 
 int fu_get_estimates(fu_handle *h, double *a_out) {
+  FU_TRY_BEGIN
   if (!h || !a_out) return fail(FU_ERR_ARG, "fu_get_estimates: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (!h->h_new_of_old.empty()) {  // device numbering -> caller numbering
@@ -3531,9 +3540,11 @@ int fu_get_estimates(fu_handle *h, double *a_out) {
     return FU_OK;
   }
   return copy_out(h, a_out, cur_a(h), sizeof(double) * h->n);
+  FU_TRY_END
 }
 
 int fu_get_flows(fu_handle *h, double *f_out) {
+  FU_TRY_BEGIN
   if (!h || (!f_out && h->E)) return fail(FU_ERR_ARG, "fu_get_flows: NULL argument");
   if (h->E == 0) return FU_OK;
   if (h->rounds == 0) {  // no round yet: every flow is 0.0 (CA:33)
@@ -3565,6 +3576,7 @@ int fu_get_flows(fu_handle *h, double *f_out) {
     return FU_OK;
   }
   return copy_out(h, f_out, src, sizeof(double) * h->E);
+  FU_TRY_END
 }
 
 int fu_get_info(fu_handle *h, int64_t info[32]) {
@@ -3587,6 +3599,7 @@ int fu_get_info(fu_handle *h, int64_t info[32]) {
 }
 
 int fu_get_pack(fu_handle *h, int32_t width[3]) {
+  FU_TRY_BEGIN
   if (!h || !width) return fail(FU_ERR_ARG, "fu_get_pack: NULL argument");
   if (int rc = set_device(h)) return rc;
   if (h->plan_pending && h->rounds > 0) {  // the plan due after the last round, as the next round would run it
@@ -3599,6 +3612,7 @@ int fu_get_pack(fu_handle *h, int32_t width[3]) {
   HIP_TRY(hipStreamSynchronize(h->stream));
   for (int k = 0; k < 3; ++k) width[k] = p[k].width;
   return FU_OK;
+  FU_TRY_END
 }
 
 int fu_get_round(fu_handle *h, int64_t *rounds_done) {
@@ -3902,6 +3916,7 @@ const fu_trace *fu__trace_view(const fu_trace *t, int32_t *n, int32_t *ticks,
 
 int fu_replay_create_from_trace(const fu_trace *t, const double *value, int32_t device,
                                 fu_replay **out) {
+  FU_TRY_BEGIN
   if (!t) return fail(FU_ERR_ARG, "fu_replay_create_from_trace: NULL trace");
   int32_t n, ticks;
   const int64_t *urp, *tto;
@@ -3909,6 +3924,7 @@ int fu_replay_create_from_trace(const fu_trace *t, const double *value, int32_t 
   int64_t nt, ne, no, nm;
   fu__trace_view(t, &n, &ticks, &urp, &tto, &tasks, &nt, &events, &ne, &oids, &no, &nm);
   return fu_replay_create(n, urp, value, ticks, tto, nt, tasks, ne, events, no, oids, nm, device, out);
+  FU_TRY_END
 }
 
 static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
@@ -3965,6 +3981,7 @@ static int replay_ticks(fu_replay *r, int32_t tick_end, int32_t n_snap, const in
 
 int fu_replay_run(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t *snap_ticks,
                   double *snaps) {
+  FU_TRY_BEGIN
   if (!r || tick_end < r->cur_tick || tick_end > r->ticks || n_snap < 0 || (n_snap > 0 && (!snap_ticks || !snaps)))
     return fail(FU_ERR_ARG, "fu_replay_run: bad arguments");
   for (int32_t k = 1; k < n_snap; ++k)
@@ -3983,6 +4000,7 @@ int fu_replay_run(fu_replay *r, int32_t tick_end, int32_t n_snap, const int32_t 
   if (hipStreamSynchronize(r->stream) != hipSuccess && rc == FU_OK) rc = fail(FU_ERR_HIP, "fu_replay_run: sync failed");
   if (d_snaps) hipFree(d_snaps);
   return rc;
+  FU_TRY_END
 }
 
 int fu_replay_run_timed(fu_replay *r, int32_t tick_end, float *ms) {
@@ -3997,6 +4015,7 @@ int fu_replay_run_timed(fu_replay *r, int32_t tick_end, float *ms) {
 }
 
 int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est) {
+  FU_TRY_BEGIN
   if (!r) return fail(FU_ERR_ARG, "fu_replay_get: NULL replay");
   HIP_TRY(hipSetDevice(r->device));
   if (last_avg) HIP_TRY(hipMemcpyAsync(last_avg, r->last, sizeof(double) * r->n, hipMemcpyDeviceToHost, r->stream));
@@ -4004,9 +4023,11 @@ int fu_replay_get(fu_replay *r, double *last_avg, double *flows, double *est) {
   if (est && r->E) HIP_TRY(hipMemcpyAsync(est, r->est, sizeof(double) * r->E, hipMemcpyDeviceToHost, r->stream));
   HIP_TRY(hipStreamSynchronize(r->stream));
   return FU_OK;
+  FU_TRY_END
 }
 
 int fu_replay_set_option(fu_replay *r, const char *key, int64_t value) {
+  FU_TRY_BEGIN
   if (!r || !key) return fail(FU_ERR_ARG, "fu_replay_set_option: NULL argument");
   if (!std::strcmp(key, "persistent")) {
     if (r->cur_tick != 0) return fail(FU_ERR_STATE, "fu_replay_set_option: persistent must be set before the first tick");
@@ -4021,6 +4042,7 @@ int fu_replay_set_option(fu_replay *r, const char *key, int64_t value) {
     return FU_OK;
   }
   return fail(FU_ERR_ARG, std::string("fu_replay_set_option: unknown key '") + key + "'");
+  FU_TRY_END
 }
 
 int fu_replay_destroy(fu_replay *r) {
