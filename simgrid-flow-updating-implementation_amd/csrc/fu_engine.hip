@@ -941,9 +941,16 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
         if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
         else val[j] = tab[nb + (int)off];
       }
+#ifdef FU_STAGE_NT  // experiment build: non-temporal G stores
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      v4u w;
+      __builtin_memcpy(&w, val, 16);
+      __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(G + gg));
+#else
       uint4 w;
       __builtin_memcpy(&w, val, 16);
       *reinterpret_cast<uint4 *>(G + gg) = w;
+#endif
     }
   }
 }
@@ -1306,7 +1313,12 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   // every G load of the tile first, then decode (escapes gather the double via col)
   if (pp.width == 0) {
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) g[k] = gi[k] >= 0 ? reinterpret_cast<const double *>(G)[gi[k]] : 0.0;
+    for (int k = 0; k < kPer; ++k)
+#ifdef FU_GLOAD_NT  // experiment build: non-temporal G loads (each staged element is read once)
+      g[k] = gi[k] >= 0 ? __builtin_nontemporal_load(reinterpret_cast<const double *>(G) + gi[k]) : 0.0;
+#else
+      g[k] = gi[k] >= 0 ? reinterpret_cast<const double *>(G)[gi[k]] : 0.0;
+#endif
   } else {
     unsigned cd[kPer];
     unsigned esc;
