@@ -257,23 +257,32 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
 // word is skipped; the value in memory is always the exact f_r).
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ long long fhi_idx(int e) { return ((long long)(e & ~31) << 1) | (e & 31); }
+#ifndef FU_FLOW_NT  // experiment builds: 1 = non-temporal flow stores, 2 = loads, 3 = both
+#define FU_FLOW_NT 0
+#endif
 __device__ __forceinline__ double ld_f(const double *F, int e) {
   const unsigned *w = reinterpret_cast<const unsigned *>(F);
   const long long i = fhi_idx(e);
+  if constexpr (FU_FLOW_NT & 2)
+    return __hiloint2double((int)__builtin_nontemporal_load(w + i), (int)__builtin_nontemporal_load(w + i + 32));
   return __hiloint2double((int)w[i], (int)w[i + 32]);
+}
+__device__ __forceinline__ void st_fw(unsigned *p, unsigned v) {
+  if constexpr (FU_FLOW_NT & 1) __builtin_nontemporal_store(v, p);
+  else st_wt(p, v);
 }
 // store f_r over f_old (the value the slot held)
 __device__ __forceinline__ void st_f(double *F, int e, double v, double f_old) {
   unsigned *w = reinterpret_cast<unsigned *>(F);
   const long long i = fhi_idx(e);
-  st_wt(w + i + 32, (unsigned)__double2loint(v));
-  if (__double2hiint(v) != __double2hiint(f_old)) st_wt(w + i, (unsigned)__double2hiint(v));
+  st_fw(w + i + 32, (unsigned)__double2loint(v));
+  if (__double2hiint(v) != __double2hiint(f_old)) st_fw(w + i, (unsigned)__double2hiint(v));
 }
 __device__ __forceinline__ void st_f_full(double *F, int e, double v) {
   unsigned *w = reinterpret_cast<unsigned *>(F);
   const long long i = fhi_idx(e);
-  st_wt(w + i + 32, (unsigned)__double2loint(v));
-  st_wt(w + i, (unsigned)__double2hiint(v));
+  st_fw(w + i + 32, (unsigned)__double2loint(v));
+  st_fw(w + i, (unsigned)__double2hiint(v));
 }
 
 // Flow mode of a round launch (fm): round 0 writes no flows at all. f_{r-2} of round 1 is
@@ -941,16 +950,13 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
         if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
         else val[j] = tab[nb + (int)off];
       }
-#ifdef FU_STAGE_NT  // experiment build: non-temporal G stores
+      // non-temporal: G is streamed out once and read back by the next launch (ER-1M
+      // kernel 8: 61.8 vs 62.7 us per round, R-MAT-24 kernel 9's G_A: 6,728 vs 6,807 us;
+      // process-separated A/Bs, profiles/r05/n, o)
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
       v4u w;
       __builtin_memcpy(&w, val, 16);
       __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(G + gg));
-#else
-      uint4 w;
-      __builtin_memcpy(&w, val, 16);
-      *reinterpret_cast<uint4 *>(G + gg) = w;
-#endif
     }
   }
 }
