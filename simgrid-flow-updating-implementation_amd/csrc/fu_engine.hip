@@ -257,20 +257,14 @@ __global__ __launch_bounds__(kBlock) void k_pack_plan(const double *__restrict__
 // word is skipped; the value in memory is always the exact f_r).
 // ------------------------------------------------------------------------------------
 __device__ __forceinline__ long long fhi_idx(int e) { return ((long long)(e & ~31) << 1) | (e & 31); }
-#ifndef FU_FLOW_NT  // experiment builds: 1 = non-temporal flow stores, 2 = loads, 3 = both
-#define FU_FLOW_NT 0
-#endif
+// (non-temporal flow loads, stores or both measured slower again in round 5: ER-1M kernel 8
+// +1.4 / +1.2 / +3.2 %, R-MAT-24 +1.2 / +8.9 / +11 %, profiles/r05/p)
 __device__ __forceinline__ double ld_f(const double *F, int e) {
   const unsigned *w = reinterpret_cast<const unsigned *>(F);
   const long long i = fhi_idx(e);
-  if constexpr (FU_FLOW_NT & 2)
-    return __hiloint2double((int)__builtin_nontemporal_load(w + i), (int)__builtin_nontemporal_load(w + i + 32));
   return __hiloint2double((int)w[i], (int)w[i + 32]);
 }
-__device__ __forceinline__ void st_fw(unsigned *p, unsigned v) {
-  if constexpr (FU_FLOW_NT & 1) __builtin_nontemporal_store(v, p);
-  else st_wt(p, v);
-}
+__device__ __forceinline__ void st_fw(unsigned *p, unsigned v) { st_wt(p, v); }
 // store f_r over f_old (the value the slot held)
 __device__ __forceinline__ void st_f(double *F, int e, double v, double f_old) {
   unsigned *w = reinterpret_cast<unsigned *>(F);
