@@ -944,13 +944,21 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
         if constexpr (LDS) val[j] = reinterpret_cast<const T *>(s_tab)[off];
         else val[j] = tab[nb + (int)off];
       }
-      // non-temporal: G is streamed out once and read back by the next launch (ER-1M
-      // kernel 8: 61.8 vs 62.7 us per round, R-MAT-24 kernel 9's G_A: 6,728 vs 6,807 us;
-      // process-separated A/Bs, profiles/r05/n, o)
+      // doubles non-temporal: G (64 MB on ER-1M, 4 GB of G_A on R-MAT-24) is streamed out
+      // once and read back by the next launch (ER-1M kernel 8: 61.8 vs 62.7 us per round,
+      // R-MAT-24 kernel 9: 6,728 vs 6,807 us; process-separated A/Bs, profiles/r05/n, o).
+      // Packed codes (8-32 MB) stay write-back: they fit on chip until the tiles read them
+      // (non-temporal there: 41.0 vs 38.8 us per 8-bit round, profiles/r05/q)
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
       v4u w;
       __builtin_memcpy(&w, val, 16);
-      __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(G + gg));
+#ifndef FU_STAGE_NT  // experiment builds: 0 = write-back stores, 2 = non-temporal at every width
+#define FU_STAGE_NT 1
+#endif
+      if constexpr (FU_STAGE_NT == 2 || (FU_STAGE_NT == 1 && sizeof(T) == 8))
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(G + gg));
+      else
+        *reinterpret_cast<v4u *>(G + gg) = w;
     }
   }
 }
