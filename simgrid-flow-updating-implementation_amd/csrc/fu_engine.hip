@@ -891,10 +891,6 @@ struct ColVec {
 };
 template <int EPL>
 __device__ __forceinline__ void ld_cols(ColVec<EPL> &c, const unsigned short *p) {
-#ifdef FU_COLS_NT  // experiment build: non-temporal column-offset loads (doubles)
-  if constexpr (EPL == 2) c.w[0].x = __builtin_nontemporal_load(reinterpret_cast<const unsigned *>(p));
-  else
-#endif
   if constexpr (EPL == 2) c.w[0].x = *reinterpret_cast<const unsigned *>(p);
   else if constexpr (EPL == 4) {
     const uint2 v = *reinterpret_cast<const uint2 *>(p);
@@ -1184,11 +1180,7 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   for (int k = 0; k < kPerT; ++k) {
     if constexpr (NT) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
     else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
-#ifdef FU_POS_NT  // experiment build: non-temporal position loads
-    pos[k] = g[k] >= 0 ? __builtin_nontemporal_load(pos16 + g[k]) : (unsigned short)0;
-#else
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
-#endif
   }
   const int next = bk + nj;
   if (next < bend) load_runs(next, o, len);  // in flight beside this bucket's loads
@@ -1275,11 +1267,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int q = t + k * kBlock;
-#ifdef FU_SIDX_NT  // experiment build: non-temporal staged-index loads
-      const unsigned short c = __builtin_nontemporal_load(s16 + (q < ne ? e0 + q : 0));
-#else
       const unsigned short c = s16[q < ne ? e0 + q : 0];
-#endif
       c16[k] = q < ne ? c : (unsigned short)0;
     }
     if constexpr (RF) {
