@@ -1178,7 +1178,10 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   unsigned short pos[kPerT];
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
-    if constexpr (NT) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
+#ifndef FU_TR_NTLOAD  // experiment builds: 0 = plain G_A loads beside the non-temporal G_B stores
+#define FU_TR_NTLOAD 1
+#endif
+    if constexpr (NT && FU_TR_NTLOAD) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
     else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
