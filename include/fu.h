@@ -129,7 +129,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 runs as one thread per row (k_isolated, 1, default) or as light tiles (0).
  * "multi_short"   kernel 9: the rows of 129-256 edges run in the multi-row blocks too (default 1;
  *                 0: one row per wave, four per block).
- * "tr_nt"         kernel 9: k_transpose's G_A loads and G_B stores non-temporal (default 1).
+ * "tr_nt"         kernel 9: k_transpose's G_B stores non-temporal (default 1; its G_A loads are plain
+ *                 since round 5: non-temporal loads measured slower, profiles/r05/u).
  * "c16"           kernel 4: 2-byte column offsets for light tiles whose columns lie within
  *                 32K ids of their 1024-edge block's first row (default 1).
  * "pack"          gather lossless 8/16/32-bit codes of the estimates once they cluster

@@ -1081,7 +1081,7 @@ constexpr int kTrThreads = 1024;
 #ifndef FU_TR_WAVES
 #define FU_TR_WAVES 1
 #endif
-template <bool NT>  // NT: streamed G_A loads / G_B stores non-temporal
+template <bool NT>  // NT: the streamed G_B stores non-temporal
 __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
@@ -1178,11 +1178,9 @@ __global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, i
   unsigned short pos[kPerT];
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
-#ifndef FU_TR_NTLOAD  // experiment builds: 0 = plain G_A loads beside the non-temporal G_B stores
-#define FU_TR_NTLOAD 1
-#endif
-    if constexpr (NT && FU_TR_NTLOAD) val[k] = g[k] >= 0 ? __builtin_nontemporal_load(GA + g[k]) : 0.0;
-    else val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
+    // plain loads (non-temporal G_A loads beside the non-temporal stores: 6,703 vs 6,612 us
+    // per round on R-MAT-24, profiles/r05/u)
+    val[k] = g[k] >= 0 ? GA[g[k]] : 0.0;
     pos[k] = g[k] >= 0 ? pos16[g[k]] : (unsigned short)0;
   }
   const int next = bk + nj;
@@ -2247,7 +2245,7 @@ struct fu_handle {
   int *hub_blk = nullptr;    // per 256-edge block of the hub edges: the hub of its first edge
   int iso_rows = 1;           // kernel 9: trailing isolated-row tiles as k_isolated (1) or as light tiles (0)
   int multi_short = 1;        // kernel 9: the rows of 129-256 edges in the multi-row blocks too (1)
-  int tr_nt = 1;              // kernel 9: non-temporal G_A loads and G_B stores in k_transpose (1)
+  int tr_nt = 1;              // kernel 9: non-temporal G_B stores in k_transpose (1)
   int *hub_off = nullptr;    // per mega tile: offset in hubxy
   double2 *hubxy = nullptr;  // (fr, er) per hub edge, staged each round
   // packed estimate table (see PackCtl): code[r & 1] = codes of a_r
@@ -3180,7 +3178,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     }
     return FU_OK;
   }
-  if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose streams G_A / G_B non-temporally (1)
+  if (!std::strcmp(key, "tr_nt")) {  // kernel 9: k_transpose stores G_B non-temporally (1)
     if (value != 0 && value != 1) return fail(FU_ERR_ARG, "fu_set_option: tr_nt must be 0 or 1");
     h->tr_nt = (int)value;
     return FU_OK;
