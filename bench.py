@@ -58,9 +58,12 @@ def parse(argv=None):
                     help="nodes (er: 1e6; rgg-dist: per GPU, 2^23; rmat: scale, 24; rr: 65536)")
     ap.add_argument("--m", type=int, default=4_000_000)
     ap.add_argument("--workload", default="auto",
-                    choices=["auto", "er", "rgg", "rmat", "rr", "rgg-dist", "pairwise"],
+                    choices=["auto", "er", "rgg", "rmat", "rr", "rgg-dist", "pairwise", "rgg-parts"],
                     help="auto = er at N = 1, rgg-dist at N > 1; rgg / rmat / rr = exploratory "
-                         "single-GPU graphs; pairwise = RR-64K tick replay (BASELINE configs[2])")
+                         "single-GPU graphs; pairwise = RR-64K tick replay (BASELINE configs[2]); "
+                         "rgg-parts = one GPU, RGG(--n, 2^28 by default) as --parts in-process "
+                         "partitions (graphs beyond one handle's 2^31 directed edges)")
+    ap.add_argument("--parts", type=int, default=2, help="rgg-parts: partitions on the one GPU")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--layout", default="auto", choices=["auto", "given", "degree"],
                     help="device node numbering: degree = relabelled by degree (hot estimates "
@@ -148,6 +151,8 @@ def main():
         sys.exit(2)
     if wl == "pairwise":
         return run_pairwise(args)
+    if wl == "rgg-parts":
+        return run_parts(args)
     return run_single(args, wl)
 
 
@@ -501,6 +506,81 @@ def run_dist(args, world, rank, local, dist):
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
+
+
+def run_parts(args):
+    """One GPU, one process: RGG(--n) cut into --parts x-slabs (fu_part_gen_rgg, no global
+    graph), each an in-process partition (fu_dist_create_local: its own handle and streams on
+    the same GPU, the halo copied into the neighbours' ghost slots on the comm streams beside
+    the interior tiles, fu_dist_run_local). For graphs beyond one handle's 2^31 directed edges
+    (RGG 2^28: 2.15e9). value = all partitions' edge updates / wall time of rounds 0..K-1."""
+    import fu
+    from fu.dist import DistCollectAll, RggPart, run_local
+
+    n = args.n or (1 << 28)
+    k = args.parts
+    t = time.perf_counter()
+    parts = [RggPart(n, avg_deg=8.0, seed=1, nparts=k, part=r) for r in range(k)]
+    vals = [p.values(seed=0) for p in parts]
+    t_gen = time.perf_counter() - t
+    e_tot = sum(p.e_local for p in parts)
+    print(f"[bench] rgg:n={n} as {k} partitions: E={e_tot} generated in {t_gen:.1f} s", file=sys.stderr, flush=True)
+    t = time.perf_counter()
+    engs = []
+    for p, v in zip(parts, vals):
+        engs.append(DistCollectAll(p.to_plan(), v, None, device=0))
+    for e in engs:
+        e.synchronize()
+    t_create = time.perf_counter() - t
+    if args.warmup:
+        run_local(engs, args.warmup)
+    for e in engs:
+        e.reset()
+    for e in engs:
+        e.synchronize()
+    for e in engs:
+        e.mark(0)
+    t = time.perf_counter()
+    run_local(engs, args.steps)
+    for e in engs:
+        e.mark(1)
+    for e in engs:
+        e.synchronize()
+    wall = time.perf_counter() - t
+    dev_ms = max(e.elapsed(0, 1) for e in engs)  # each partition's stream, events around the window
+    halo = sum(p.n_ghost_a for p in parts)
+    alg = 24 * e_tot + 28 * n + 8 * halo
+    per_round = dev_ms * 1e-3 / args.steps
+    kinfo = engs[0].info()
+    free = None
+    try:
+        import torch
+
+        free = [x / 2 ** 30 for x in torch.cuda.mem_get_info(0)]  # (free, total) GiB while resident
+    except Exception:  # noqa: BLE001
+        pass
+    for e in engs:
+        e.close()
+    line = {
+        "metric": METRIC, "value": e_tot * args.steps / wall, "unit": "edge-updates/s", "n_gpus": 1,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (seeded RGG, U[0,100) values)",
+        "config": {"workload": f"rgg-parts:n={n},deg=8 as {k} in-process x-slab partitions on one GPU "
+                               "(halo by device copies every round)",
+                   "n": n, "E_directed": e_tot, "parts": k, "E_per_part": [p.e_local for p in parts],
+                   "halo_estimates_per_round": halo, "kernel_selected": kinfo["kernel"],
+                   "tile_selected": kinfo["tile"], "rounds_timed": f"0-{args.steps - 1} from the zero state",
+                   "graph_gen_s": t_gen, "create_s": t_create, "hbm_free_total_GiB": free,
+                   "parallelism": f"{k} partitions, one GPU"},
+        "roofline": {"bound": "hbm", "achieved": alg / per_round / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": alg / per_round / 1e9 / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_launch": alg, "avg_launch_us": per_round * 1e6,
+                     "kernel": "k_round_recon per partition (own streams), halo copies on the comm streams",
+                     "launch_window": f"rounds 0-{args.steps - 1} (round 0 included), the slowest partition's events"},
+        "cpu_baseline": None,
+    }
+    print(json.dumps(line), flush=True)
 
 
 def weak_unit(args):

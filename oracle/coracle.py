@@ -37,6 +37,10 @@ def lib():
                                  _i32p, _i32p, ctypes.c_int64, ctypes.c_int32, _i32p, _f64p,
                                  _f64p, _f64p, _f64p]
         L.fuo_max_threads.restype = ctypes.c_int
+        L.fuo_rev64.argtypes = [ctypes.c_int32, _i64p, _i32p, _i64p, ctypes.c_int]
+        L.fuo_rev64.restype = ctypes.c_int64
+        L.fuo_ca_sync64.argtypes = [ctypes.c_int32, _i64p, _i32p, _i64p, _f64p, ctypes.c_int32,
+                                    _f64p, _f64p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -55,6 +59,29 @@ def ca_sync(rowptr, col, rev, values, rounds, nthreads=1):
                            _c(values, np.float64), int(rounds), a, f, int(nthreads))
     if rc != 0:
         raise RuntimeError(f"fuo_ca_sync failed ({rc})")
+    return a, f
+
+
+def rev64(rowptr, col, nthreads=1):
+    """The reverse-edge index as int64 (graphs of 2^31 or more directed edges)."""
+    rowptr = _c(rowptr, np.int64)
+    rev = np.empty(int(rowptr[-1]), dtype=np.int64)
+    bad = lib().fuo_rev64(len(rowptr) - 1, rowptr, _c(col, np.int32), rev, int(nthreads))
+    if bad:
+        raise ValueError(f"{bad} edges have no reverse edge")
+    return rev
+
+
+def ca_sync64(rowptr, col, rev, values, rounds, nthreads=1):
+    """ca_sync with an int64 reverse index (rev64): the same arithmetic."""
+    rowptr = _c(rowptr, np.int64)
+    n = len(rowptr) - 1
+    a = np.empty(n)
+    f = np.empty(int(rowptr[-1]))
+    rc = lib().fuo_ca_sync64(n, rowptr, _c(col, np.int32), _c(rev, np.int64),
+                             _c(values, np.float64), int(rounds), a, f, int(nthreads))
+    if rc != 0:
+        raise RuntimeError(f"fuo_ca_sync64 failed ({rc})")
     return a, f
 
 

@@ -41,6 +41,49 @@ static void round_ca(int32_t n, const int64_t *rowptr, const int32_t *col, const
   (void)nthreads;
 }
 
+/* The same round with a 64-bit reverse index (graphs of 2^31 or more directed edges, which
+ * the engine runs as partitions; the arithmetic is round_ca's). */
+static void round_ca64(int32_t n, const int64_t *rowptr, const int32_t *col, const int64_t *rev,
+                       const double *v, const double *f_old, const double *a_old,
+                       double *f_new, double *a_new, int nthreads) {
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1024) num_threads(nthreads)
+#endif
+  for (int32_t i = 0; i < n; ++i) {
+    int64_t b = rowptr[i], e = rowptr[i + 1];
+    double S = 0.0, T = 0.0;
+    for (int64_t k = b; k < e; ++k) {
+      S = S + (-f_old[rev[k]]);
+      T = T + a_old[col[k]];
+    }
+    double a = ((v[i] - S) + T) / (double)(e - b + 1);
+    a_new[i] = a;
+    for (int64_t k = b; k < e; ++k) f_new[k] = ((-f_old[rev[k]]) + a) - a_old[col[k]];
+  }
+  (void)nthreads;
+}
+
+/* rev[k] = the position of edge (col[k] -> i) for edge k = (i -> col[k]), 64-bit; the first
+ * match in row col[k] (simple graphs have one). Returns the number of edges without a reverse
+ * edge (0 for a symmetric graph). */
+int64_t fuo_rev64(int32_t n, const int64_t *rowptr, const int32_t *col, int64_t *rev, int nthreads) {
+  int64_t bad = 0;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 4096) num_threads(nthreads) reduction(+ : bad)
+#endif
+  for (int32_t i = 0; i < n; ++i) {
+    for (int64_t k = rowptr[i]; k < rowptr[i + 1]; ++k) {
+      const int32_t j = col[k];
+      int64_t q = rowptr[j], qe = rowptr[j + 1];
+      while (q < qe && col[q] != i) ++q;
+      if (q < qe) rev[k] = q;
+      else { rev[k] = -1; ++bad; }
+    }
+  }
+  (void)nthreads;
+  return bad;
+}
+
 /* Round 0: timeout fire on zero state (CA:33-34, CA:87-91). */
 static void round0_ca(int32_t n, const int64_t *rowptr, const double *v, double *f,
                       double *a, int nthreads) {
@@ -69,6 +112,28 @@ int fuo_ca_sync(int32_t n, const int64_t *rowptr, const int32_t *col, const int3
   round0_ca(n, rowptr, v, fa, aa, nthreads);
   for (int32_t r = 1; r < rounds; ++r) {
     round_ca(n, rowptr, col, rev, v, fa, aa, fb, ab, nthreads);
+    double *t = fa; fa = fb; fb = t;
+    t = aa; aa = ab; ab = t;
+  }
+  if (fa != f_out) memcpy(f_out, fa, sizeof(double) * (size_t)E);
+  if (aa != a_out) memcpy(a_out, aa, sizeof(double) * (size_t)n);
+  free(f2);
+  free(a2);
+  return 0;
+}
+
+/* fuo_ca_sync with a 64-bit reverse index (fuo_rev64). */
+int fuo_ca_sync64(int32_t n, const int64_t *rowptr, const int32_t *col, const int64_t *rev,
+                  const double *v, int32_t rounds, double *a_out, double *f_out, int nthreads) {
+  int64_t E = rowptr[n];
+  if (rounds <= 0) return -1;
+  double *f2 = (double *)malloc(sizeof(double) * (size_t)(E > 0 ? E : 1));
+  double *a2 = (double *)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+  if (!f2 || !a2) { free(f2); free(a2); return -2; }
+  double *fa = f_out, *aa = a_out, *fb = f2, *ab = a2;
+  round0_ca(n, rowptr, v, fa, aa, nthreads);
+  for (int32_t r = 1; r < rounds; ++r) {
+    round_ca64(n, rowptr, col, rev, v, fa, aa, fb, ab, nthreads);
     double *t = fa; fa = fb; fb = t;
     t = aa; aa = ab; ab = t;
   }

@@ -85,6 +85,10 @@ static void symmetric_from_pairs(int32_t n, const std::vector<uint32_t> &u,
 int build_rev(fu_graph &g) {
   const int32_t n = g.n;
   const int64_t E = g.rowptr[n];
+  if (E > (int64_t)INT32_MAX)  // rev is int32 (fu_graph_export): no silent truncation
+    return fail(FU_ERR_GRAPH, "graph has " + std::to_string(E) +
+                                  " directed edges, more than an int32 reverse index holds; run it as partitions "
+                                  "(fu_part_gen_rgg + fu_dist_create_local)");
   // sorted view of every row: perm[rowptr[i]..] = positions sorted by neighbour id
   std::vector<int32_t> perm(E);
   bool all_sorted = true;

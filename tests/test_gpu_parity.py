@@ -949,6 +949,50 @@ def test_rgg_2pow23_partition_unit_bitwise():
     d.close()
 
 
+@pytest.mark.timeout(1100)
+@pytest.mark.skipif(not os.environ.get("FU_BIG_GRAPH"), reason="set FU_BIG_GRAPH=1 (several minutes, ~90 GB of host memory)")
+def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
+    """A graph beyond one handle's 2^31 directed edges on one MI355X: RGG 2^28 (2.15e9
+    directed edges) as two in-process x-slab partitions (fu_part_gen_rgg, fu_dist_create_local,
+    fu_dist_run_local: the halo copied into the neighbour's ghost slots every round), rounds
+    0-19 bitwise against the C oracle (16 threads, 64-bit reverse index) on the global graph,
+    assembled from the slabs' rows in global numbering (the slab generator's rows are the
+    global generator's, test_dist_rgg_slabs_local_transport_bitwise)."""
+    from fu.dist import DistCollectAll, RggPart, run_local
+
+    n, k, rounds = 1 << 28, 2, 20
+    parts = [RggPart(n, avg_deg=8.0, seed=1, nparts=k, part=r) for r in range(k)]
+    E = sum(p.e_local for p in parts)
+    assert E > 2 ** 31 - 1
+    print(f"[big] {k} slabs, E = {E}", flush=True)  # progress lines: the run takes minutes
+    engs = [DistCollectAll(p.to_plan(), p.values(seed=0), None) for p in parts]
+    run_local(engs, rounds)
+    print("[big] rounds queued", flush=True)
+    got = [(p.lo, p.hi, e.estimates(), e.flows()) for p, e in zip(parts, engs)]
+    for e in engs:
+        e.close()
+    del engs
+    print("[big] estimates and flows read back", flush=True)
+    rowptr = np.empty(n + 1, dtype=np.int64)
+    col = np.empty(E, dtype=np.int32)
+    v = np.empty(n)
+    off = 0
+    for p in parts:
+        rowptr[p.lo:p.hi] = p.rowptr[:-1] + off
+        col[off:off + p.e_local] = p.global_col()
+        v[p.lo:p.hi] = p.values(seed=0)
+        off += p.e_local
+    rowptr[n] = off
+    del parts
+    rev = coracle.rev64(rowptr, col, 16)
+    print("[big] global CSR and reverse index built", flush=True)
+    a_ref, f_ref = coracle.ca_sync64(rowptr, col, rev, v, rounds, nthreads=16)
+    print("[big] C oracle done", flush=True)
+    for lo, hi, a, f in got:
+        assert np.array_equal(a, a_ref[lo:hi])
+        assert np.array_equal(f, f_ref[rowptr[lo]:rowptr[hi]])
+
+
 @pytest.mark.timeout(900)
 def test_rgg64m_single_gpu_properties():
     """BASELINE config 5's graph at full size on one GPU (2^26 nodes, E = 5.4e8): 10 rounds,

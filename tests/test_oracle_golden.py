@@ -30,6 +30,19 @@ def test_c_oracle_ca_sync(name, meta, threads):
         assert np.array_equal(f, d["flows"][k]), (name, r)
 
 
+@pytest.mark.parametrize("name,meta", ca_sync_fixtures())
+def test_c_oracle_ca_sync64(name, meta):
+    """The 64-bit reverse-index variant (graphs of 2^31 or more directed edges): its index
+    equals build_rev's and its rounds the same fixtures bitwise."""
+    d = load_npz(meta["file"])
+    rev = coracle.rev64(d["rowptr"], d["col"], 4)
+    assert np.array_equal(rev, oracle.build_rev(d["rowptr"], d["col"]).astype(np.int64))
+    for k, r in enumerate(int(x) for x in d["rounds"]):
+        a, f = coracle.ca_sync64(d["rowptr"], d["col"], rev, d["values"], r + 1, 4)
+        assert np.array_equal(a, d["last_avg"][k]), (name, r)
+        assert np.array_equal(f, d["flows"][k]), (name, r)
+
+
 @pytest.mark.parametrize("name,fn", tick_fixtures())
 def test_tick_emulator(name, fn):
     d = load_json(fn)
