@@ -960,6 +960,17 @@ def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
     global generator's, test_dist_rgg_slabs_local_transport_bitwise)."""
     from fu.dist import DistCollectAll, RggPart, run_local
 
+    import threading
+    import time
+
+    stop = threading.Event()
+
+    def beat():  # a line every 30 s: the oracle's C calls run for minutes (ctypes drops the GIL)
+        t0 = time.time()
+        while not stop.wait(30):
+            print(f"[big] {time.time() - t0:.0f} s", flush=True)
+
+    threading.Thread(target=beat, daemon=True).start()
     n, k, rounds = 1 << 28, 2, 20
     parts = [RggPart(n, avg_deg=8.0, seed=1, nparts=k, part=r) for r in range(k)]
     E = sum(p.e_local for p in parts)
@@ -988,6 +999,7 @@ def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
     print("[big] global CSR and reverse index built", flush=True)
     a_ref, f_ref = coracle.ca_sync64(rowptr, col, rev, v, rounds, nthreads=16)
     print("[big] C oracle done", flush=True)
+    stop.set()
     for lo, hi, a, f in got:
         assert np.array_equal(a, a_ref[lo:hi])
         assert np.array_equal(f, f_ref[rowptr[lo]:rowptr[hi]])
