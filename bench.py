@@ -64,6 +64,8 @@ def parse(argv=None):
                          "rgg-parts = one GPU, RGG(--n, 2^28 by default) as --parts in-process "
                          "partitions (graphs beyond one handle's 2^31 directed edges)")
     ap.add_argument("--parts", type=int, default=2, help="rgg-parts: partitions on the one GPU")
+    ap.add_argument("--deg", type=float, default=9.0,
+                    help="rgg-parts: average degree (9: RGG 2^28 has 2.4e9 directed edges, beyond 2^31)")
     ap.add_argument("--kernel", default="auto")
     ap.add_argument("--layout", default="auto", choices=["auto", "given", "degree"],
                     help="device node numbering: degree = relabelled by degree (hot estimates "
@@ -519,8 +521,9 @@ def run_parts(args):
 
     n = args.n or (1 << 28)
     k = args.parts
+    deg = args.deg
     t = time.perf_counter()
-    parts = [RggPart(n, avg_deg=8.0, seed=1, nparts=k, part=r) for r in range(k)]
+    parts = [RggPart(n, avg_deg=deg, seed=1, nparts=k, part=r) for r in range(k)]
     vals = [p.values(seed=0) for p in parts]
     t_gen = time.perf_counter() - t
     e_tot = sum(p.e_local for p in parts)
@@ -552,13 +555,8 @@ def run_parts(args):
     alg = 24 * e_tot + 28 * n + 8 * halo
     per_round = dev_ms * 1e-3 / args.steps
     kinfo = engs[0].info()
-    free = None
-    try:
-        import torch
-
-        free = [x / 2 ** 30 for x in torch.cuda.mem_get_info(0)]  # (free, total) GiB while resident
-    except Exception:  # noqa: BLE001
-        pass
+    fr, tot = fu.mem_info(0)  # while the partitions are resident
+    free = [fr / 2 ** 30, tot / 2 ** 30]
     for e in engs:
         e.close()
     line = {
@@ -566,7 +564,7 @@ def run_parts(args):
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall * 1e3 / args.steps,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
         "data": "synthetic (seeded RGG, U[0,100) values)",
-        "config": {"workload": f"rgg-parts:n={n},deg=8 as {k} in-process x-slab partitions on one GPU "
+        "config": {"workload": f"rgg-parts:n={n},deg={deg:g} as {k} in-process x-slab partitions on one GPU "
                                "(halo by device copies every round)",
                    "n": n, "E_directed": e_tot, "parts": k, "E_per_part": [p.e_local for p in parts],
                    "halo_estimates_per_round": halo, "kernel_selected": kinfo["kernel"],

@@ -41,6 +41,8 @@ const char *fu_last_error(void);
 int fu_version(void);
 /* Number of visible HIP devices (0 without a GPU; never an error on a CPU-only host). */
 int fu_device_count(int32_t *out);
+/* Free and total bytes of HBM on `device` (hipMemGetInfo): how large a graph still fits. */
+int fu_mem_info(int32_t device, int64_t *free_bytes, int64_t *total_bytes);
 
 /* ======================================================================================
  * Host graphs (native C++; no GPU needed)

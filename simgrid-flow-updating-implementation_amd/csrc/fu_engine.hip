@@ -3642,6 +3642,19 @@ int fu_get_round(fu_handle *h, int64_t *rounds_done) {
   return FU_OK;
 }
 
+int fu_mem_info(int32_t device, int64_t *free_bytes, int64_t *total_bytes) {
+  if (!free_bytes || !total_bytes) return fail(FU_ERR_ARG, "fu_mem_info: NULL argument");
+  int nd = 0;
+  if (hipGetDeviceCount(&nd) != hipSuccess || nd == 0) return fail(FU_ERR_HIP, "fu_mem_info: no HIP device visible");
+  if (device < 0 || device >= nd) return fail(FU_ERR_ARG, "fu_mem_info: bad device");
+  HIP_TRY(hipSetDevice(device));
+  size_t fr = 0, tot = 0;
+  HIP_TRY(hipMemGetInfo(&fr, &tot));
+  *free_bytes = (int64_t)fr;
+  *total_bytes = (int64_t)tot;
+  return FU_OK;
+}
+
 int fu_copy_bandwidth(int32_t device, int64_t bytes, int32_t iters, double *gbs) {
   FU_TRY_BEGIN
   if (!gbs || bytes < 16 * 1024 || iters < 1) return fail(FU_ERR_ARG, "fu_copy_bandwidth: bad arguments");

@@ -45,6 +45,7 @@ _SIGS = {
     "fu_last_error": ([], cp),
     "fu_version": ([], ctypes.c_int),
     "fu_device_count": ([P(i32)], ctypes.c_int),
+    "fu_mem_info": ([i32, P(i64), P(i64)], ctypes.c_int),
     "fu_graph_from_edges": ([i32, i64, vp, vp, P(vp)], ctypes.c_int),
     "fu_graph_from_csr": ([i32, vp, vp, i32, P(vp)], ctypes.c_int),
     "fu_graph_gen_er": ([i32, i64, u64, P(vp)], ctypes.c_int),
@@ -144,6 +145,13 @@ def copy_bandwidth(device: int = 0, nbytes: int = 1 << 30, iters: int = 5) -> fl
     g = f64(0.0)
     call("fu_copy_bandwidth", int(device), int(nbytes), int(iters), ctypes.byref(g))
     return float(g.value)
+
+
+def mem_info(device: int = 0) -> tuple:
+    """(free, total) bytes of HBM on the device."""
+    fr, tot = i64(0), i64(0)
+    call("fu_mem_info", int(device), ctypes.byref(fr), ctypes.byref(tot))
+    return int(fr.value), int(tot.value)
 
 
 def device_count() -> int:

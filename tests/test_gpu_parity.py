@@ -952,8 +952,9 @@ def test_rgg_2pow23_partition_unit_bitwise():
 @pytest.mark.timeout(1100)
 @pytest.mark.skipif(not os.environ.get("FU_BIG_GRAPH"), reason="set FU_BIG_GRAPH=1 (several minutes, ~90 GB of host memory)")
 def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
-    """A graph beyond one handle's 2^31 directed edges on one MI355X: RGG 2^28 (2.15e9
-    directed edges) as two in-process x-slab partitions (fu_part_gen_rgg, fu_dist_create_local,
+    """A graph beyond one handle's 2^31 directed edges on one MI355X: RGG 2^28 at average
+    degree 9 (2.4e9 directed edges; at degree 8 it has 2,147,384,282, just under 2^31) as two
+    in-process x-slab partitions (fu_part_gen_rgg, fu_dist_create_local,
     fu_dist_run_local: the halo copied into the neighbour's ghost slots every round), rounds
     0-19 bitwise against the C oracle (16 threads, 64-bit reverse index) on the global graph,
     assembled from the slabs' rows in global numbering (the slab generator's rows are the
@@ -972,7 +973,7 @@ def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
 
     threading.Thread(target=beat, daemon=True).start()
     n, k, rounds = 1 << 28, 2, 20
-    parts = [RggPart(n, avg_deg=8.0, seed=1, nparts=k, part=r) for r in range(k)]
+    parts = [RggPart(n, avg_deg=9.0, seed=1, nparts=k, part=r) for r in range(k)]
     E = sum(p.e_local for p in parts)
     assert E > 2 ** 31 - 1
     print(f"[big] {k} slabs, E = {E}", flush=True)  # progress lines: the run takes minutes
