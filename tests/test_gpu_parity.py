@@ -272,6 +272,37 @@ def test_engine_small_platform_watcher_lines(tmp_path, mode, tag):
     assert np.max(np.abs(res["last_avg"] - 190 / 6)) / (190 / 6) < 1e-12
 
 
+@pytest.mark.parametrize("mode", ["ca", "pw"])
+def test_cli_reference_inputs_watcher_lines(tmp_path, monkeypatch, capsys, mode):
+    """`python -m fu collectall|pairwise` run where the reference runs (./platforms/
+    small_platform.xml, ./actors.xml: CA:154,157) prints the reference's watcher lines
+    (CA:134-142) at t = 10 ... 1000; `--sync` and `bench-graph` run too."""
+    from fu.__main__ import main
+
+    d = load_json(f"tick_small_platform_{mode}_fwd.json")
+    (tmp_path / "platforms").mkdir()
+    write_platform_xml(tmp_path / "platforms" / "small_platform.xml")
+    write_deployment_xml(tmp_path / "actors.xml", d["actors"])
+    monkeypatch.chdir(tmp_path)
+    assert main(["collectall" if mode == "ca" else "pairwise"]) == 0
+    out = capsys.readouterr().out.splitlines()
+    watch = [ln for ln in out if ":watcher:" in ln and ("last_avg{" in ln or "value{" in ln)]
+    by_t = {}
+    for ln in watch:
+        by_t.setdefault(float(ln.split()[1].rstrip("]")), []).append(ln.split("] ", 2)[2])
+    names = d["names"]
+    vd = {nm: float(a[1]) for nm, a in zip(names, d["actors"])}
+    for t in range(10, 1001, 10):
+        la = {names[k]: v for k, v in zip(d["snap_keys"][t], d["snap_vals"][t])}
+        assert by_t[float(t)] == [f"value{vd}"] + ([f"last_avg{la}"] if la else []), t
+    if mode == "ca":
+        assert main(["collectall", "--sync", "--rounds", "200"]) == 0
+        assert "last_avg{" in capsys.readouterr().out
+        assert main(["bench-graph", "rr:n=4096,d=8", "--rounds", "50"]) == 0
+        line = capsys.readouterr().out
+        assert "n=4096" in line and "edge_updates/s=" in line and "max_err=" in line
+
+
 def test_full_size_er1m_convergence_and_prefix_parity():
     """BASELINE config 2 at full size: ER n=1e6 m=4e6. Bitwise vs the C oracle for 60 rounds,
     then the 1000-round run converges to the per-component means (< 1e-9)."""
