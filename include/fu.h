@@ -242,16 +242,27 @@ int fu_trace_build_routes(int32_t n, const int64_t *decl_rowptr, const int32_t *
  * with no bandwidth, then msg_bytes at the max-min fair share of bw_factor * bandwidth on
  * every shared link it crosses (capped by its FATPIPE links); it is consumed at the first tick
  * after its end. Alone, a transfer takes the per-route time above (SimGrid LV08: lat_factor
- * 13.01, bw_factor 0.97, 154-byte messages). Deviation from LV08: every flow on a link gets an
- * EQUAL max-min share; SimGrid weights each flow's share by its sharing penalty (route latency
- * plus weight_S / bandwidth per link), so two flows of different routes on one link get
- * different rates here than in SimGrid. The reference platform's 154-byte transfers all end
- * within one tick, where the two agree (the plain schedule); no TCP-window bound either. */
+ * 13.01, bw_factor 0.97, 154-byte messages). Every flow on a link gets an EQUAL max-min
+ * share here; fu_trace_build_links_ex adds LV08's weighting by sharing penalty and the TCP
+ * window bound (the drop-in Engine uses it). The reference platform's 154-byte transfers all
+ * end within one tick, where every variant gives the plain schedule. */
 int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
                          int32_t ticks, const char *order, const char *faults, int32_t n_links,
                          const double *link_bw, const double *link_lat, const int32_t *link_shared,
                          const int64_t *route_off, const int32_t *route_links, double msg_bytes,
                          double lat_factor, double bw_factor, fu_trace **out);
+/* fu_trace_build_links with SimGrid LV08's weighted sharing: a transfer's share of a shared
+ * link is proportional to 1 / its sharing penalty, the route's latency sum + weight_S /
+ * bandwidth of each of its links (LV08: weight_S = 20537), and with tcp_gamma > 0 its rate
+ * is capped at tcp_gamma / (2 * latency sum), the TCP window (LV08: 4194304). weight_S = 0
+ * and tcp_gamma = 0 are fu_trace_build_links. Parity-unpinned (SimGrid is not installable
+ * offline); oracle/oracle.py's LinkNet restates it operation for operation. */
+int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                            int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                            const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                            const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                            double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
+                            fu_trace **out);
 int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed);
 /* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
  * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */

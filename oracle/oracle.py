@@ -196,10 +196,11 @@ class LinkNet:
     """Link-sharing transfer model (fu_trace.cpp LinkNet), restated
     operation for operation so both give the same doubles: a transfer matched at tick t has
     a latency phase of lat_factor * sum(latency), then `bytes` at its max-min fair share of
-    bw_factor * bandwidth on the shared links it crosses, capped by its FATPIPE links.
-    Every flow on a link gets an equal share (plain max-min); SimGrid's LV08 weights shares by
-    each flow's sharing penalty -- a documented deviation (fu.h). Parity-unpinned against
-    SimGrid (not installable offline)."""
+    bw_factor * bandwidth on the shared links it crosses, capped by its FATPIPE links and,
+    with tcp_gamma > 0, by the TCP window tcp_gamma / (2 * latency sum). Shares are weighted
+    by 1 / the flow's sharing penalty, LV08's latency sum + weight_S / bandwidth over its
+    links (weight_S = 0: penalty 1, equal shares). Parity-unpinned against SimGrid (not
+    installable offline)."""
 
     def __init__(self, net):
         self.n = int(net["n"])
@@ -211,6 +212,8 @@ class LinkNet:
         self.bytes = float(net.get("bytes", 154.0))
         self.lat_factor = float(net.get("lat_factor", 13.01))
         self.bw_factor = float(net.get("bw_factor", 0.97))
+        self.weight_S = float(net.get("weight_S", 0.0))
+        self.tcp_gamma = float(net.get("tcp_gamma", 0.0))
         self.active = []  # flows (dicts) not done, in start order
         self.now = 0.0
 
@@ -220,13 +223,17 @@ class LinkNet:
     def start(self, src, dst, t):
         r = src * self.n + dst
         f = {"r": r, "rate": 0.0, "end": math.inf, "phase": 0, "rem": self.bytes}
-        lsum, cap = 0.0, math.inf
+        lsum, cap, sw = 0.0, math.inf, 0.0
         for k in self.links(f):
             lsum = lsum + self.lat[k]
+            sw = sw + self.weight_S / self.bw[k]
             if not self.shared[k]:
                 cap = min(cap, self.bw_factor * self.bw[k])
+        if self.tcp_gamma > 0.0 and lsum > 0.0:
+            cap = min(cap, self.tcp_gamma / (2.0 * lsum))
         f["lat_end"] = t + self.lat_factor * lsum
         f["cap"] = cap
+        f["pen"] = lsum + sw if self.weight_S > 0.0 else 1.0
         if self.roff[r] == self.roff[r + 1]:  # same host: no transfer
             f["phase"], f["end"] = 2, t
             return f
@@ -237,31 +244,34 @@ class LinkNet:
         nl = len(self.bw)
         crem = [self.bw_factor * self.bw[k] for k in range(nl)]
         cnt = [0] * nl
+        use = [0.0] * nl
         un = [f for f in self.active if f["phase"] == 1]
         for f in un:
             for k in self.links(f):
                 if self.shared[k]:
                     cnt[k] += 1
+                    use[k] = use[k] + 1.0 / f["pen"]
         while un:
             best = math.inf
             for k in range(nl):
                 if cnt[k] > 0:
-                    best = min(best, max(0.0, crem[k] / cnt[k]))
+                    best = min(best, max(0.0, crem[k] / use[k]))
             for f in un:
-                best = min(best, f["cap"])
+                best = min(best, f["cap"] * f["pen"])
             keep, fix = [], []
             for f in un:
-                b = f["cap"] == best
+                b = f["cap"] * f["pen"] == best
                 for k in self.links(f):
                     if b:
                         break
-                    b = bool(self.shared[k]) and cnt[k] > 0 and max(0.0, crem[k] / cnt[k]) == best
+                    b = bool(self.shared[k]) and cnt[k] > 0 and max(0.0, crem[k] / use[k]) == best
                 (fix if b else keep).append(f)
             for f in fix:
-                f["rate"] = best
+                f["rate"] = f["cap"] if f["cap"] * f["pen"] == best else best / f["pen"]
                 for k in self.links(f):
                     if self.shared[k]:
-                        crem[k] = crem[k] - best
+                        crem[k] = crem[k] - f["rate"]
+                        use[k] = use[k] - 1.0 / f["pen"]
                         cnt[k] -= 1
             un = keep
 

@@ -61,8 +61,11 @@ using namespace fu;
 // starts its transfer at time t: a latency phase of lat_factor * sum(route latencies) with
 // no bandwidth, then `bytes` at the rate max-min fair sharing gives it. A shared link l
 // offers bw_factor * bw_l to the transfers in their data phase that cross it, split by
-// progressive filling; a FATPIPE link caps each transfer at bw_factor * bw_l without
-// sharing. Rates change only when a transfer enters or leaves its data phase. Alone, a
+// weighted progressive filling: a transfer's share is proportional to 1 / its sharing
+// penalty, LV08's route latency sum + weight_S / bw_k over its links (weight_S = 0: equal
+// shares); a FATPIPE link caps each transfer at bw_factor * bw_l without sharing, and with
+// tcp_gamma > 0 the TCP window caps it at tcp_gamma / (2 * route latency sum) (SimGrid's
+// CM02 / LV08 bounds). Rates change only when a transfer enters or leaves its data phase. Alone, a
 // transfer takes lat_factor * sum(lat) + bytes / (bw_factor * min bw), the fixed per-route
 // time of fu_trace_build_routes. The message is consumed at the first tick > its end
 // (CA:76: the actor tests the receive once per tick). oracle/oracle.py (LinkNet) mirrors
@@ -74,11 +77,13 @@ struct LinkNet {
   const int64_t *roff = nullptr;
   const int32_t *rl = nullptr;
   double bytes = 154.0, lat_factor = 13.01, bw_factor = 0.97;
+  double weight_S = 0.0, tcp_gamma = 0.0;  // LV08: 20537 and 4194304 (fu/platform.py)
   struct Flow {
     int64_t r;         // route index src * n + dst
     double lat_end;    // end of the latency phase
     double rem;        // bytes left (data phase)
-    double cap;        // FATPIPE cap (inf: none)
+    double cap;        // FATPIPE / TCP-window cap (inf: none)
+    double pen;        // sharing penalty (1 with weight_S = 0: equal shares)
     double rate;
     double end;        // completion time (inf while running)
     int phase;         // 0 latency, 1 data, 2 done
@@ -91,14 +96,17 @@ struct LinkNet {
     if ((int32_t)fl.size() <= id) fl.resize(id + 1);
     Flow &f = fl[id];
     f.r = (int64_t)src * n + dst;
-    double l = 0.0, cap = std::numeric_limits<double>::infinity();
+    double l = 0.0, cap = std::numeric_limits<double>::infinity(), sw = 0.0;
     for (int64_t k = roff[f.r]; k < roff[f.r + 1]; ++k) {
       l = l + lat[rl[k]];
+      sw = sw + weight_S / bw[rl[k]];
       if (!shared[rl[k]]) cap = std::min(cap, bw_factor * bw[rl[k]]);
     }
+    if (tcp_gamma > 0.0 && l > 0.0) cap = std::min(cap, tcp_gamma / (2.0 * l));
     f.lat_end = t + lat_factor * l;
     f.rem = bytes;
     f.cap = cap;
+    f.pen = weight_S > 0.0 ? l + sw : 1.0;
     f.rate = 0.0;
     f.end = std::numeric_limits<double>::infinity();
     f.phase = 0;
@@ -109,40 +117,46 @@ struct LinkNet {
     }
     active.push_back(id);
   }
-  // progressive filling over the data-phase transfers, every flow on a link with an EQUAL
-  // share (plain max-min). SimGrid's LV08 weights a flow's share by its sharing penalty (route
-  // latency + weight_S / bandwidth per link): a documented deviation (fu.h), parity-unpinned;
-  // it changes nothing while every transfer ends within its tick (the reference platform)
+  // weighted progressive filling over the data-phase transfers (SimGrid's LMM max-min):
+  // a link's level is its remaining capacity / the sum of 1 / penalty of its unfixed
+  // transfers; the lowest level (or a transfer's cap * penalty) fixes the transfers it
+  // binds at level / penalty (or their cap). weight_S = 0 gives every penalty 1: plain
+  // max-min, equal shares. Parity-unpinned against SimGrid (fu.h)
   void rates() {
-    std::vector<double> crem(n_links, 0.0);
+    std::vector<double> crem(n_links, 0.0), use(n_links, 0.0);
     std::vector<int32_t> cnt(n_links, 0);
     std::vector<int32_t> un;
     for (int32_t id : active) {
       if (fl[id].phase != 1) continue;
       un.push_back(id);
       for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1]; ++k)
-        if (shared[rl[k]]) cnt[rl[k]]++;
+        if (shared[rl[k]]) {
+          cnt[rl[k]]++;
+          use[rl[k]] = use[rl[k]] + 1.0 / fl[id].pen;
+        }
     }
     for (int32_t l = 0; l < n_links; ++l) crem[l] = bw_factor * bw[l];
     while (!un.empty()) {
       double best = std::numeric_limits<double>::infinity();
       for (int32_t l = 0; l < n_links; ++l)
-        if (cnt[l] > 0) best = std::min(best, std::max(0.0, crem[l] / cnt[l]));
-      for (int32_t id : un) best = std::min(best, fl[id].cap);
+        if (cnt[l] > 0) best = std::min(best, std::max(0.0, crem[l] / use[l]));
+      for (int32_t id : un) best = std::min(best, fl[id].cap * fl[id].pen);
       std::vector<int32_t> keep, fix;
       for (int32_t id : un) {
-        bool b = fl[id].cap == best;
+        bool b = fl[id].cap * fl[id].pen == best;
         for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1] && !b; ++k) {
           const int32_t l = rl[k];
-          b = shared[l] && cnt[l] > 0 && std::max(0.0, crem[l] / cnt[l]) == best;
+          b = shared[l] && cnt[l] > 0 && std::max(0.0, crem[l] / use[l]) == best;
         }
         (b ? fix : keep).push_back(id);
       }
       for (int32_t id : fix) {
-        fl[id].rate = best;
-        for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1]; ++k)
+        Flow &f = fl[id];
+        f.rate = f.cap * f.pen == best ? f.cap : best / f.pen;
+        for (int64_t k = roff[f.r]; k < roff[f.r + 1]; ++k)
           if (shared[rl[k]]) {
-            crem[rl[k]] = crem[rl[k]] - best;
+            crem[rl[k]] = crem[rl[k]] - f.rate;
+            use[rl[k]] = use[rl[k]] - 1.0 / f.pen;
             cnt[rl[k]]--;
           }
       }
@@ -453,9 +467,20 @@ int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *d
                          const double *link_bw, const double *link_lat, const int32_t *link_shared,
                          const int64_t *route_off, const int32_t *route_links, double msg_bytes,
                          double lat_factor, double bw_factor, fu_trace **out) {
+  return fu_trace_build_links_ex(n, decl_rowptr, decl_col, mode, ticks, order, faults, n_links, link_bw, link_lat,
+                                 link_shared, route_off, route_links, msg_bytes, lat_factor, bw_factor, 0.0, 0.0, out);
+}
+
+int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                            int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                            const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                            const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                            double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
+                            fu_trace **out) {
   FU_TRY_BEGIN
   if (n <= 0 || n_links < 0 || !route_off || (n_links > 0 && (!link_bw || !link_lat || !link_shared)) ||
-      !(msg_bytes >= 0.0) || !(lat_factor >= 0.0) || !(bw_factor > 0.0))
+      !(msg_bytes >= 0.0) || !(lat_factor >= 0.0) || !(bw_factor > 0.0) || !(weight_S >= 0.0) ||
+      !(tcp_gamma >= 0.0))
     return fail(FU_ERR_ARG, "fu_trace_build_links: bad arguments");
   const int64_t nr = (int64_t)n * n;
   if (route_off[0] != 0) return fail(FU_ERR_ARG, "fu_trace_build_links: route_off[0] must be 0");
@@ -479,6 +504,8 @@ int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *d
   net.bytes = msg_bytes;
   net.lat_factor = lat_factor;
   net.bw_factor = bw_factor;
+  net.weight_S = weight_S;
+  net.tcp_gamma = tcp_gamma;
   return build_trace(n, decl_rowptr, decl_col, mode, ticks, order, faults, nullptr, &net, out);
   FU_TRY_END
 }

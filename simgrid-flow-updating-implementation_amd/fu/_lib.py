@@ -82,6 +82,8 @@ _SIGS = {
     "fu_trace_build_routes": ([i32, vp, vp, i32, i32, cp, cp, vp, P(vp)], ctypes.c_int),
     "fu_trace_build_links": ([i32, vp, vp, i32, i32, cp, cp, i32, vp, vp, vp, vp, vp, f64, f64, f64, P(vp)],
                              ctypes.c_int),
+    "fu_trace_build_links_ex": ([i32, vp, vp, i32, i32, cp, cp, i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, f64,
+                                 P(vp)], ctypes.c_int),
     "fu_trace_fault_stats": ([vp, P(i64), P(i64)], ctypes.c_int),
     "fu_trace_info": ([vp, vp], ctypes.c_int),
     "fu_trace_export": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),

@@ -21,6 +21,8 @@ _UNITS_T = {"": 1.0, "s": 1.0, "ms": 1e-3, "us": 1e-6, "ns": 1e-9, "ps": 1e-12,
 
 # LV08 network model defaults of SimGrid (latency factor, bandwidth factor).
 LV08_LATENCY_FACTOR = 13.01
+LV08_WEIGHT_S = 20537.0     # sharing penalty: latency sum + weight_S / bandwidth per route link
+TCP_GAMMA = 4194304.0       # TCP window: a transfer's rate <= gamma / (2 * latency sum)
 LV08_BANDWIDTH_FACTOR = 0.97
 
 
@@ -75,7 +77,8 @@ class Platform:
         """The link model of fu_trace_build_links for the actors on `hosts` (in actor order):
         every link (bandwidth, latency, shared unless FATPIPE) and the route of every host
         pair (empty for a host to itself). Concurrent transfers share the links' bandwidth
-        (max-min fair); alone, a transfer takes route_time. pairs: the (i, j) actor pairs
+        (max-min fair, each share weighted by 1 / LV08's sharing penalty, rates capped by the
+        TCP window); alone, a transfer takes route_time (below the TCP-window cap). pairs: the (i, j) actor pairs
         that exchange messages (None = all): only they need a route; the others stay empty.
         A pair with no route in the platform also stays empty, i.e. its messages arrive within
         one tick, the plain schedule of the reference platform (CA:76) -- the tolerance of the
@@ -95,7 +98,8 @@ class Platform:
                 "shared": np.array([0 if k in self.fatpipe else 1 for k in ids], dtype=np.int32),
                 "route_off": np.array(off, dtype=np.int64), "route_links": np.array(lst, dtype=np.int32),
                 "bytes": float(size_bytes), "lat_factor": LV08_LATENCY_FACTOR,
-                "bw_factor": LV08_BANDWIDTH_FACTOR, "n": n}
+                "bw_factor": LV08_BANDWIDTH_FACTOR, "weight_S": LV08_WEIGHT_S, "tcp_gamma": TCP_GAMMA,
+                "n": n}
 
 
 def load_platform(path: str) -> Platform:

@@ -228,8 +228,8 @@ class Engine:
     def _link_net(self, names, decl_rp, decl_col):
         """The platform's links and the routes of every pair of actors that exchange messages
         (declared neighbours, both directions: replies go back to the sender), for
-        fu_trace_build_links: concurrent transfers share link bandwidth (SimGrid LV08 factors,
-        fu/platform.py). On the reference platform every transfer ends within a tick, so the
+        fu_trace_build_links_ex: concurrent transfers share link bandwidth (SimGrid LV08
+        factors, shares weighted by the sharing penalty, the TCP window: fu/platform.py). On the reference platform every transfer ends within a tick, so the
         schedule is the plain one (CA:76)."""
         src = np.repeat(np.arange(len(names)), np.diff(decl_rp))
         pairs = set(zip(src.tolist(), np.asarray(decl_col).tolist()))

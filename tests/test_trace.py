@@ -203,10 +203,11 @@ def _random_net(n, seed, slow):
             "bw_factor": 0.97}
 
 
+@pytest.mark.parametrize("lv08", [False, True])
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
 @pytest.mark.parametrize("order", ["fwd", "rand:5"])
 @pytest.mark.parametrize("seed", [1, 2])
-def test_link_sharing_matches_emulator(mode, order, seed):
+def test_link_sharing_matches_emulator(mode, order, seed, lv08):
     """Link sharing (§8(f) row 3, fu_trace_build_links): concurrent transfers split the
     shared links' bandwidth max-min fairly (FATPIPE links cap each transfer alone), so a
     message's delivery tick depends on the traffic beside it. The native builder and the
@@ -217,6 +218,8 @@ def test_link_sharing_matches_emulator(mode, order, seed):
     names, vals, rp, col = fixture_decl_csr(d)
     n = len(names)
     net = _random_net(n, seed, slow=True)
+    if lv08:  # shares weighted by the sharing penalty, the TCP window (fu_trace_build_links_ex)
+        net = dict(net, weight_S=fu.platform.LV08_WEIGHT_S, tcp_gamma=fu.platform.TCP_GAMMA)
     faults = "drop=0.05,delay=3:0.05,seed=4" if seed == 2 else None
     em = oracle.TickEmulator(d["actors"], "ca" if mode == "collectall" else "pw", faults=faults, net=net)
     snaps = {}
@@ -246,6 +249,10 @@ def test_link_sharing_matches_emulator(mode, order, seed):
     alone = fu.Trace(rp, col, mode, 2000, order, faults=faults, route_s=rt).arrays()
     assert not (np.array_equal(alone["tick_task_off"], a["tick_task_off"])
                 and np.array_equal(alone["events"], a["events"]))
+    if lv08:  # and the weighting matters: equal shares give another schedule
+        eq = fu.Trace(rp, col, mode, 2000, order, faults=faults, net=_random_net(n, seed, slow=True)).arrays()
+        assert not (np.array_equal(eq["tick_task_off"], a["tick_task_off"])
+                    and np.array_equal(eq["events"], a["events"]))
 
 
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
@@ -287,6 +294,36 @@ def test_link_model_single_transfer_time_and_sharing():
     f1, f2 = ln.start(1, 2, 0.0), ln.start(2, 1, 0.0)  # both on FATPIPE link 1
     ln.advance_to(10.0)
     assert f1["end"] == f2["end"] == pytest.approx(154.0 / 97.0)
+
+
+def test_link_model_lv08_weights_and_tcp_window():
+    """LV08's weighting: two transfers on one shared link split it in proportion to 1 / their
+    sharing penalties (latency sum + weight_S / bandwidth of each route link), so the one
+    that also crosses a slow FATPIPE link gets the smaller share; the TCP window caps a
+    transfer at gamma / (2 * latency sum). Weighted schedules differ from equal shares."""
+    W, G = fu.platform.LV08_WEIGHT_S, fu.platform.TCP_GAMMA
+    # links: 0 shared (1000 B/s, 10 ms), 1 FATPIPE (2000 B/s, 0 s); route 0->1: [0],
+    # route 1->0: [0, 1] (0 -> 2 and the rest: unused)
+    net = {"n": 3, "bw": np.array([1000.0, 2000.0]), "lat": np.array([0.01, 0.0]), "shared": np.array([1, 0]),
+           "route_off": np.array([0, 0, 1, 1, 3, 3, 3, 3, 3, 3]), "route_links": np.array([0, 0, 1]),
+           "bytes": 1e6, "lat_factor": 13.01, "bw_factor": 0.97, "weight_S": W, "tcp_gamma": 0.0}
+    ln = oracle.LinkNet(net)
+    f1, f2 = ln.start(0, 1, 0.0), ln.start(1, 0, 0.0)
+    ln.advance_to(0.2)  # both past their latency phase (13.01 x 10 ms)
+    p1, p2 = 0.01 + W / 1000.0, 0.01 + W / 1000.0 + W / 2000.0
+    assert f1["pen"] == p1 and f2["pen"] == p2
+    assert f1["rate"] / f2["rate"] == pytest.approx(p2 / p1)
+    assert f1["rate"] + f2["rate"] == pytest.approx(0.97 * 1000.0)
+    eq = oracle.LinkNet(dict(net, weight_S=0.0))
+    g1, g2 = eq.start(0, 1, 0.0), eq.start(1, 0, 0.0)
+    eq.advance_to(0.2)
+    assert g1["rate"] == g2["rate"] == 0.97 * 1000.0 / 2
+    # the TCP window: gamma / (2 x 10 ms) = 210 MB/s caps a 1 GB/s link
+    fast = dict(net, bw=np.array([1e9, 2e9]), tcp_gamma=G)
+    ln = oracle.LinkNet(fast)
+    f = ln.start(0, 1, 0.0)
+    ln.advance_to(0.2)
+    assert f["rate"] == G / (2.0 * 0.01) < 0.97 * 1e9
 
 
 def test_link_model_argument_checks():
