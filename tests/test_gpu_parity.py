@@ -1039,10 +1039,14 @@ def test_rgg_2pow28_two_partitions_one_gpu_bitwise():
 
 @pytest.mark.timeout(900)
 def test_rgg64m_single_gpu_properties():
-    """BASELINE config 5's graph at full size on one GPU (2^26 nodes, E = 5.4e8): 10 rounds,
-    finite estimates, the flow bookkeeping (Σ a + Σ f = Σ v: mass conserved counting the flows
-    in flight), and the mean of the values recovered to 1e-9 by the math.fsum means."""
+    """BASELINE config 5's graph at full size on one GPU (2^26 nodes, E = 5.4e8): 10 rounds
+    on the single-GPU engine bitwise against the C oracle, with finite estimates, the flow
+    bookkeeping (Σ a + Σ f = Σ v: mass conserved counting the flows in flight) and the mean of
+    the values recovered to 1e-9; then rounds 0-19 through the partitioned path at one rank
+    (the `--workload rgg-dist --strong` line: slab generator, RCCL communicator) bitwise."""
     import math
+
+    from fu.dist import DistCollectAll, RggPart, unique_id
 
     n = 1 << 26
     g = fu.Graph.random_geometric(n, avg_deg=8.0, seed=1)
@@ -1056,6 +1060,17 @@ def test_rgg64m_single_gpu_properties():
     mean_v = math.fsum(v.tolist()) / n
     mass = (math.fsum(a.tolist()) + float(np.sum(f))) / n
     assert abs(mass - mean_v) < 1e-9 * mean_v
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 10, nthreads=16)
+    assert np.array_equal(a, a_ref)
+    assert np.array_equal(f, f_ref)
+    del a, f
+    part = RggPart(n, avg_deg=8.0, seed=1, nparts=1, part=0)
+    d = DistCollectAll(part.to_plan(), part.values(seed=0), unique_id())
+    d.run(20)
+    coracle.ca_rounds(g.rowptr, g.col, g.rev, v, 10, a_ref, f_ref, nthreads=16)
+    assert np.array_equal(d.estimates(), a_ref)
+    assert np.array_equal(d.flows(), f_ref)
+    d.close()
 
 
 @pytest.mark.parametrize("seed", range(12))
