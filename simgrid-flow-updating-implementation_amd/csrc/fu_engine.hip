@@ -869,7 +869,10 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
 // kernel 4 heavy tiles in a launch of their own. Results are bitwise those of kernel 4.
 // ------------------------------------------------------------------------------------
 constexpr int kStageThreads = 1024;   // one block per CU (the slice takes 128 KB of its LDS)
-constexpr int kStageU = 4;            // steps per lane in flight
+#ifndef FU_STAGE_U  // experiment builds: steps per lane in flight
+#define FU_STAGE_U 4
+#endif
+constexpr int kStageU = FU_STAGE_U;   // steps per lane in flight
 
 struct StageArgs {
   int P[4], Q[4], SN[4], NB[4];        // slices, blocks per slice, nodes per slice, blocks
