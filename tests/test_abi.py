@@ -119,6 +119,8 @@ def test_device_entry_points_fail_loudly_without_gpu():
     tr = fu.Trace(g.rowptr, g.col, "pairwise", 60)
     with pytest.raises(fu.FuError, match="no HIP device"):
         fu.Replay(tr, np.ones(g.n))
+    with pytest.raises(fu.FuError, match="no HIP device"):
+        fu.mem_info(0)
 
 
 def test_null_arguments_are_errors():

@@ -113,6 +113,21 @@ def test_first_rounds_flows_each_round(kernel):
     eng.close()
 
 
+def test_mem_info_tracks_a_handle():
+    """fu_mem_info: the device's HBM (288 GB on an MI355X), and a handle's device memory
+    shows as used while it lives."""
+    free0, total = fu.mem_info(0)
+    assert 0 < free0 <= total and total > 200 * 2 ** 30
+    g = fu.Graph.erdos_renyi(1_000_000, 4_000_000, seed=1)
+    eng = fu.CollectAll(g, fu.uniform_values(g.n, seed=0))
+    eng.run(2)
+    free1, _ = fu.mem_info(0)
+    assert free1 < free0 - 100 * 2 ** 20  # flows, estimates, tables: > 100 MB for ER-1M
+    eng.close()
+    with pytest.raises(fu.FuError, match="bad device"):
+        fu.mem_info(99)
+
+
 def test_nan_propagates_to_err():
     g = fu.Graph.random_regular(256, 4, seed=1)
     v = fu.uniform_values(g.n, seed=0)
