@@ -915,28 +915,27 @@ __device__ __forceinline__ unsigned col_at(const ColVec<EPL> &c, int j) {
 // Steps per batch: enough that every lane keeps 64 B of column loads in flight whatever the
 // element width (4 steps of 4-byte loads for doubles left 16 KB in flight per CU, ~2 TB/s at
 // HBM latency).
-template <typename T, int UB = kStageU>  // UB: k_stage<64 KB> (two blocks per CU, 64 VGPRs) halves it
+template <typename T>
 struct StageU {
   static constexpr int EPL = 16 / (int)sizeof(T);
-  static constexpr int U = EPL >= 8 ? UB : UB * 8 / EPL;
-  using Cols = ColVec<EPL>;
+  static constexpr int U = EPL >= 8 ? kStageU : kStageU * 8 / EPL;
 };
 
 // One batch: U steps of EPL elements per lane, all column loads first (caller), then the
 // LDS (or global) lookups and one 16-byte store per step.
-template <typename T, bool LDS, typename SU>  // SU = StageU<T, UB>
-__device__ __forceinline__ void stage_load(typename SU::Cols (&c)[SU::U], int g, int g1,
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_load(ColVec<StageU<T>::EPL> (&c)[StageU<T>::U], int g, int g1,
                                            const unsigned short *__restrict__ colS) {
-  constexpr int EPL = SU::EPL, U = SU::U, STEP = kStageThreads * EPL;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, STEP = kStageThreads * EPL;
 #pragma unroll
   for (int u = 0; u < U; ++u)
     if (g + u * STEP < g1) ld_cols<EPL>(c[u], colS + g + u * STEP);
 }
-template <typename T, bool LDS, typename SU>
-__device__ __forceinline__ void stage_put(const typename SU::Cols (&c)[SU::U], int g, int g1,
+template <typename T, bool LDS>
+__device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[StageU<T>::U], int g, int g1,
                                           const unsigned char *s_tab, const T *__restrict__ tab, int nb,
                                           T *__restrict__ G) {
-  constexpr int EPL = SU::EPL, U = SU::U, STEP = kStageThreads * EPL;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, STEP = kStageThreads * EPL;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int gg = g + u * STEP;
@@ -971,14 +970,12 @@ __device__ __forceinline__ void stage_put(const typename SU::Cols (&c)[SU::U], i
 // layout and is read from global memory), then the block's G range [g0, g1), software
 // pipelined: the next batch's column loads are issued before the current batch is looked
 // up and stored (two register sets, so no in-flight register is copied).
-template <typename T, bool LDS, int LDSB = kStageLds>
+template <typename T, bool LDS>
 __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt, int g0, int g1,
                                            const unsigned short *__restrict__ colS,
                                            const T *__restrict__ tab, T *__restrict__ G) {
-  constexpr int UB = LDSB < kStageLds ? kStageU / 2 : kStageU;
-  using SU = StageU<T, UB>;
-  constexpr int EPL = SU::EPL, U = SU::U, BSTEP = U * kStageThreads * EPL;
-  constexpr int kW = LDSB / 16 / kStageThreads;
+  constexpr int EPL = StageU<T>::EPL, U = StageU<T>::U, BSTEP = U * kStageThreads * EPL;
+  constexpr int kW = kStageLds / 16 / kStageThreads;
   const int t = threadIdx.x;
   uint4 buf[kW];
   const int bytes = LDS ? cnt * (int)sizeof(T) : 0;
@@ -991,9 +988,9 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
       buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
     }
   }
-  typename SU::Cols ca[U], cb[U];
+  ColVec<EPL> ca[U], cb[U];
   int g = g0 + t * EPL;
-  stage_load<T, LDS, SU>(ca, g, g1, colS);
+  stage_load<T, LDS>(ca, g, g1, colS);
   if constexpr (LDS) {  // slice stores after the first batch's loads are in flight
 #pragma unroll
     for (int u = 0; u < kW; ++u) {
@@ -1006,28 +1003,23 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
   }
   for (;;) {
     if (g >= g1) break;
-    stage_load<T, LDS, SU>(cb, g + BSTEP, g1, colS);
-    stage_put<T, LDS, SU>(ca, g, g1, s_tab, tab, nb, G);
+    stage_load<T, LDS>(cb, g + BSTEP, g1, colS);
+    stage_put<T, LDS>(ca, g, g1, s_tab, tab, nb, G);
     g += BSTEP;
     if (g >= g1) break;
-    stage_load<T, LDS, SU>(ca, g + BSTEP, g1, colS);
-    stage_put<T, LDS, SU>(cb, g, g1, s_tab, tab, nb, G);
+    stage_load<T, LDS>(ca, g + BSTEP, g1, colS);
+    stage_put<T, LDS>(cb, g, g1, s_tab, tab, nb, G);
     g += BSTEP;
   }
 }
 
-// LDSB: the slice buffer. kStageLds (128 KB, one block per CU) for every layout; 64 KB
-// (two blocks per CU) for the 1-byte codes' layout, whose slices are 64K nodes x 1 B: launched
-// while the host's copy of the packing width is 8 (any other layout then takes the
-// global-table path, correct and slower, for the rounds before the host sees the change).
-template <int LDSB>
-__global__ __launch_bounds__(kStageThreads, LDSB < kStageLds ? 8 : 1) void k_stage(StageArgs sa, int n,
+__global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         const double *__restrict__ a_prev,
                                                         const void *__restrict__ code_prev,
                                                         PackCtl *ctl, int rslot,
                                                         void *__restrict__ G, const int *__restrict__ psample,
                                                         int *pw_host) {
-  __shared__ __align__(16) unsigned char s_tab[LDSB];
+  __shared__ __align__(16) unsigned char s_tab[kStageLds];
   // the packing plan from a_{r-1} (the table staged here; due after round r-1) rides on the
   // stage launch: k_round_staged, the plan's first reader, starts after this launch, so the
   // plan needs no launch (and stream slot) of its own. Its block is block 0, dispatched
@@ -1054,12 +1046,12 @@ __global__ __launch_bounds__(kStageThreads, LDSB < kStageLds ? 8 : 1) void k_sta
   const unsigned short *colS = sa.colS[li];
 #define FU_BODY(T)                                                                                    \
   do {                                                                                                \
-    if ((int)sizeof(T) <= LB && (long long)SN * (long long)sizeof(T) <= LDSB)                         \
-      stage_body<T, true, LDSB>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),   \
-                                reinterpret_cast<T *>(G));                                            \
+    if ((int)sizeof(T) <= LB)                                                                         \
+      stage_body<T, true>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),         \
+                          reinterpret_cast<T *>(G));                                                  \
     else                                                                                              \
-      stage_body<T, false, LDSB>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),  \
-                                 reinterpret_cast<T *>(G));                                           \
+      stage_body<T, false>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),        \
+                           reinterpret_cast<T *>(G));                                                 \
   } while (0)
   if (wb == 1) FU_BODY(unsigned char);
   else if (wb == 2) FU_BODY(unsigned short);
@@ -2617,12 +2609,8 @@ int launch_k8(fu_handle *h, RoundCtx &c) {
   const StageArgs sa = stage_args(h, &sgrid);
   const void *cp = h->code[(c.r - 1) & 1];
   if (h->st_ntiles) {
-    if (FP::kStageNarrowPerCu > 1 && h->seen_width == 8 && h->st[0].P)  // 1-byte codes: 64 KB slices
-      hipLaunchKernelGGL(k_stage<kStageLds / 2>, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa,
-                         h->na, c.ap, cp, h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
-    else
-      hipLaunchKernelGGL(k_stage<kStageLds>, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa,
-                         h->na, c.ap, cp, h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
+    hipLaunchKernelGGL(k_stage, dim3(sgrid + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap, cp,
+                       h->pctl, r1, h->stG, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }
   plan_alone(h, c);
@@ -2710,7 +2698,7 @@ int launch_k9(fu_handle *h, RoundCtx &c) {
   sa.colS[3] = h->tr.colS;
   sa.f64 = 1;
   {
-    hipLaunchKernelGGL(k_stage<kStageLds>, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap,
+    hipLaunchKernelGGL(k_stage, dim3(h->tr.NB + (c.plan ? 8 : 0)), dim3(kStageThreads), 0, h->stream, sa, h->na, c.ap,
                        cp, h->pctl, r1, h->tr.GA, c.plan ? h->psample : nullptr, h->pw_dev);
     c.plan = false;
   }

@@ -209,10 +209,7 @@ int build_stage_layouts(const Graph &g, const std::vector<I4> &light, int n_cu, 
       w = "kernel 8 (staged slices): more than " + std::to_string(kStageMaxP) + " slices";
       continue;
     }
-    // blocks per slice: one stage block per CU (the 1-byte layout: kStageNarrowPerCu, its
-    // 64 KB slices let k_stage<64 KB> run two per CU)
-    const int64_t cus = (int64_t)n_cu * (li == 0 && SN <= kStageLds / 2 ? kStageNarrowPerCu : 1);
-    const int64_t Q = std::max<int64_t>(1, std::min<int64_t>(T, (cus + P / 2) / P));
+    const int64_t Q = std::max<int64_t>(1, std::min<int64_t>(T, (n_cu + P / 2) / P));
     auto part = [&](int t) { return (int64_t)t * Q / T; };
     // elements per (slice, part) and runs per tile
     std::vector<int64_t> cnt(P * Q, 0);

@@ -27,10 +27,6 @@ constexpr int kR0E = 1024;                       // round-0 flow blocks; c16 blo
 constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
 constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 constexpr int kStageLds = 131072;                // bytes of estimate table per slice
-#ifndef FU_STAGE_NARROW  // experiment builds: stage blocks per CU for the 1-byte layout
-#define FU_STAGE_NARROW 1
-#endif
-constexpr int kStageNarrowPerCu = FU_STAGE_NARROW;  // 2: 64 KB slices, two stage blocks per CU
 #ifndef FU_STAGE_TE
 #define FU_STAGE_TE 1024
 #endif
