@@ -80,6 +80,9 @@ def parse(argv=None):
                     help="rgg-dist: strong scaling, --n nodes in all (2^26 by default) split over the ranks")
     ap.add_argument("--opt", action="append", default=[], metavar="KEY=VALUE",
                     help="engine option for the headline engine (fu_set_option; A/B runs)")
+    ap.add_argument("--settle-ms", type=float, default=None,
+                    help="untimed rounds run back to back right before a timed window, at least this "
+                         "long (default 25 ms; at N > 1 a fixed round count, the same on every rank)")
     ap.add_argument("--no-unit", action="store_true",
                     help="N = 1 default line without its weak_scaling_unit (config 5's per-GPU RGG)")
     return ap.parse_args(argv)
@@ -235,12 +238,19 @@ def make_graph(wl, n_arg, m_arg):
     return fu.Graph.random_regular(n, 8, seed=1), f"rr:n={n},d=8 collect-all generation-synchronous rounds"
 
 
-def prepare(eng, kernel, warmup, widths=None, tune=True):
+SETTLE_MS = 25.0  # untimed rounds right before a timed window, at least this long (wall)
+
+
+def prepare(eng, kernel, warmup, widths=None, tune=True, settle_ms=None):
     """Untimed setup: one autotune pass (kernel auto; tune=False: the engine was tuned at this
     width already), `warmup` rounds in chunks of 64 (the host sees each packing plan's width
     between calls, so the autotuner also covers every width the warmup reaches; winners are
-    kept across fu_reset; at most four passes per engine), fu_reset. widths: a list that
-    receives (rounds done, packing plan width) after each chunk."""
+    kept across fu_reset; at most four passes per engine), then rounds until the GPU has
+    run at least settle_ms (default SETTLE_MS) of them back to back right before the window
+    (with 5 warmup rounds of 60 us the chip starts the window cold: rounds 1-19 of ER-1M
+    took 59.7 us against 58.1 after 25 ms of rounds, four alternating pairs,
+    profiles/r05/ag), fu_reset. widths: a list that receives (rounds done, packing plan
+    width) after each warmup chunk. Returns the settle rounds run."""
     if kernel == "auto" and tune:
         eng.tune()
     done = 0
@@ -250,7 +260,14 @@ def prepare(eng, kernel, warmup, widths=None, tune=True):
         eng.synchronize()
         if widths is not None:
             widths.append((done, eng.pack_widths()[2]))
+    settle = SETTLE_MS if settle_ms is None else settle_ms
+    n_settle, t0 = 0, time.perf_counter()
+    while settle > 0 and (time.perf_counter() - t0) * 1e3 < settle:
+        eng.run(16)
+        eng.synchronize()
+        n_settle += 16
     eng.reset()
+    return n_settle
 
 
 def measure_window(eng, g, steps):
@@ -289,7 +306,7 @@ def run_single(args, wl):
         k, val = kv.split("=", 1)
         eng.set_option(k, int(val))
     t_setup = time.perf_counter()
-    prepare(eng, args.kernel, args.warmup)
+    n_settle = prepare(eng, args.kernel, args.warmup, settle_ms=args.settle_ms)
     t_setup = time.perf_counter() - t_setup
 
     wall, phases, roof, value_r1, kinfo, kname = measure_window(eng, g, args.steps)
@@ -341,6 +358,8 @@ def run_single(args, wl):
             "autotune_us_per_round": kinfo["tune_us_per_round"],
             "autotune_winner_by_width": kinfo["tune_winner_by_width"],
             "pack_width_after": pack_after, "setup_s": t_setup, "phases": phases,
+            "settle": {"rounds": n_settle, "ms": SETTLE_MS if args.settle_ms is None else args.settle_ms,
+                       "note": "untimed rounds back to back right before the window (bench.prepare)"},
             "options": args.opt,
             "parallelism": "single GPU",
         },
@@ -631,6 +650,11 @@ def measure_dist(args, world, rank, local, dist):
         eng.tune()  # collective: the same rounds on every rank
     if args.warmup:
         eng.run(args.warmup)
+    # settle: a fixed round count (the same on every rank: each round is a halo exchange),
+    # about SETTLE_MS of rounds for the 2^23-node slab (~0.3 ms per round)
+    n_settle = 0 if args.settle_ms == 0 else 80
+    if n_settle:
+        eng.run(n_settle)
     eng.reset()
     eng.synchronize()
 
@@ -674,6 +698,7 @@ def measure_dist(args, world, rank, local, dist):
                          e_tot=e_tot, n_tot=n_tot, halo=halo, n_total=n_total, per=per, kinfo=kinfo,
                          halo_us=halo_us, round_us=1e3 * dev1 / max(1, args.steps - 1), t_gen=t_gen,
                          conv=conv, strong=args.strong, rccl_parity=parity, traffic=traffic)
+        line["config"]["settle_rounds"] = n_settle  # untimed, right before the window, every rank
     eng.close()
     return line
 
