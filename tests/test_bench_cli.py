@@ -237,6 +237,8 @@ def test_n1_line_carries_config2_rmat24_pairwise_units(monkeypatch, capsys):
     bench.run_single(args, "er")
     line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert line["steps"] == 20 and line["roofline"]["copy_GBs"] == 5500.0
+    st = line["config"]["settle"]  # untimed rounds right before the window (>= 25 ms)
+    assert st["ms"] == 25.0 and st["rounds"] >= 16 and st["rounds"] % 16 == 0
     io = line["host_io"]  # the PCIe-inclusive rate, beside (never as) the value
     assert io["host_bytes_in"] == 8 * 1_000_001 + 4 * 7_999_972 + 8 * 1_000_000
     assert 0 < io["value_with_create_and_download"] <= line["value"]
