@@ -168,10 +168,10 @@ def timed_rounds(eng, steps: int):
     b = chunk_bounds(steps)
     eng.synchronize()
     t0 = time.perf_counter()
-    eng.mark(0)
-    for k in range(len(b) - 1):
-        eng.run(b[k + 1] - b[k])
-        eng.mark(k + 1)
+    # one host call for the whole window (fu_run_collectall_marked): no interpreter work
+    # between the marks, so round 0 (the first launch on an idle stream) is timed from its
+    # event to its end without Python's call overhead in between
+    eng.run_marked(b)
     eng.synchronize()
     wall = time.perf_counter() - t0
     dev = [eng.elapsed(k, k + 1) for k in range(len(b) - 1)]
@@ -282,8 +282,8 @@ def measure_window(eng, g, steps):
     alg_bytes = 24 * g.E + 28 * g.n
     roof = roofline(alg_bytes, dev_ms, b, pmc_traffic(g.n, g.E, kname, steps), round_kernels(kinfo))
     ws = window_stats(g.n, g.E, kname, steps)
-    if ws:
-        roof["window_stats"] = ws
+    if ws:  # an archived record of another run (possibly another tree): never this run's numbers
+        roof["archived_window_profile"] = ws
     value_r1 = g.E * (steps - 1) / (sum(dev_ms[1:]) * 1e-3) if steps > 1 else None
     return wall, phases, roof, value_r1, kinfo, kname
 
@@ -514,7 +514,10 @@ def window_stats(n, E, kernel_selected, steps):
                 and rec.get("rounds_timed") == steps:
             return {"file": os.path.relpath(path, ROOT), "avg_round_us": rec.get("avg_round_us"),
                     "frac": rec.get("frac"), "per_kernel": rec.get("per_kernel_per_round"),
-                    "box_copy_GBs": rec.get("copy_GBs")}
+                    "box_copy_GBs": rec.get("copy_GBs"), "commit": rec.get("commit"),
+                    "note": "archival: the kernel-trace record of this window committed under profiles/ "
+                            "(another run, maybe another tree and box), for recomputing the fraction from "
+                            "tracked files; this run's own numbers are the fields above"}
     return None
 
 

@@ -110,7 +110,12 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  *                 reconstruction, direct estimate gathers), 8 = stage (estimates staged slice
  *                 by slice through LDS; single GPU, needs a slice layout), 9 = pregather
  *                 (stage + per-bucket transpose into edge order; single GPU, <= 2^25 nodes).
- *                 Partitioned (fu_dist_*) handles run kernel 4. All kernels are bitwise equal.
+ *                 All kernels are bitwise equal. On an RCCL rank (fu_dist_create) this
+ *                 option is collective: every rank sets it, and a kernel whose layout fails
+ *                 on one rank (the slice limits count ghost slots, so they are rank-local)
+ *                 fails with FU_ERR_STATE on every rank, so no rank starts rounds alone.
+ *                 Kernel 9 on partitions sends its halo after the round (no overlap): it is
+ *                 meant for the in-process transport and power-law graphs; auto never picks it.
  * "tile_edges"    kernel 4 tile edges: 2048, 1024 (default) or 512; "tile_nodes" 0/128/256.
  * "hub_threshold" rows of higher degree run as heavy rows, one wave each (default 128).
  * "mega_hub"      rows of higher degree run as mega hubs: one chain-only block each, their
@@ -140,12 +145,11 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * "stage_layout"  kernel 8, tests: -1 = by packing width, 0..3 = the 1/2/4/8-byte layout.
  * "staged_lo"     kernel 8: staged indices loaded ahead of the flows (1, default) or
  *                 interleaved with them (0; the round-1 order, kept for A/B and tests).
- * Removed after measurement (FU_ERR_ARG): "tr_pipe", "hub_prio", "side_tiles", "split_tr",
- * "hub_cus" / "hub_cu_stride" (the hub path on CU-masked streams: round 5, profiles/r05/b),
- * "st_split" (kernel 8's next stage overlapping this round's tiles: profiles/r05/c), "tr_hot"
- * (kernel 9's hot-estimate table in the transposes: DESIGN §4.12), "nt" (kernel 4's
- * non-temporal column loads: DESIGN §4.11)
- * (DESIGN.md §4.12), "hub_multi", "hub_blocks", "fuse", "light_geo". */
+ * Removed after measurement (FU_ERR_ARG; the numbers are in DESIGN.md §4 and
+ * profiles/MEASUREMENTS.md): "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_multi",
+ * "hub_blocks", "fuse", "light_geo", "tr_hot" (kernel 9), "hub_cus" / "hub_cu_stride" (the
+ * hub path on CU-masked streams, profiles/r05/b), "st_split" (kernel 8's next stage beside
+ * this round's tiles, profiles/r05/c) and "nt" (kernel 4's non-temporal column loads). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);
@@ -164,6 +168,11 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms);
  * advance the state: call fu_reset before a run that must start from zero. The winner is
  * kept across fu_reset. Synchronises. Lets a caller tune outside a timed region. */
 int fu_tune(fu_handle *h);
+/* A timed window in one call: runs rounds_at[n_marks - 1] rounds and records mark k (the
+ * event of fu_mark slot k) once rounds_at[k] of them are queued (non-decreasing, rounds_at[0]
+ * = 0 marks the start; n_marks <= 64). Asynchronous; read the times with fu_mark_elapsed.
+ * bench.py times its windows with it, so no host interpreter runs between the marks. */
+int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *rounds_at);
 /* Record HIP event `slot` (0..63) on the handle's stream (asynchronous). */
 int fu_mark(fu_handle *h, int32_t slot);
 /* *ms = device time between two recorded marks (waits for `to`). */
@@ -263,6 +272,20 @@ int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t
                             const int64_t *route_off, const int32_t *route_links, double msg_bytes,
                             double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
                             fu_trace **out);
+/* fu_trace_build_links_ex with SimGrid's network/crosstraffic: every transfer also loads each
+ * shared link of its reverse route (route dst -> src) with crosstraffic x its rate (the TCP
+ * acknowledgements; SimGrid: 0.05), and a FATPIPE link of the reverse route alone caps it at
+ * bw_factor * bandwidth / crosstraffic. crosstraffic = 0 is fu_trace_build_links_ex. SimGrid
+ * enables it by default, but this repository keeps it OFF by default (the drop-in Engine
+ * turns it on with --cfg=network/crosstraffic:1): its effect on a schedule cannot be pinned
+ * offline, and on the reference platform every 154-byte transfer ends within its tick with or
+ * without it. Parity-unpinned; oracle/oracle.py's LinkNet restates it operation for operation. */
+int fu_trace_build_links_cross(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                               int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                               const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                               const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                               double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
+                               double crosstraffic, fu_trace **out);
 int fu_trace_fault_stats(const fu_trace *t, int64_t *dropped, int64_t *delayed);
 /* info[0]=union edges, [1]=tasks, [2]=events, [3]=out_ids, [4]=message slots,
  * [5]=ticks, [6]=dynamic neighbour additions (CA:94-96 errors), [7]=messages sent. */

@@ -199,8 +199,10 @@ class LinkNet:
     bw_factor * bandwidth on the shared links it crosses, capped by its FATPIPE links and,
     with tcp_gamma > 0, by the TCP window tcp_gamma / (2 * latency sum). Shares are weighted
     by 1 / the flow's sharing penalty, LV08's latency sum + weight_S / bandwidth over its
-    links (weight_S = 0: penalty 1, equal shares). Parity-unpinned against SimGrid (not
-    installable offline)."""
+    links (weight_S = 0: penalty 1, equal shares). With crosstraffic c > 0 (SimGrid's
+    network/crosstraffic) a flow also loads each shared link of its reverse route with c x
+    its rate, and a FATPIPE link of the reverse route alone caps it at bw_factor * bw / c.
+    Parity-unpinned against SimGrid (not installable offline)."""
 
     def __init__(self, net):
         self.n = int(net["n"])
@@ -214,6 +216,7 @@ class LinkNet:
         self.bw_factor = float(net.get("bw_factor", 0.97))
         self.weight_S = float(net.get("weight_S", 0.0))
         self.tcp_gamma = float(net.get("tcp_gamma", 0.0))
+        self.cross = float(net.get("crosstraffic", 0.0))
         self.active = []  # flows (dicts) not done, in start order
         self.now = 0.0
 
@@ -224,11 +227,22 @@ class LinkNet:
         r = src * self.n + dst
         f = {"r": r, "rate": 0.0, "end": math.inf, "phase": 0, "rem": self.bytes}
         lsum, cap, sw = 0.0, math.inf, 0.0
+        f["lk"] = []  # (link, coefficient): its shared route links, then its reverse route's
         for k in self.links(f):
             lsum = lsum + self.lat[k]
             sw = sw + self.weight_S / self.bw[k]
             if not self.shared[k]:
                 cap = min(cap, self.bw_factor * self.bw[k])
+            else:
+                f["lk"].append((k, 1.0))
+        if self.cross > 0.0:
+            rb = dst * self.n + src
+            fwd = self.links(f)
+            for k in self.rl[self.roff[rb]:self.roff[rb + 1]]:
+                if self.shared[k]:
+                    f["lk"].append((k, self.cross))
+                elif k not in fwd:
+                    cap = min(cap, self.bw_factor * self.bw[k] / self.cross)
         if self.tcp_gamma > 0.0 and lsum > 0.0:
             cap = min(cap, self.tcp_gamma / (2.0 * lsum))
         f["lat_end"] = t + self.lat_factor * lsum
@@ -247,10 +261,9 @@ class LinkNet:
         use = [0.0] * nl
         un = [f for f in self.active if f["phase"] == 1]
         for f in un:
-            for k in self.links(f):
-                if self.shared[k]:
-                    cnt[k] += 1
-                    use[k] = use[k] + 1.0 / f["pen"]
+            for k, c in f["lk"]:
+                cnt[k] += 1
+                use[k] = use[k] + c / f["pen"]
         while un:
             best = math.inf
             for k in range(nl):
@@ -261,18 +274,17 @@ class LinkNet:
             keep, fix = [], []
             for f in un:
                 b = f["cap"] * f["pen"] == best
-                for k in self.links(f):
+                for k, _c in f["lk"]:
                     if b:
                         break
-                    b = bool(self.shared[k]) and cnt[k] > 0 and max(0.0, crem[k] / use[k]) == best
+                    b = cnt[k] > 0 and max(0.0, crem[k] / use[k]) == best
                 (fix if b else keep).append(f)
             for f in fix:
                 f["rate"] = f["cap"] if f["cap"] * f["pen"] == best else best / f["pen"]
-                for k in self.links(f):
-                    if self.shared[k]:
-                        crem[k] = crem[k] - f["rate"]
-                        use[k] = use[k] - 1.0 / f["pen"]
-                        cnt[k] -= 1
+                for k, c in f["lk"]:
+                    crem[k] = crem[k] - c * f["rate"]
+                    use[k] = use[k] - c / f["pen"]
+                    cnt[k] -= 1
             un = keep
 
     def advance_to(self, T):

@@ -56,6 +56,7 @@ struct DistState {
   bool any_halo = true;          // RCCL transport: this rank sends or receives estimates (else no comm-stream hop)
   int64_t packed_round = -1;     // in-process transport: round whose packed halo awaits the exchange
   int64_t exchanged_round = -1;  // in-process transport: last round whose halo was exchanged
+  unsigned long long *agree = nullptr;  // RCCL transport: one word for fu__dist_agree
 };
 
 __global__ void k_pack(long long cnt, const int *__restrict__ idx, const double *__restrict__ src,
@@ -170,6 +171,25 @@ int fu__dist_round_hook(fu_handle *h, int phase) {
   return FU_OK;
 }
 
+// Collective agreement on a host-side result (RCCL transport): *ok_all = the minimum of
+// ok_local over all ranks, so a call that failed on one rank fails on every rank instead of
+// leaving its peers to block in the next halo exchange. Every rank must call it. The
+// in-process transport has one caller for all ranks, which sees every rank's result itself.
+int fu__dist_agree(fu_handle *h, int ok_local, int *ok_all) {
+  auto *d = static_cast<DistState *>(fu__handle_dist(h));
+  *ok_all = ok_local;
+  if (!d || !d->comm) return FU_OK;
+  if (!d->agree) HIPD_TRY(hipMalloc((void **)&d->agree, sizeof(unsigned long long)));
+  unsigned long long v = ok_local ? 1ull : 0ull;
+  HIPD_TRY(hipStreamSynchronize(d->comm_stream));
+  HIPD_TRY(hipMemcpyAsync(d->agree, &v, sizeof(v), hipMemcpyHostToDevice, d->comm_stream));
+  NCCL_TRY(ncclAllReduce(d->agree, d->agree, 1, ncclUint64, ncclMin, d->comm, d->comm_stream));
+  HIPD_TRY(hipMemcpyAsync(&v, d->agree, sizeof(v), hipMemcpyDeviceToHost, d->comm_stream));
+  HIPD_TRY(hipStreamSynchronize(d->comm_stream));
+  *ok_all = v != 0;
+  return FU_OK;
+}
+
 void fu__dist_free(fu_handle *h) {
   auto *d = static_cast<DistState *>(fu__handle_dist(h));
   if (!d) return;
@@ -181,7 +201,7 @@ void fu__dist_free(fu_handle *h) {
   if (d->ev_h0) hipEventDestroy(d->ev_h0);
   if (d->ev_h1) hipEventDestroy(d->ev_h1);
   if (d->comm_stream) hipStreamDestroy(d->comm_stream);
-  void *ptrs[] = {d->send_a_idx, d->sbuf_a};
+  void *ptrs[] = {d->send_a_idx, d->sbuf_a, d->agree};
   for (void *p : ptrs)
     if (p) hipFree(p);
   delete d;

@@ -113,23 +113,9 @@ struct PackCtl {
   int pad;
 };
 
-// Write-through store (global_store ... sc1): the line leaves the XCD's L2 at once instead
-// of staying dirty there. A kernel's end writes back every dirty L2 line before the next
-// launch may start, so round kernels that leave their output (flows, estimates, codes,
-// staged words) dirty pay that writeback serially at each boundary (MI355X_MICROARCH.md:
-// + bytes / 6 TB/s per boundary); streamed through, it overlaps the kernel's own work.
-// Byte and short sc1 stores go out as one fabric write each (MI355X_MICROARCH.md: 6-12x the
-// per-byte cost of wide ones), so 1- and 2-byte elements keep plain (write-back) stores.
-// Measured on ER-1M: write-through did not shorten the round kernels (kernel 4 lost 4.5 us,
-// kernel 8 gained nothing), so it is off unless built with -DFU_WT=1.
-#ifndef FU_WT
-#define FU_WT 0
-#endif
-template <typename T>
-__device__ __forceinline__ void st_wt(T *p, T v) {
-  if constexpr (FU_WT && sizeof(T) >= 4) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else *p = v;
-}
+// Round outputs (flows, estimates, codes) use plain write-back stores. Write-through (sc1)
+// stores, so that no dirty lines wait for the launch boundary's L2 writeback, were measured
+// in round 2 and removed: on ER-1M kernel 4 lost 4.5 us per round and kernel 8 gained nothing.
 
 __device__ inline unsigned long long dkey(double x) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(x);
@@ -149,9 +135,9 @@ __device__ inline void put_code(const PackCtl &pc, void *tab, int i, double a) {
   const unsigned long long off = dkey(a) - pc.base;
   const unsigned esc = pc.width == 32 ? 0xFFFFFFFFu : (1u << pc.width) - 1u;
   const unsigned cd = off < (unsigned long long)esc ? (unsigned)off : esc;
-  if (pc.width == 8) st_wt(reinterpret_cast<unsigned char *>(tab) + i, (unsigned char)cd);
-  else if (pc.width == 16) st_wt(reinterpret_cast<unsigned short *>(tab) + i, (unsigned short)cd);
-  else st_wt(reinterpret_cast<unsigned *>(tab) + i, cd);
+  if (pc.width == 8) *(reinterpret_cast<unsigned char *>(tab) + i) = (unsigned char)cd;
+  else if (pc.width == 16) *(reinterpret_cast<unsigned short *>(tab) + i) = (unsigned short)cd;
+  else *(reinterpret_cast<unsigned *>(tab) + i) = cd;
 }
 template <int W>
 __device__ inline double decode_or(unsigned cd, unsigned long long base, const double *a_prev, int j) {
@@ -264,7 +250,7 @@ __device__ __forceinline__ double ld_f(const double *F, int e) {
   const long long i = fhi_idx(e);
   return __hiloint2double((int)w[i], (int)w[i + 32]);
 }
-__device__ __forceinline__ void st_fw(unsigned *p, unsigned v) { st_wt(p, v); }
+__device__ __forceinline__ void st_fw(unsigned *p, unsigned v) { *p = v; }
 // store f_r over f_old (the value the slot held)
 __device__ __forceinline__ void st_f(double *F, int e, double v, double f_old) {
   unsigned *w = reinterpret_cast<unsigned *>(F);
@@ -378,10 +364,7 @@ __device__ inline void wave_sync() {
 // (no register copies: those cost two more VALU instructions per element). The caller
 // keeps xs and es in different LDS banks (es = xs + 8 TE + 8 bytes in the tiles), so the
 // two addresses of one read do not conflict.
-#ifndef FU_CHAIN_B
-#define FU_CHAIN_B 16  // measured: 8 -> 8.75, 16 -> 7.2, 32 -> 6.4 ns per element (32 costs registers)
-#endif
-template <int B = FU_CHAIN_B>
+template <int B = kChainB>
 __device__ __forceinline__ void chain_sum(const double *xs, const double *es, int cn, double &S, double &T) {
   const bool odd = threadIdx.x & 1;
   const double *src = odd ? es : xs;
@@ -503,12 +486,12 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
             }
             wave_sync();
             // the register-resident mid launch: 8-element batches (its rows hold 64 VGPRs)
-            chain_sum<(HRL > kHeavyRL ? 8 : FU_CHAIN_B)>(xs, es, min(CH, d - c * CH), S, T);
+            chain_sum<(HRL > kHeavyRL ? 8 : kChainB)>(xs, es, min(CH, d - c * CH), S, T);
           }
         }
         const double a = ((v[i] - S) + T) / (double)(d + 1);
         if (lane == 0) {
-          st_wt(a_new + i, a);
+          *(a_new + i) = a;
           if (pc.width) put_code(pc, code_new, i, a);
           if (CHECK) eb = err_bits(a, target[i]);
         }
@@ -551,7 +534,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
       }
       const double a = ((v[i] - S) + T) / (double)(d + 1);
       if (lane == 0) {
-        st_wt(a_new + i, a);
+        *(a_new + i) = a;
         if (pc.width) put_code(pc, code_new, i, a);
         if (CHECK) eb = err_bits(a, target[i]);
       }
@@ -647,7 +630,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     if (t == 0) {
       const double a = ((v[i] - S) + T) / (double)(d + 1);
       s_a[0] = a;
-      st_wt(a_new + i, a);
+      *(a_new + i) = a;
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
@@ -695,7 +678,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     if (t == 0) {
       const double a = ((v[i] - S) + T) / (double)(e - b + 1);
       s_a[0] = a;
-      st_wt(a_new + i, a);
+      *(a_new + i) = a;
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
@@ -832,7 +815,7 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
-    st_wt(a_new + nb + t, a);
+    *(a_new + nb + t) = a;
     if (pc.width) put_code(pc, code_new, nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
@@ -869,10 +852,6 @@ __global__ __launch_bounds__(kBlock, (HRL > kHeavyRL ? 3 : 1)) void k_round_reco
 // kernel 4 heavy tiles in a launch of their own. Results are bitwise those of kernel 4.
 // ------------------------------------------------------------------------------------
 constexpr int kStageThreads = 1024;   // one block per CU (the slice takes 128 KB of its LDS)
-#ifndef FU_STAGE_U  // experiment builds: steps per lane in flight
-#define FU_STAGE_U 4
-#endif
-constexpr int kStageU = FU_STAGE_U;   // steps per lane in flight
 
 struct StageArgs {
   int P[4], Q[4], SN[4], NB[4];        // slices, blocks per slice, nodes per slice, blocks
@@ -955,10 +934,7 @@ __device__ __forceinline__ void stage_put(const ColVec<StageU<T>::EPL> (&c)[Stag
       typedef unsigned v4u __attribute__((ext_vector_type(4)));
       v4u w;
       __builtin_memcpy(&w, val, 16);
-#ifndef FU_STAGE_NT  // experiment builds: 0 = write-back stores, 2 = non-temporal at every width
-#define FU_STAGE_NT 1
-#endif
-      if constexpr (FU_STAGE_NT == 2 || (FU_STAGE_NT == 1 && sizeof(T) == 8))
+      if constexpr (sizeof(T) >= kStageNtMinBytes)
         __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(G + gg));
       else
         *reinterpret_cast<v4u *>(G + gg) = w;
@@ -1081,11 +1057,8 @@ constexpr int kTrThreads = 1024;
 // bucket's run starts (offT) are loaded while this bucket's G_A loads are in flight, and its
 // G_B stores drain while the next bucket is scanned (with one block per bucket, each block
 // paid the offT round trip first and held its slot until its stores were done).
-#ifndef FU_TR_WAVES
-#define FU_TR_WAVES 1
-#endif
 template <bool NT>  // NT: the streamed G_B stores non-temporal
-__global__ __launch_bounds__(kTrThreads, FU_TR_WAVES) void k_transpose(int b0, int nbk, int P, long long E,
+__global__ __launch_bounds__(kTrThreads, kTrWaves) void k_transpose(int b0, int nbk, int P, long long E,
                                                         const int *__restrict__ offT,
                                                         const double *__restrict__ GA,
                                                         const unsigned short *__restrict__ pos16,
@@ -1215,7 +1188,7 @@ __global__ __launch_bounds__(kBlock) void k_isolated(int i0, int n, const double
   unsigned long long eb = 0;
   if (i < n) {
     const double a = ((v[i] - 0.0) + 0.0) / (double)1;
-    st_wt(a_new + i, a);
+    *(a_new + i) = a;
     if (pc.width) put_code(pc, code_new, i, a);
     if (check) eb = err_bits(a, target[i]);
   }
@@ -1326,11 +1299,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   if (pp.width == 0) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
-#ifdef FU_GLOAD_NT  // experiment build: non-temporal G loads (each staged element is read once)
-      g[k] = gi[k] >= 0 ? __builtin_nontemporal_load(reinterpret_cast<const double *>(G) + gi[k]) : 0.0;
-#else
       g[k] = gi[k] >= 0 ? reinterpret_cast<const double *>(G)[gi[k]] : 0.0;
-#endif
   } else {
     unsigned cd[kPer];
     unsigned esc;
@@ -1375,7 +1344,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
     }
     const double a = ((vv - S) + T) / (double)(qe - qb + 1);
     s_a[t] = a;
-    st_wt(a_new + nb + t, a);
+    *(a_new + nb + t) = a;
     if (pc.width) put_code(pc, code_new, nb + t, a);
     if (CHECK) eb = err_bits(a, target[nb + t]);
   }
@@ -1558,7 +1527,7 @@ __global__ __launch_bounds__(kBlock) void k_heavy_multi(
       const int i = hrows[r0 + cr];
       const double a = ((v[i] - acc) + T) / (double)(s_d[cr] + 1);
       s_a[cr] = a;
-      st_wt(a_new + i, a);
+      *(a_new + i) = a;
       if (pc.width) put_code(pc, code_new, i, a);
       if (CHECK) eb = err_bits(a, target[i]);
     }
@@ -1877,9 +1846,6 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist(
 //     has arrived in one of the two polls, at most two pairwise fires: RR-64K runs two
 //     {receive, fire} pairs per iteration.
 // The collect-all path (k messages per fire) stores its messages as it goes.
-#ifndef FU_REPLAY_SLEEP
-#define FU_REPLAY_SLEEP 2  // s_sleep units (64 cycles) between passes that made no progress
-#endif
 constexpr int kRW = 4;       // events per iteration at most
 constexpr int kScan = 4;     // ring entries searched for the next two receives
 constexpr int kRing = 16;    // LDS ring entries per lane
@@ -2119,7 +2085,7 @@ __global__ __launch_bounds__(kBlock) void k_replay_persist_reg(
         send(o2, f2, a2);
       }
     }
-    if (!__any(prog)) __builtin_amdgcn_s_sleep(FU_REPLAY_SLEEP);
+    if (!__any(prog)) __builtin_amdgcn_s_sleep(kReplaySleep);
     if (++it > max_iters) {  // bounded spin: a bug must end the kernel, not hang the GPU
       atomicExch(status, 1);
       break;
@@ -2311,6 +2277,7 @@ struct fu_handle {
 
 extern "C" int fu__dist_round_hook(fu_handle *h, int phase);
 extern "C" void fu__dist_free(fu_handle *h);
+extern "C" int fu__dist_agree(fu_handle *h, int ok_local, int *ok_all);
 
 namespace {
 
@@ -3113,13 +3080,18 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     if (value != 0 && value != 4 && value != 8 && value != 9)
       return fail(FU_ERR_ARG, "fu_set_option: kernel must be 0 (auto), 4 (recon), 8 (stage) or 9 (pregather)");
     if (h->rounds != 0) return fail(FU_ERR_STATE, "fu_set_option: kernel can only change before the first round (call fu_reset)");
-    if (value == 8) {
-      if (int rc = ensure_stage(h)) return rc;
+    int rc = FU_OK;
+    if (value == 8) rc = ensure_stage(h);
+    if (value == 9) rc = ensure_transpose(h);  // the slice limit counts ghost slots: rank-dependent
+    if (h->dist) {  // RCCL ranks: a kernel that fails on one rank fails on all (collective)
+      const std::string why = rc ? fu_last_error() : "";
+      int all_ok = 1;
+      if (int rc2 = fu__dist_agree(h, rc == FU_OK, &all_ok)) return rc2;
+      if (rc) return fail(rc, why);
+      if (!all_ok) return fail(FU_ERR_STATE, "fu_set_option: kernel " + std::to_string(value) + " failed on another rank");
     }
-    if (value == 9) {
-      if (int rc = ensure_transpose(h)) return rc;
-      h->geo = 1;
-    }
+    if (rc) return rc;
+    if (value == 9) h->geo = 1;
     h->kernel = value == 0 ? 4 : (int)value;
     h->autotune = value == 0;
     h->tuned = false;
@@ -3463,6 +3435,35 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
   HIP_TRY(hipEventRecord(h->ev3, h->stream));
   HIP_TRY(hipEventSynchronize(h->ev3));
   HIP_TRY(hipEventElapsedTime(ms, h->ev2, h->ev3));
+  return FU_OK;
+  FU_TRY_END
+}
+
+// A timed window in one host call: mark k (HIP event slot k) is recorded once rounds_at[k]
+// rounds of this call have been queued (rounds_at[0] = 0: before the first). Between the
+// marks no host code but the launches runs, so the device time of the window's first round
+// (round 0 after fu_reset: the GPU waits on an idle stream for its launch) holds no
+// interpreter overhead between the first mark and the first launch.
+int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *rounds_at) {
+  FU_TRY_BEGIN
+  if (!h || !rounds_at || n_marks < 1 || n_marks > 64 || rounds_at[0] < 0)
+    return fail(FU_ERR_ARG, "fu_run_collectall_marked: bad arguments (1..64 marks, rounds_at[0] >= 0)");
+  for (int k = 1; k < n_marks; ++k)
+    if (rounds_at[k] < rounds_at[k - 1]) return fail(FU_ERR_ARG, "fu_run_collectall_marked: rounds_at must not decrease");
+  if (int rc = set_device(h)) return rc;
+  for (int k = 0; k < n_marks; ++k)
+    if (!h->marks[k]) HIP_TRY(hipEventCreate(&h->marks[k]));
+  int32_t done = 0;
+  for (int k = 0; k < n_marks; ++k) {
+    if (rounds_at[k] > done) {
+      if (int rc = run_rounds(h, rounds_at[k] - done, 0, 0)) return rc;
+      done = rounds_at[k];
+    }
+    if (h->dist) {  // a mark after a round includes that round's halo (comm stream)
+      if (int rc = fu__dist_round_hook(h, 0)) return rc;
+    }
+    HIP_TRY(hipEventRecord(h->marks[k], h->stream));
+  }
   return FU_OK;
   FU_TRY_END
 }

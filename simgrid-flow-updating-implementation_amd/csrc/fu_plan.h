@@ -14,6 +14,8 @@
 #include <string>
 #include <vector>
 
+#include "fu_tuning.h"
+
 namespace fu {
 namespace plan {
 
@@ -27,25 +29,14 @@ constexpr int kR0E = 1024;                       // round-0 flow blocks; c16 blo
 constexpr int kGeoEdges[4] = {2048, 1024, 1024, 512};
 constexpr int kGeoNodes[4] = {256, 128, 256, 64};
 constexpr int kStageLds = 131072;                // bytes of estimate table per slice
-#ifndef FU_STAGE_TE
-#define FU_STAGE_TE 1024
-#endif
-#ifndef FU_STAGE_TN
-#define FU_STAGE_TN 128
-#endif
-constexpr int kStageTE = FU_STAGE_TE, kStageTN = FU_STAGE_TN;  // kernel 8 light tiles (experiment builds override)
+using ::kStageTE;                                // csrc/fu_tuning.h
+using ::kStageTN;
+using ::kTrBE;
+using ::kHeavyRL;
 constexpr int kStageRuns = 64;                   // slice runs per tile the u16 index addresses
 constexpr int kStageMaxP = 512;                  // slices per kernel 8 layout
-#ifndef FU_TR_BE
-#define FU_TR_BE 8192
-#endif
-constexpr int kTrBE = FU_TR_BE;                  // kernel 9: edges per transpose bucket
 static_assert(kTrBE <= 32768 && kTrBE % 1024 == 0 && kTrBE / 64 <= 1024, "u16 positions, coarse table");
 constexpr int kTrMaxP = 2048;                    // kernel 9: slices of 16K nodes (n <= 2^25)
-#ifndef FU_HEAVY_RL
-#define FU_HEAVY_RL 4
-#endif
-constexpr int kHeavyRL = FU_HEAVY_RL;            // heavy rows kept in registers: 64 x kHeavyRL edges
 constexpr int kMidRL = 16;                       // kernel 9 register launch: rows of <= 64 x kMidRL
 constexpr int kMR = 16;                          // k_heavy_multi: rows per block
 constexpr int kHubBlk = 256;                     // k_hub_stage / k_hub_flows threads per block

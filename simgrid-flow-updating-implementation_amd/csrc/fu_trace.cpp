@@ -65,7 +65,10 @@ using namespace fu;
 // penalty, LV08's route latency sum + weight_S / bw_k over its links (weight_S = 0: equal
 // shares); a FATPIPE link caps each transfer at bw_factor * bw_l without sharing, and with
 // tcp_gamma > 0 the TCP window caps it at tcp_gamma / (2 * route latency sum) (SimGrid's
-// CM02 / LV08 bounds). Rates change only when a transfer enters or leaves its data phase. Alone, a
+// CM02 / LV08 bounds). With cross > 0 (SimGrid's network/crosstraffic, 0.05 there) a transfer
+// also loads every shared link of its reverse route with cross x its rate (the TCP
+// acknowledgements), and a FATPIPE link of the reverse route only caps it at
+// bw_factor * bw / cross. Rates change only when a transfer enters or leaves its data phase. Alone, a
 // transfer takes lat_factor * sum(lat) + bytes / (bw_factor * min bw), the fixed per-route
 // time of fu_trace_build_routes. The message is consumed at the first tick > its end
 // (CA:76: the actor tests the receive once per tick). oracle/oracle.py (LinkNet) mirrors
@@ -78,6 +81,7 @@ struct LinkNet {
   const int32_t *rl = nullptr;
   double bytes = 154.0, lat_factor = 13.01, bw_factor = 0.97;
   double weight_S = 0.0, tcp_gamma = 0.0;  // LV08: 20537 and 4194304 (fu/platform.py)
+  double cross = 0.0;                      // network/crosstraffic (SimGrid: 0.05; 0 = off)
   struct Flow {
     int64_t r;         // route index src * n + dst
     double lat_end;    // end of the latency phase
@@ -87,6 +91,10 @@ struct LinkNet {
     double rate;
     double end;        // completion time (inf while running)
     int phase;         // 0 latency, 1 data, 2 done
+    // the shared links the transfer loads and its coefficient on each: 1 on its route (in
+    // route order), then cross on its reverse route's (crosstraffic; a link on both routes
+    // appears twice)
+    std::vector<std::pair<int32_t, double>> lk;
   };
   std::vector<Flow> fl;           // one per message id
   std::vector<int32_t> active;    // message ids not done, in start order
@@ -97,10 +105,25 @@ struct LinkNet {
     Flow &f = fl[id];
     f.r = (int64_t)src * n + dst;
     double l = 0.0, cap = std::numeric_limits<double>::infinity(), sw = 0.0;
+    f.lk.clear();
     for (int64_t k = roff[f.r]; k < roff[f.r + 1]; ++k) {
       l = l + lat[rl[k]];
       sw = sw + weight_S / bw[rl[k]];
       if (!shared[rl[k]]) cap = std::min(cap, bw_factor * bw[rl[k]]);
+      else f.lk.emplace_back(rl[k], 1.0);
+    }
+    if (cross > 0.0) {
+      const int64_t rb = (int64_t)dst * n + src;
+      for (int64_t k = roff[rb]; k < roff[rb + 1]; ++k) {
+        const int32_t q = rl[k];
+        if (shared[q]) {
+          f.lk.emplace_back(q, cross);
+        } else {
+          bool fwd = false;  // a FATPIPE link of both routes: consumption max(1, cross) = 1
+          for (int64_t j = roff[f.r]; j < roff[f.r + 1]; ++j) fwd = fwd || rl[j] == q;
+          if (!fwd) cap = std::min(cap, bw_factor * bw[q] / cross);
+        }
+      }
     }
     if (tcp_gamma > 0.0 && l > 0.0) cap = std::min(cap, tcp_gamma / (2.0 * l));
     f.lat_end = t + lat_factor * l;
@@ -129,11 +152,10 @@ struct LinkNet {
     for (int32_t id : active) {
       if (fl[id].phase != 1) continue;
       un.push_back(id);
-      for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1]; ++k)
-        if (shared[rl[k]]) {
-          cnt[rl[k]]++;
-          use[rl[k]] = use[rl[k]] + 1.0 / fl[id].pen;
-        }
+      for (const auto &lc : fl[id].lk) {
+        cnt[lc.first]++;
+        use[lc.first] = use[lc.first] + lc.second / fl[id].pen;
+      }
     }
     for (int32_t l = 0; l < n_links; ++l) crem[l] = bw_factor * bw[l];
     while (!un.empty()) {
@@ -144,21 +166,20 @@ struct LinkNet {
       std::vector<int32_t> keep, fix;
       for (int32_t id : un) {
         bool b = fl[id].cap * fl[id].pen == best;
-        for (int64_t k = roff[fl[id].r]; k < roff[fl[id].r + 1] && !b; ++k) {
-          const int32_t l = rl[k];
-          b = shared[l] && cnt[l] > 0 && std::max(0.0, crem[l] / use[l]) == best;
+        for (size_t q = 0; q < fl[id].lk.size() && !b; ++q) {
+          const int32_t l = fl[id].lk[q].first;
+          b = cnt[l] > 0 && std::max(0.0, crem[l] / use[l]) == best;
         }
         (b ? fix : keep).push_back(id);
       }
       for (int32_t id : fix) {
         Flow &f = fl[id];
         f.rate = f.cap * f.pen == best ? f.cap : best / f.pen;
-        for (int64_t k = roff[f.r]; k < roff[f.r + 1]; ++k)
-          if (shared[rl[k]]) {
-            crem[rl[k]] = crem[rl[k]] - f.rate;
-            use[rl[k]] = use[rl[k]] - 1.0 / f.pen;
-            cnt[rl[k]]--;
-          }
+        for (const auto &lc : f.lk) {
+          crem[lc.first] = crem[lc.first] - lc.second * f.rate;
+          use[lc.first] = use[lc.first] - lc.second / f.pen;
+          cnt[lc.first]--;
+        }
       }
       un.swap(keep);
     }
@@ -467,8 +488,9 @@ int fu_trace_build_links(int32_t n, const int64_t *decl_rowptr, const int32_t *d
                          const double *link_bw, const double *link_lat, const int32_t *link_shared,
                          const int64_t *route_off, const int32_t *route_links, double msg_bytes,
                          double lat_factor, double bw_factor, fu_trace **out) {
-  return fu_trace_build_links_ex(n, decl_rowptr, decl_col, mode, ticks, order, faults, n_links, link_bw, link_lat,
-                                 link_shared, route_off, route_links, msg_bytes, lat_factor, bw_factor, 0.0, 0.0, out);
+  return fu_trace_build_links_cross(n, decl_rowptr, decl_col, mode, ticks, order, faults, n_links, link_bw,
+                                    link_lat, link_shared, route_off, route_links, msg_bytes, lat_factor, bw_factor,
+                                    0.0, 0.0, 0.0, out);
 }
 
 int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
@@ -477,10 +499,21 @@ int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t
                             const int64_t *route_off, const int32_t *route_links, double msg_bytes,
                             double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
                             fu_trace **out) {
+  return fu_trace_build_links_cross(n, decl_rowptr, decl_col, mode, ticks, order, faults, n_links, link_bw,
+                                    link_lat, link_shared, route_off, route_links, msg_bytes, lat_factor, bw_factor,
+                                    weight_S, tcp_gamma, 0.0, out);
+}
+
+int fu_trace_build_links_cross(int32_t n, const int64_t *decl_rowptr, const int32_t *decl_col, int32_t mode,
+                               int32_t ticks, const char *order, const char *faults, int32_t n_links,
+                               const double *link_bw, const double *link_lat, const int32_t *link_shared,
+                               const int64_t *route_off, const int32_t *route_links, double msg_bytes,
+                               double lat_factor, double bw_factor, double weight_S, double tcp_gamma,
+                               double crosstraffic, fu_trace **out) {
   FU_TRY_BEGIN
   if (n <= 0 || n_links < 0 || !route_off || (n_links > 0 && (!link_bw || !link_lat || !link_shared)) ||
       !(msg_bytes >= 0.0) || !(lat_factor >= 0.0) || !(bw_factor > 0.0) || !(weight_S >= 0.0) ||
-      !(tcp_gamma >= 0.0))
+      !(tcp_gamma >= 0.0) || !(crosstraffic >= 0.0) || !(crosstraffic <= 1.0))
     return fail(FU_ERR_ARG, "fu_trace_build_links: bad arguments");
   const int64_t nr = (int64_t)n * n;
   if (route_off[0] != 0) return fail(FU_ERR_ARG, "fu_trace_build_links: route_off[0] must be 0");
@@ -506,6 +539,7 @@ int fu_trace_build_links_ex(int32_t n, const int64_t *decl_rowptr, const int32_t
   net.bw_factor = bw_factor;
   net.weight_S = weight_S;
   net.tcp_gamma = tcp_gamma;
+  net.cross = crosstraffic;
   return build_trace(n, decl_rowptr, decl_col, mode, ticks, order, faults, nullptr, &net, out);
   FU_TRY_END
 }

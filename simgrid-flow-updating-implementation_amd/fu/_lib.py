@@ -66,6 +66,7 @@ _SIGS = {
     "fu_run_collectall": ([vp, i32, i32, vp], ctypes.c_int),
     "fu_run_collectall_timed": ([vp, i32, P(f32)], ctypes.c_int),
     "fu_tune": ([vp], ctypes.c_int),
+    "fu_run_collectall_marked": ([vp, i32, vp], ctypes.c_int),
     "fu_mark": ([vp, i32], ctypes.c_int),
     "fu_mark_elapsed": ([vp, i32, i32, P(f32)], ctypes.c_int),
     "fu_max_err": ([vp, P(f64)], ctypes.c_int),
@@ -84,6 +85,8 @@ _SIGS = {
                              ctypes.c_int),
     "fu_trace_build_links_ex": ([i32, vp, vp, i32, i32, cp, cp, i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, f64,
                                  P(vp)], ctypes.c_int),
+    "fu_trace_build_links_cross": ([i32, vp, vp, i32, i32, cp, cp, i32, vp, vp, vp, vp, vp, f64, f64, f64, f64, f64,
+                                    f64, P(vp)], ctypes.c_int),
     "fu_trace_fault_stats": ([vp, P(i64), P(i64)], ctypes.c_int),
     "fu_trace_info": ([vp, vp], ctypes.c_int),
     "fu_trace_export": ([vp, vp, vp, vp, vp, vp, vp, vp, vp], ctypes.c_int),

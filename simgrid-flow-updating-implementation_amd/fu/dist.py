@@ -357,6 +357,10 @@ class DistCollectAll:
     def reset(self):
         L.call("fu_reset", self._h)
 
+    def run_marked(self, rounds_at):
+        ra = np.ascontiguousarray(rounds_at, dtype=np.int32)
+        L.call("fu_run_collectall_marked", self._h, len(ra), L.ptr(ra))
+
     def mark(self, slot: int):
         L.call("fu_mark", self._h, int(slot))
 

@@ -121,6 +121,12 @@ class CollectAll:
         at the current packing width; the state advances, so reset() before a timed run."""
         L.call("fu_tune", self._h)
 
+    def run_marked(self, rounds_at):
+        """Run rounds_at[-1] rounds in one call, recording mark k once rounds_at[k] of them
+        are queued (rounds_at[0] = 0: the start). Asynchronous; see elapsed()."""
+        ra = np.ascontiguousarray(rounds_at, dtype=np.int32)
+        L.call("fu_run_collectall_marked", self._h, len(ra), L.ptr(ra))
+
     def mark(self, slot: int):
         """Record HIP event `slot` (0..63) on the engine's stream (asynchronous)."""
         L.call("fu_mark", self._h, int(slot))
@@ -194,8 +200,9 @@ class Trace:
         tick t is consumed from tick t + floor(T) + 1 (fu_trace_build_routes).
         net: optional link model (fu.platform.Platform.link_net): transfers share the
         links' bandwidth (max-min fair, weighted by LV08's sharing penalty when net holds
-        weight_S > 0, capped by the TCP window with tcp_gamma > 0: fu_trace_build_links_ex);
-        exclusive with route_s."""
+        weight_S > 0, capped by the TCP window with tcp_gamma > 0, each transfer loading its
+        reverse route with crosstraffic > 0: fu_trace_build_links_cross); exclusive with
+        route_s."""
         rp = np.ascontiguousarray(decl_rowptr, dtype=np.int64)
         c = np.ascontiguousarray(decl_col, dtype=np.int32)
         self.n = len(rp) - 1
@@ -219,12 +226,13 @@ class Trace:
                 raise ValueError("net['route_off'] must have n * n + 1 entries")
             nl = len(self._net["bw"])
             z = lambda a: L.ptr(a) if len(a) else None  # noqa: E731
-            L.call("fu_trace_build_links_ex", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
+            L.call("fu_trace_build_links_cross", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
                    self.ticks, order.encode(), faults.encode() if faults else None, nl, z(self._net["bw"]),
                    z(self._net["lat"]), z(self._net["shared"]), L.ptr(self._net["route_off"]),
                    z(self._net["route_links"]), float(net.get("bytes", 154.0)),
                    float(net.get("lat_factor", 13.01)), float(net.get("bw_factor", 0.97)),
-                   float(net.get("weight_S", 0.0)), float(net.get("tcp_gamma", 0.0)), ctypes.byref(out))
+                   float(net.get("weight_S", 0.0)), float(net.get("tcp_gamma", 0.0)),
+                   float(net.get("crosstraffic", 0.0)), ctypes.byref(out))
         else:
             L.call("fu_trace_build_routes", self.n, L.ptr(rp), L.ptr(c) if len(c) else None, MODE[mode],
                    self.ticks, order.encode(), faults.encode() if faults else None,

@@ -11,6 +11,7 @@ CA:157). Here they are parsed into:
 from __future__ import annotations
 
 import re
+import warnings
 import xml.etree.ElementTree as ET
 from dataclasses import dataclass, field
 
@@ -24,6 +25,7 @@ LV08_LATENCY_FACTOR = 13.01
 LV08_WEIGHT_S = 20537.0     # sharing penalty: latency sum + weight_S / bandwidth per route link
 TCP_GAMMA = 4194304.0       # TCP window: a transfer's rate <= gamma / (2 * latency sum)
 LV08_BANDWIDTH_FACTOR = 0.97
+CROSSTRAFFIC = 0.05          # network/crosstraffic: a transfer's load on its reverse route's links
 
 
 def parse_bandwidth(s: str) -> float:
@@ -63,43 +65,61 @@ class Platform:
         self.hosts[name] = speed
 
     def route_time(self, src: str, dst: str, size_bytes: float = 154.0) -> float:
-        """LV08 transfer-time estimate: 13.01 * sum(latency) + size / (0.97 * min bw)."""
+        """LV08 transfer time of a lone transfer: 13.01 * sum(latency) + size / rate, where
+        rate = min(0.97 * min bandwidth, TCP window gamma / (2 * sum(latency))): the same
+        bound the link model (link_net, fu_trace_build_links_ex) puts on every transfer, so a
+        lone transfer takes the same time in both models."""
         links = self.routes.get((src, dst))
         if links is None:
             raise KeyError(f"no route {src} -> {dst}")
         if not links:
             return 0.0
         lat = sum(self.links[k][1] for k in links)
-        bw = min(self.links[k][0] for k in links)
-        return LV08_LATENCY_FACTOR * lat + size_bytes / (LV08_BANDWIDTH_FACTOR * bw)
+        rate = min(LV08_BANDWIDTH_FACTOR * self.links[k][0] for k in links)
+        if lat > 0.0:
+            rate = min(rate, TCP_GAMMA / (2.0 * lat))
+        return LV08_LATENCY_FACTOR * lat + size_bytes / rate
 
-    def link_net(self, hosts, size_bytes: float = 154.0, pairs=None) -> dict:
+    def link_net(self, hosts, size_bytes: float = 154.0, pairs=None, allow_unrouted: bool = False,
+                 crosstraffic: float = 0.0) -> dict:
         """The link model of fu_trace_build_links for the actors on `hosts` (in actor order):
         every link (bandwidth, latency, shared unless FATPIPE) and the route of every host
         pair (empty for a host to itself). Concurrent transfers share the links' bandwidth
         (max-min fair, each share weighted by 1 / LV08's sharing penalty, rates capped by the
-        TCP window); alone, a transfer takes route_time (below the TCP-window cap). pairs: the (i, j) actor pairs
-        that exchange messages (None = all): only they need a route; the others stay empty.
-        A pair with no route in the platform also stays empty, i.e. its messages arrive within
-        one tick, the plain schedule of the reference platform (CA:76) -- the tolerance of the
-        per-route model (route_matrix), so platforms that route only some host pairs run."""
+        TCP window); alone, a transfer takes route_time. pairs: the (i, j) actor pairs that
+        exchange messages (None = all): only they need a route; the others stay empty.
+        A needed pair the platform does not route raises KeyError listing every such pair, as
+        SimGrid's Full routing stops on a missing route. allow_unrouted=True gives those pairs
+        an empty route instead (delivery within one tick, the plain schedule of CA:76) and
+        warns with the list. crosstraffic: SimGrid's network/crosstraffic factor (each
+        transfer also loads the links of its reverse route with that share of its rate; 0.05
+        in SimGrid, 0 = off, the default here: parity-unpinned, fu.h)."""
         ids = sorted(self.links)
         at = {k: q for q, k in enumerate(ids)}
         n = len(hosts)
         need = None if pairs is None else {(int(i), int(j)) for i, j in pairs}
-        off, lst = [0], []
+        off, lst, missing = [0], [], []
         for i, a in enumerate(hosts):
             for j, b in enumerate(hosts):
-                if a != b and (need is None or (i, j) in need) and (a, b) in self.routes:
-                    lst.extend(at[k] for k in self.routes[(a, b)])
+                if a != b and (need is None or (i, j) in need):
+                    if (a, b) in self.routes:
+                        lst.extend(at[k] for k in self.routes[(a, b)])
+                    else:
+                        missing.append((a, b))
                 off.append(len(lst))
+        if missing:
+            desc = ", ".join(f"{a} -> {b}" for a, b in missing)
+            if not allow_unrouted:
+                raise KeyError(f"no route {desc} in the platform (pass allow_unrouted=True, or "
+                               "--fu-allow-unrouted to the Engine, to deliver them within one tick)")
+            warnings.warn(f"unrouted host pairs get one-tick delivery: {desc}", stacklevel=2)
         return {"bw": np.array([self.links[k][0] for k in ids], dtype=np.float64),
                 "lat": np.array([self.links[k][1] for k in ids], dtype=np.float64),
                 "shared": np.array([0 if k in self.fatpipe else 1 for k in ids], dtype=np.int32),
                 "route_off": np.array(off, dtype=np.int64), "route_links": np.array(lst, dtype=np.int32),
                 "bytes": float(size_bytes), "lat_factor": LV08_LATENCY_FACTOR,
                 "bw_factor": LV08_BANDWIDTH_FACTOR, "weight_S": LV08_WEIGHT_S, "tcp_gamma": TCP_GAMMA,
-                "n": n}
+                "crosstraffic": float(crosstraffic), "n": n}
 
 
 def load_platform(path: str) -> Platform:

@@ -28,7 +28,7 @@ import sys
 import numpy as np
 
 from .engine import CollectAll, Replay, Trace
-from .platform import (Platform, declared_csr, load_deployment, load_platform,
+from .platform import (CROSSTRAFFIC, Platform, declared_csr, load_deployment, load_platform,
                        symmetric_union_csr)
 
 
@@ -67,7 +67,11 @@ class Engine:
     """Drop-in for `simgrid.Engine` as the reference scripts use it."""
 
     def __init__(self, argv=None, *, order: str = "fwd", device: int = 0, sync: bool = False,
-                 out=None):
+                 out=None, allow_unrouted: bool = False, crosstraffic: float = 0.0):
+        """allow_unrouted: neighbouring hosts the platform does not route get one-tick delivery
+        instead of an error. crosstraffic: SimGrid's network/crosstraffic factor in the link
+        model (0 = off, the default here; SimGrid's own default is on, at 0.05, but its effect
+        cannot be pinned offline)."""
         self.argv = list(argv or [])
         # engine flags may also come through argv like SimGrid's --cfg (CA:152)
         for a in self.argv[1:]:
@@ -77,9 +81,16 @@ class Engine:
                 device = int(a.split("=", 1)[1])
             elif a == "--fu-sync":
                 sync = True
+            elif a == "--fu-allow-unrouted":
+                allow_unrouted = True
+            elif a.startswith("--cfg=network/crosstraffic:"):  # SimGrid's own flag
+                val = a.split(":", 1)[1].strip().lower()
+                crosstraffic = CROSSTRAFFIC if val in ("1", "yes", "true", "on") else 0.0
         self.order = order
         self.device = device
         self.sync = sync
+        self.allow_unrouted = allow_unrouted
+        self.crosstraffic = float(crosstraffic)
         self.out = out if out is not None else sys.stdout
         self.platform: Platform | None = None
         self.registry = {}
@@ -234,7 +245,8 @@ class Engine:
         src = np.repeat(np.arange(len(names)), np.diff(decl_rp))
         pairs = set(zip(src.tolist(), np.asarray(decl_col).tolist()))
         pairs |= {(j, i) for i, j in pairs}
-        return self.platform.link_net(names, pairs=pairs)
+        return self.platform.link_net(names, pairs=pairs, allow_unrouted=self.allow_unrouted,
+                                      crosstraffic=self.crosstraffic)
 
     def _route_matrix(self, names):
         """Transfer time (s) of every host pair's route under SimGrid's LV08 model

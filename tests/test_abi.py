@@ -129,3 +129,5 @@ def test_null_arguments_are_errors():
     assert "bad arguments" in L.last_error()
     assert L.lib.fu_graph_info(None, None, None, None, None) < 0
     assert L.lib.fu_run_collectall(None, 1, 0, None) < 0
+    assert L.lib.fu_run_collectall_marked(None, 1, None) < 0
+    assert "bad arguments" in L.last_error()

@@ -190,6 +190,12 @@ class _FakeEngine:
     def mark(self, slot):
         self.marks[slot] = self.r
 
+    def run_marked(self, b):
+        base = self.r
+        for k, x in enumerate(b):
+            self.marks[k] = base + x
+        self.r = base + b[-1]
+
     def elapsed(self, a, b):
         return (self.marks[b] - self.marks[a]) * 0.05
 
@@ -311,3 +317,141 @@ def test_pairwise_replicas_at_two_ranks(tmp_path):
     assert line["n_gpus"] == 2 and line["scaling"] == "weak" and "replicas x2" in line["config"]["parallelism"]
     assert abs(line["value"] - 2 * line["value_per_gpu"]) < 1e-6 * line["value"]
     assert line["cpu_baseline"] is None
+
+
+class _RecordingDist:
+    """A DistCollectAll stand-in that records, in order, every call of bench.py's N > 1
+    sequence that moves rounds (each round is one halo exchange) or runs a collective (the
+    kernel option, the error all-reduce): a rank whose sequence differs would hang RCCL. Its
+    autotune pass runs the rounds FP::tune_rounds_fixed gives for this rank's own state
+    (tools/plan_check --tune-rank), which the test makes differ from rank to rank."""
+    log = None
+    tune_rounds = None
+
+    def __init__(self, plan, values, uid, device=0, kernel="auto"):
+        self.n, self.E = plan.n_local, plan.e_local
+        self.log.append(["create", kernel])
+
+    def tune(self):
+        self.log.append(["rounds", self.tune_rounds, "tune"])
+
+    def run(self, rounds, err_every=0):
+        self.log.append(["rounds", int(rounds), "err" if err_every else ""])
+        return np.zeros(max(rounds // err_every, 1)) if err_every else None
+
+    def run_marked(self, b):
+        self.log.append(["rounds", int(b[-1]), "marked"])
+
+    def reset(self):
+        self.log.append(["reset"])
+
+    def synchronize(self):
+        pass
+
+    def set_targets(self, t):
+        pass
+
+    def halo_ms(self):
+        return 0.01
+
+    def elapsed(self, a, b):
+        return 0.3
+
+    def estimates(self):
+        return np.zeros(self.n)
+
+    def flows(self):
+        return np.zeros(self.E)
+
+    def info(self):
+        return {"kernel": "recon", "tile": (1024, 128)}
+
+    def close(self):
+        pass
+
+
+class _RefEngine:
+    def __init__(self, g, v, device=0, **k):
+        self.n, self.E = g.n, g.E
+
+    def run(self, rounds, err_every=0):
+        pass
+
+    def estimates(self):
+        return np.zeros(self.n)
+
+    def flows(self):
+        return np.zeros(self.E)
+
+    def close(self):
+        pass
+
+
+def _dist_sequence_rank(rank, world, port, outdir, table):
+    import json
+
+    import torch.distributed as dist
+
+    import fu
+    import fu.dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", world_size=world, rank=rank)
+    log = []
+    _RecordingDist.log = log
+    # this rank's autotune state: kernel 8 / 9 layouts and candidate drops differ by rank
+    _RecordingDist.tune_rounds = table[rank]
+    fu.dist.DistCollectAll = _RecordingDist
+    fu.dist.unique_id = lambda: bytes(128)
+    fu.CollectAll = _RefEngine
+    monkey = bench.RCCL_PARITY_N
+    bench.RCCL_PARITY_N = 1 << 14
+    try:
+        args = bench.parse(["--gpus", str(world), "--workload", "rgg-dist", "--steps", "20", "--warmup", "5",
+                            "--n", str(1 << 13), "--conv-rounds", "300", "--cpu-seconds", "0"])
+        line = bench.measure_dist(args, world, rank, rank, dist)
+    finally:
+        bench.RCCL_PARITY_N = monkey
+    with open(os.path.join(outdir, f"seq{rank}.json"), "w") as f:
+        json.dump({"log": log, "line": line}, f)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_sequence_identical_on_every_rank(tmp_path, world):
+    """bench.py --gpus N (N = 2, 4): every rank runs the same sequence of round counts and
+    collectives -- the RCCL parity prelude (30 rounds), the kernel option, the autotune pass,
+    the warmup, the fixed 80-round settle, the timed window, the halo samples and the
+    convergence run with its per-round error all-reduce -- although the ranks' own autotune
+    states differ (kernel 8 / 9 layouts present or not, candidates dropped on their own
+    timings): the pass's round count comes from FP::tune_rounds_fixed for each rank's state
+    (tools/plan_check --tune-rank). A rank whose count differed would hang RCCL instead of
+    failing (CA:74, CA:124). gloo on the CPU, engines recorded, graphs and plans real."""
+    import json
+    import subprocess
+
+    import torch.multiprocessing as mp
+
+    from conftest import ROOT
+
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools"), "bin/plan_check"], check=True)
+    pc = os.path.join(ROOT, "tools", "bin", "plan_check")
+    table = []
+    for rank in range(world):
+        k8, k9, code = int(rank % 2 == 0), int(rank % 3 == 0), (rank * 77) % 256
+        out = subprocess.run([pc, "--tune-rank", "0", str(k8), str(k9), str(code)], check=True,
+                             capture_output=True, text=True).stdout.split()
+        table.append(int(out[1]))
+    mp.spawn(_dist_sequence_rank, args=(world, bench._free_port(), str(tmp_path), table), nprocs=world, join=True)
+    seqs = [json.loads((tmp_path / f"seq{r}.json").read_text()) for r in range(world)]
+    for r in range(1, world):
+        assert seqs[r]["log"] == seqs[0]["log"], r
+    log = seqs[0]["log"]
+    rounds = [e for e in log if e[0] == "rounds"]
+    assert rounds[0] == ["rounds", bench.RCCL_PARITY_ROUNDS, ""]          # the parity prelude
+    assert ["rounds", table[0], "tune"] in rounds and table[0] == 36      # one pass, FP::tune_rounds_fixed
+    assert ["rounds", 5, ""] in rounds and ["rounds", 80, ""] in rounds   # warmup, settle
+    assert ["rounds", 20, "marked"] in rounds and ["rounds", 300, "err"] in rounds
+    line = seqs[0]["line"]
+    assert line["config"]["settle_rounds"] == 80 and line["rccl_parity"] == "bitwise"
+    assert all(s["line"] is None for s in seqs[1:])

@@ -203,7 +203,7 @@ def _random_net(n, seed, slow):
             "bw_factor": 0.97}
 
 
-@pytest.mark.parametrize("lv08", [False, True])
+@pytest.mark.parametrize("lv08", [False, True, "cross"])
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
 @pytest.mark.parametrize("order", ["fwd", "rand:5"])
 @pytest.mark.parametrize("seed", [1, 2])
@@ -220,6 +220,8 @@ def test_link_sharing_matches_emulator(mode, order, seed, lv08):
     net = _random_net(n, seed, slow=True)
     if lv08:  # shares weighted by the sharing penalty, the TCP window (fu_trace_build_links_ex)
         net = dict(net, weight_S=fu.platform.LV08_WEIGHT_S, tcp_gamma=fu.platform.TCP_GAMMA)
+    if lv08 == "cross":  # and SimGrid's crosstraffic (fu_trace_build_links_cross)
+        net = dict(net, crosstraffic=fu.platform.CROSSTRAFFIC)
     faults = "drop=0.05,delay=3:0.05,seed=4" if seed == 2 else None
     em = oracle.TickEmulator(d["actors"], "ca" if mode == "collectall" else "pw", faults=faults, net=net)
     snaps = {}
@@ -253,6 +255,10 @@ def test_link_sharing_matches_emulator(mode, order, seed, lv08):
         eq = fu.Trace(rp, col, mode, 2000, order, faults=faults, net=_random_net(n, seed, slow=True)).arrays()
         assert not (np.array_equal(eq["tick_task_off"], a["tick_task_off"])
                     and np.array_equal(eq["events"], a["events"]))
+    if lv08 == "cross":  # and so does the crosstraffic: without it another schedule
+        nc = fu.Trace(rp, col, mode, 2000, order, faults=faults, net=dict(net, crosstraffic=0.0)).arrays()
+        assert not (np.array_equal(nc["tick_task_off"], a["tick_task_off"])
+                    and np.array_equal(nc["events"], a["events"]))
 
 
 @pytest.mark.parametrize("mode", ["collectall", "pairwise"])
@@ -324,6 +330,39 @@ def test_link_model_lv08_weights_and_tcp_window():
     f = ln.start(0, 1, 0.0)
     ln.advance_to(0.2)
     assert f["rate"] == G / (2.0 * 0.01) < 0.97 * 1e9
+
+
+def test_link_model_crosstraffic_loads_the_reverse_route():
+    """SimGrid's network/crosstraffic (fu_trace_build_links_cross): a transfer also loads the
+    shared links of its reverse route with 0.05 of its rate. Two opposite transfers over two
+    one-way links (0 -> 1 on link 0, 1 -> 0 on link 1) each see the other's acknowledgements:
+    rate x + 0.05 y <= C on each link gives x = y = C / 1.05; without it each has its link
+    alone. A FATPIPE link on the reverse route only caps a transfer at C / 0.05. Checked on
+    the emulator's LinkNet; the native builder equals it event for event (test above)."""
+    C = 0.97 * 1000.0
+    net = {"n": 2, "bw": np.array([1000.0, 1000.0]), "lat": np.array([0.0, 0.0]), "shared": np.array([1, 1]),
+           "route_off": np.array([0, 0, 1, 2, 2]), "route_links": np.array([0, 1]),
+           "bytes": 1e4, "lat_factor": 13.01, "bw_factor": 0.97, "crosstraffic": 0.05}
+    ln = oracle.LinkNet(net)
+    f1, f2 = ln.start(0, 1, 0.0), ln.start(1, 0, 0.0)
+    ln.advance_to(0.001)
+    assert f1["rate"] == pytest.approx(C / 1.05) and f2["rate"] == pytest.approx(C / 1.05)
+    off = oracle.LinkNet(dict(net, crosstraffic=0.0))
+    g1, g2 = off.start(0, 1, 0.0), off.start(1, 0, 0.0)
+    off.advance_to(0.001)
+    assert g1["rate"] == g2["rate"] == C
+    alone = oracle.LinkNet(net)  # one transfer: its acknowledgements load only link 1
+    h = alone.start(0, 1, 0.0)
+    alone.advance_to(0.001)
+    assert h["rate"] == C
+    fat = oracle.LinkNet(dict(net, shared=np.array([1, 0]), bw=np.array([1000.0, 10.0])))
+    k = fat.start(0, 1, 0.0)  # reverse route: FATPIPE link 1 of 10 B/s caps it at 9.7 / 0.05
+    fat.advance_to(0.001)
+    assert k["rate"] == pytest.approx(0.97 * 10.0 / 0.05)
+    with pytest.raises(fu.FuError, match="bad arguments"):
+        names = ["a", "b"]
+        fu.Trace(np.array([0, 1, 2]), np.array([1, 0]), "pairwise", 10, net=dict(net, crosstraffic=2.0))
+        del names
 
 
 def test_link_model_argument_checks():

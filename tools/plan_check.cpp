@@ -665,6 +665,20 @@ int main(int argc, char **argv) {
       std::printf("plan_check --tune: %ld checks, %ld failed\n", g_checks, g_fail);
       return g_fail ? 1 : 0;
     }
+  // --tune-rank WIDTH K8_OK K9_OK CODE: the rounds of one multi-GPU autotune pass for one rank
+  // state (tune_out of candidate c = (CODE >> 2c) & 3), as the engine runs it
+  // (tests/test_bench_cli.py drives bench.py's N > 1 sequence with these counts)
+  if (argc == 6 && !std::strcmp(argv[1], "--tune-rank")) {
+    FP::TuneRank r;
+    r.dist = true;
+    r.width = std::atoi(argv[2]);
+    r.k8_ok = std::atoi(argv[3]) != 0;
+    r.k9_ok = std::atoi(argv[4]) != 0;
+    const int code = std::atoi(argv[5]);
+    for (int c = 0; c < FP::kNCands; ++c) r.tune_out[c] = (code >> (2 * c)) & 3;
+    std::printf("tune_rounds %d need %d\n", FP::tune_rounds_fixed(r), FP::tune_need(r));
+    return 0;
+  }
   for (int a = 1; a < argc; ++a) {
     const std::string k = argv[a];
     auto need = [&](int cnt) {

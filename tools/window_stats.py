@@ -1,10 +1,11 @@
 #!/usr/bin/env python3
 """Per-kernel durations inside bench.py's timed window (rounds 0..K-1 from the zero state) from
 a rocprofv3 --kernel-trace CSV of the same command, as the record bench.py quotes
-(`roofline.window_stats`) when n, E, kernel and K match its run.
+(`roofline.archived_window_profile`, marked archival: another run's record) when n, E, kernel
+and K match its run.
 
     python tools/window_stats.py TRACE.csv --n N --E E --kernel KNAME --steps K [--which I]
-                                 [--copy-GBs C] [--out profiles/r05/NAME_window_stats.json]
+                                 [--copy-GBs C] [--commit SHA] [--out profiles/r06/NAME_window_stats.json]
                                  [--dump profiles/r05/NAME_window_trace.csv]
 
 The window starts at the (I+1)-th k_round0 launch of the process (I = 1 by default: the first
@@ -33,6 +34,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--which", type=int, default=1, help="index of the k_round0 launch that starts the window")
     ap.add_argument("--copy-GBs", type=float, default=None, help="the same run's roofline.copy_GBs")
+    ap.add_argument("--commit", default=None, help="git commit of the tree the trace ran")
     ap.add_argument("--out")
     ap.add_argument("--dump", help="write the window's launches (name, start, end ns) as CSV, so that the "
                                    "record can be recomputed from a tracked file")
@@ -80,7 +82,7 @@ def main():
         "per_kernel_per_round": {k: round(sum(v) / (a.steps - 1), 3) for k, v in per.items()},
         "per_kernel": {k: {"calls": len(v), "mean_us": round(sum(v) / len(v), 3), "min_us": round(min(v), 3),
                            "max_us": round(max(v), 3)} for k, v in per.items()},
-        "copy_GBs": a.copy_GBs,
+        "copy_GBs": a.copy_GBs, "commit": a.commit,
     }
     if a.dump:
         with open(a.dump, "w") as f:
