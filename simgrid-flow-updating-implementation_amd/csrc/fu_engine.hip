@@ -2135,6 +2135,8 @@ struct RoundCtx {
 // ======================================================================================
 // handle
 // ======================================================================================
+constexpr int kPreMarks = 12;  // fu_mark slots created with the handle (a window's marks)
+
 struct fu_handle {
   int device = 0;
   // layout 1 (fu_create_from_graph_ex): device node p = caller node old_of_new[p]; the
@@ -2145,7 +2147,7 @@ struct fu_handle {
   hipStream_t stream2 = nullptr;            // kernel 4's heavy tiles, concurrently (fork_heavy)
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
-  hipEvent_t marks[64] = {};                // fu_mark slots (created on first use)
+  hipEvent_t marks[64] = {};                // fu_mark slots (the first kPreMarks at creation, others on first use)
   hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
   int32_t n = 0;
   int64_t E = 0;
@@ -2969,6 +2971,10 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
+  // the marks a timed window uses (bench.py: up to 12) exist before any window starts: event
+  // creation costs the host tens of microseconds, which a window must not contain
+  for (int k = 0; k < kPreMarks; ++k)
+    if (hipEventCreate(&h->marks[k]) != hipSuccess) return cleanup(fail(FU_ERR_HIP, "hipEventCreate failed"));
   if (hipHostMalloc(reinterpret_cast<void **>(&h->h_pw), sizeof(int), hipHostMallocDefault) != hipSuccess)
     return cleanup(fail(FU_ERR_ALLOC, "hipHostMalloc failed"));
   *h->h_pw = 0;
