@@ -166,12 +166,12 @@ def timed_rounds(eng, steps: int):
     round 0 and each chunk, one host sync at the end. Returns (wall_s, per-chunk device ms,
     bounds)."""
     b = chunk_bounds(steps)
+    ra = np.asarray(b, dtype=np.int32)  # ready before the clock starts
     eng.synchronize()
     t0 = time.perf_counter()
-    # one host call for the whole window (fu_run_collectall_marked): no interpreter work
-    # between the marks, so round 0 (the first launch on an idle stream) is timed from its
-    # event to its end without Python's call overhead in between
-    eng.run_marked(b)
+    # one host call for the whole window (fu_run_collectall_marked); mark 0 is round 0's own
+    # start (the kernel's start event), not an event on the idle stream ahead of its dispatch
+    eng.run_marked(ra)
     eng.synchronize()
     wall = time.perf_counter() - t0
     dev = [eng.elapsed(k, k + 1) for k in range(len(b) - 1)]
@@ -266,6 +266,11 @@ def prepare(eng, kernel, warmup, widths=None, tune=True, settle_ms=None):
         eng.run(16)
         eng.synchronize()
         n_settle += 16
+    # the window's own host path once, untimed (rounds 0-1 from the zero state): its first
+    # call in a process costs ~50 us of host time (profiles/r06/d: 1180 against 1148 us)
+    eng.reset()
+    eng.run_marked(np.asarray(chunk_bounds(2), dtype=np.int32))
+    eng.synchronize()
     eng.reset()
     return n_settle
 

@@ -11,6 +11,7 @@
 // contract, and `/` is the correctly rounded IEEE fp64 division. Every sum is a sequential
 // dependency chain in row order, including for hubs (see k_round_tile's heavy path).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -2148,6 +2149,8 @@ struct fu_handle {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;  // autotune timing
   hipEvent_t ev2 = nullptr, ev3 = nullptr;  // fu_run_collectall_timed
   hipEvent_t marks[64] = {};                // fu_mark slots (the first kPreMarks at creation, others on first use)
+  hipEvent_t r0_start = nullptr;            // fu_run_collectall_marked: mark 0 = the start of k_round0,
+  hipEvent_t r0_stop = nullptr;             //   mark 1 (when it follows round 0) = its end
   hipEvent_t ev_pw = nullptr, ev_fork = nullptr, ev_join = nullptr;
   int32_t n = 0;
   int64_t E = 0;
@@ -2557,8 +2560,15 @@ void plan_alone(fu_handle *h, RoundCtx &c) {
 int launch_round0(fu_handle *h, RoundCtx &c) {
   static_assert(sizeof(PackCtl) * 3 == 6 * sizeof(unsigned long long), "k_round0 clears 3 PackCtl");
   h->lagf[0] = h->lagf[1] = 0;  // zero state: no lagged flows
-  hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
-                     h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
+  if (h->r0_start) {  // a timed window's first mark: the kernel's own start (hipExtLaunchKernel)
+    hipExtLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->r0_start,
+                          h->r0_stop, 0, h->n, h->na, (const int *)h->rowptr, (const double *)h->v, h->a[0], h->a[2],
+                          reinterpret_cast<unsigned long long *>(h->pctl));
+    h->r0_start = h->r0_stop = nullptr;
+  } else {
+    hipLaunchKernelGGL(k_round0, dim3(grid_for(std::max(h->na, 6))), dim3(kBlock), 0, h->stream, h->n, h->na,
+                       h->rowptr, h->v, h->a[0], h->a[2], reinterpret_cast<unsigned long long *>(h->pctl));
+  }
   if (c.err)
     hipLaunchKernelGGL(k_max_err, dim3(std::min(1024u, grid_for(h->n))), dim3(kBlock), 0, h->stream, h->n,
                        h->a[0], h->target, c.err);
@@ -3446,10 +3456,11 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms) {
 }
 
 // A timed window in one host call: mark k (HIP event slot k) is recorded once rounds_at[k]
-// rounds of this call have been queued (rounds_at[0] = 0: before the first). Between the
-// marks no host code but the launches runs, so the device time of the window's first round
-// (round 0 after fu_reset: the GPU waits on an idle stream for its launch) holds no
-// interpreter overhead between the first mark and the first launch.
+// rounds of this call have been queued (rounds_at[0] = 0: before the first). A window that
+// starts with round 0 (after fu_reset, single GPU) takes mark 0 from k_round0's own start and,
+// when mark 1 follows round 0, mark 1 from its end (hipExtLaunchKernel's start / stop events):
+// an event recorded on the idle stream ahead of the launch would time-stamp at once and hold
+// the first dispatch's latency, and a marker behind it its own ~5 us, in round 0's time.
 int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *rounds_at) {
   FU_TRY_BEGIN
   if (!h || !rounds_at || n_marks < 1 || n_marks > 64 || rounds_at[0] < 0)
@@ -3460,6 +3471,8 @@ int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *round
   for (int k = 0; k < n_marks; ++k)
     if (!h->marks[k]) HIP_TRY(hipEventCreate(&h->marks[k]));
   int32_t done = 0;
+  const bool r0 = rounds_at[0] == 0 && n_marks > 1 && rounds_at[1] > 0 && h->rounds == 0 && !h->dist;
+  const bool r0_end = r0 && rounds_at[1] == 1;
   for (int k = 0; k < n_marks; ++k) {
     if (rounds_at[k] > done) {
       if (int rc = run_rounds(h, rounds_at[k] - done, 0, 0)) return rc;
@@ -3468,7 +3481,16 @@ int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *round
     if (h->dist) {  // a mark after a round includes that round's halo (comm stream)
       if (int rc = fu__dist_round_hook(h, 0)) return rc;
     }
-    HIP_TRY(hipEventRecord(h->marks[k], h->stream));
+    if (k == 0 && r0) {  // recorded by round 0's own launch
+      h->r0_start = h->marks[0];
+      if (r0_end) h->r0_stop = h->marks[1];
+    } else if (!(k == 1 && r0_end)) {
+      HIP_TRY(hipEventRecord(h->marks[k], h->stream));
+    }
+  }
+  if (h->r0_start) {  // round 0 did not launch through launch_round0: never the case
+    h->r0_start = h->r0_stop = nullptr;
+    return fail(FU_ERR_STATE, "fu_run_collectall_marked: round 0 was not launched");
   }
   return FU_OK;
   FU_TRY_END

@@ -124,8 +124,9 @@ class CollectAll:
     def run_marked(self, rounds_at):
         """Run rounds_at[-1] rounds in one call, recording mark k once rounds_at[k] of them
         are queued (rounds_at[0] = 0: the start). Asynchronous; see elapsed()."""
-        ra = np.ascontiguousarray(rounds_at, dtype=np.int32)
-        L.call("fu_run_collectall_marked", self._h, len(ra), L.ptr(ra))
+        ra = rounds_at if isinstance(rounds_at, np.ndarray) and rounds_at.dtype == np.int32 \
+            and rounds_at.flags["C_CONTIGUOUS"] else np.ascontiguousarray(rounds_at, dtype=np.int32)
+        L.call("fu_run_collectall_marked", self._h, len(ra), ra.ctypes.data)
 
     def mark(self, slot: int):
         """Record HIP event `slot` (0..63) on the engine's stream (asynchronous)."""

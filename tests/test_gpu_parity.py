@@ -240,6 +240,29 @@ def test_headline_window_bitwise():
     eng.close()
 
 
+@pytest.mark.parametrize("bounds", [[0, 1, 7], [0, 3, 7], [0, 0, 2, 7]])
+def test_marked_window_matches_plain_rounds(bounds):
+    """fu_run_collectall_marked (bench.py's timed window): marks at the bounds, round 0's
+    marks from k_round0's own start / stop events when the window starts at round 0; the
+    state equals plain rounds bitwise, every interval is a positive device time, and a second
+    window (not from round 0) records its marks as plain events."""
+    g = fu.Graph.erdos_renyi(20000, 80000, seed=5)
+    v = fu.uniform_values(g.n, seed=2)
+    eng = fu.CollectAll(g, v)
+    eng.run_marked(np.asarray(bounds, dtype=np.int32))
+    eng.synchronize()
+    for k in range(len(bounds) - 1):
+        if bounds[k + 1] > bounds[k]:
+            assert eng.elapsed(k, k + 1) > 0.0, k
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, bounds[-1], nthreads=8)
+    assert np.array_equal(eng.estimates(), a_ref) and np.array_equal(eng.flows(), f_ref)
+    eng.run_marked(np.asarray([0, 2], dtype=np.int32))
+    assert eng.elapsed(0, 1) > 0.0
+    coracle.ca_rounds(g.rowptr, g.col, g.rev, v, 2, a_ref, f_ref, nthreads=8)
+    assert np.array_equal(eng.estimates(), a_ref)
+    eng.close()
+
+
 def test_pairwise_unit_window_bitwise():
     """BASELINE config 3 exactly as `pairwise_unit` times it: RR-64K pairwise, tie order
     rand:3, the default persistent register kernel run to tick 101, then ticks 101-500

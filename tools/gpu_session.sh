@@ -25,15 +25,7 @@ for s in $STEPS; do
     prof)   export TMPDIR=/tmp
             step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 "$ROOTDIR/bench.py" --cpu-seconds 0 ${BENCH_ARGS:-} ;;
     sweep)  step sweep 900 python tools/sweep.py ${SWEEP_ARGS:-} ;;
-    sweeplibs) i=0
-               for lib in ${SWEEP_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...), in the order given
-                 i=$((i+1))
-                 step "sweep_${i}_$lib" 600 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so python tools/sweep.py ${SWEEP_ARGS:-}
-               done ;;
     replay) step replay 400 python tools/bench_replay.py ;;
-    replaylibs) for lib in ${REPLAY_LIBS:-libfu}; do  # A/B of experiment builds (make VARIANT=...)
-                  step "replay_$lib" 400 env FU_LIBRARY=$ROOTDIR/simgrid-flow-updating-implementation_amd/fu/$lib.so TICKS=1000 python tools/bench_replay.py
-                done ;;
     rgg)    step bench_rgg 400 python bench.py --workload rgg --n 8388608 --no-conv --cpu-seconds 0 ;;
     rmat)   step bench_rmat 500 python bench.py --workload rmat --no-conv --cpu-seconds 0 --steps ${RMAT_STEPS:-20} --warmup 2 ${RMAT_ARGS:-} ;;
     profrmat) export TMPDIR=/tmp
