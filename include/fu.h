@@ -149,7 +149,8 @@ int fu_create_from_graph_ex(const fu_graph *g, const double *value, int32_t devi
  * profiles/MEASUREMENTS.md): "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_multi",
  * "hub_blocks", "fuse", "light_geo", "tr_hot" (kernel 9), "hub_cus" / "hub_cu_stride" (the
  * hub path on CU-masked streams, profiles/r05/b), "st_split" (kernel 8's next stage beside
- * this round's tiles, profiles/r05/c) and "nt" (kernel 4's non-temporal column loads). */
+ * this round's tiles, profiles/r05/c), "nt" (kernel 4's non-temporal column loads) and "g56"
+ * (kernel 8's 7-byte staged codes, profiles/r06/g). */
 int fu_set_option(fu_handle *h, const char *key, int64_t value);
 /* Zero the state: the next round run is round 0. */
 int fu_reset(fu_handle *h);

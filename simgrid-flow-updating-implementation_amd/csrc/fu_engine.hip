@@ -862,10 +862,7 @@ struct StageArgs {
   const int *dtab[4];                  // per light tile: kStageRuns x (G index - m) of each run
   int sel[4];                          // layout used for tables of width 8, 16, 32, 0
   int f64;                             // kernel 9: always stage the doubles (layout 3)
-  int g56;                             // kernel 8, unpacked table in layout 3: 7-byte staged codes
-  unsigned long long base56;           //   code = key(x) - base56 (escape 2^56 - 1: gather the double)
 };
-constexpr unsigned long long kEsc56 = (1ull << 56) - 1;
 __device__ __forceinline__ int width_index(int width) {
   return width == 8 ? 0 : width == 16 ? 1 : width == 32 ? 2 : 3;
 }
@@ -993,82 +990,6 @@ __device__ __forceinline__ void stage_body(unsigned char *s_tab, int nb, int cnt
   }
 }
 
-// Kernel 8 with the table unpacked (every round before the estimates cluster, e.g. the
-// driver's ER-1M window): the staged element is a 7-byte code, key(x) - base56 when it lies in
-// [0, 2^56 - 2], else the escape 2^56 - 1 (the tile then gathers the double: exact either way).
-// 2^56 keys span 16 binades around the values' median, so random doubles of one magnitude all
-// fit, and G moves 7 instead of 8 bytes per edge, each way. A lane stages 16 elements per step
-// (one slice lookup each) as 112 bytes, seven 16-byte non-temporal stores; the (slice, part)
-// regions start at multiples of 16 elements, so every lane's 112 bytes are 16-byte aligned.
-__device__ __forceinline__ void stage_body56(unsigned char *s_tab, int nb, int cnt, int g0, int g1,
-                                             const unsigned short *__restrict__ colS,
-                                             const double *__restrict__ tab, unsigned char *__restrict__ G,
-                                             unsigned long long base) {
-  constexpr int EPL = 16, U = kStageU, STEP = kStageThreads * EPL, BSTEP = U * STEP;
-  constexpr int kW = kStageLds / 16 / kStageThreads;
-  const int t = threadIdx.x;
-  uint4 buf[kW];
-  const int w16 = (cnt * 8) >> 4;
-  {
-    const uint4 *s16 = reinterpret_cast<const uint4 *>(tab + nb);
-#pragma unroll
-    for (int u = 0; u < kW; ++u) {
-      const int k = t + u * kStageThreads;
-      buf[u] = k < w16 ? s16[k] : make_uint4(0u, 0u, 0u, 0u);
-    }
-  }
-  ColVec<EPL> ca[U], cb[U];
-  auto load = [&](ColVec<EPL>(&c)[U], int g) {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-      if (g + u * STEP < g1) ld_cols<EPL>(c[u], colS + g + u * STEP);
-  };
-  auto put = [&](const ColVec<EPL>(&c)[U], int g) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int gg = g + u * STEP;
-      if (gg < g1) {
-        unsigned long long w[14] = {};
-#pragma unroll
-        for (int j = 0; j < EPL; ++j) {
-          const double x = reinterpret_cast<const double *>(s_tab)[col_at<EPL>(c[u], j)];
-          unsigned long long cd = dkey(x) - base;
-          cd = cd < kEsc56 ? cd : kEsc56;
-          const int bit = 56 * j, wi = bit >> 6, sh = bit & 63;
-          w[wi] |= cd << sh;
-          if (sh > 8) w[wi + 1] |= cd >> (64 - sh);
-        }
-        typedef unsigned v4u __attribute__((ext_vector_type(4)));
-        v4u *dst = reinterpret_cast<v4u *>(G + 7ll * gg);
-#pragma unroll
-        for (int q = 0; q < 7; ++q) {
-          v4u o;
-          __builtin_memcpy(&o, &w[2 * q], 16);
-          __builtin_nontemporal_store(o, dst + q);
-        }
-      }
-    }
-  };
-  int g = g0 + t * EPL;
-  load(ca, g);
-#pragma unroll
-  for (int u = 0; u < kW; ++u) {
-    const int k = t + u * kStageThreads;
-    if (k < w16) reinterpret_cast<uint4 *>(s_tab)[k] = buf[u];
-  }
-  __syncthreads();
-  for (;;) {
-    if (g >= g1) break;
-    load(cb, g + BSTEP);
-    put(ca, g);
-    g += BSTEP;
-    if (g >= g1) break;
-    load(ca, g + BSTEP);
-    put(cb, g);
-    g += BSTEP;
-  }
-}
-
 __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
                                                         const double *__restrict__ a_prev,
                                                         const void *__restrict__ code_prev,
@@ -1109,11 +1030,6 @@ __global__ __launch_bounds__(kStageThreads) void k_stage(StageArgs sa, int n,
       stage_body<T, false>(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const T *>(src),        \
                            reinterpret_cast<T *>(G));                                                 \
   } while (0)
-  if (wb == 8 && li == 3 && sa.g56 && !sa.f64) {  // unpacked table, kernel 8: 7-byte codes
-    stage_body56(s_tab, nb, cnt, rg.x, rg.y, colS, reinterpret_cast<const double *>(src),
-                 reinterpret_cast<unsigned char *>(G), sa.base56);
-    return;
-  }
   if (wb == 1) FU_BODY(unsigned char);
   else if (wb == 2) FU_BODY(unsigned short);
   else if (wb == 4) FU_BODY(unsigned);
@@ -1381,22 +1297,7 @@ __global__ __launch_bounds__(kBlock) void k_round_staged(
   own2 = t < nn ? a_prev2[nb + t] : 0.0;
   }
   // every G load of the tile first, then decode (escapes gather the double via col)
-  if (pp.width == 0 && lsel == 3 && sa.g56) {  // 7-byte codes (stage_body56): two aligned words
-    const unsigned long long *G64 = reinterpret_cast<const unsigned long long *>(G);
-    unsigned long long lo[kPer], hi[kPer];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const long long wi = gi[k] >= 0 ? (7ll * gi[k]) >> 3 : 0;
-      lo[k] = G64[wi];
-      hi[k] = G64[wi + 1];
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int sh = (int)((7ll * (gi[k] >= 0 ? gi[k] : 0)) & 7) * 8;
-      const unsigned long long cd = ((lo[k] >> sh) | (sh ? hi[k] << (64 - sh) : 0ull)) & kEsc56;
-      g[k] = gi[k] < 0 ? 0.0 : cd == kEsc56 ? a_prev[col[e0 + (int)(si[k] & 0xFFFFu)]] : dkey_inv(sa.base56 + cd);
-    }
-  } else if (pp.width == 0) {
+  if (pp.width == 0) {
 #pragma unroll
     for (int k = 0; k < kPer; ++k)
       g[k] = gi[k] >= 0 ? reinterpret_cast<const double *>(G)[gi[k]] : 0.0;
@@ -2276,8 +2177,6 @@ struct fu_handle {
   int mid_heavy = 1;     // kernel 9: heavy rows of <= 64 x kMidRL edges in a register-resident launch
   int tr_bpx = 32;       // kernel 9: k_transpose blocks per XCD (1 per CU), each looping over buckets; 0 = one per bucket
   int staged_lo = 1;     // kernel 8: staged indices loaded before the flows (LO)
-  int g56 = 1;           // kernel 8: 7-byte staged codes while the table is unpacked (stage_body56)
-  unsigned long long base56 = 0;  // their base: key(median of the values) - 2^55
   int c16 = 1;           // kernel 4: narrow light tiles read 2-byte column offsets
   int multi_mid = 1;     // kernel 9: k_heavy_multi also takes the register launch's rows (257-1024)
   int split_hubs = 1;     // kernel 4: mega-hub tiles alone on the side stream
@@ -2557,8 +2456,6 @@ StageArgs stage_args(fu_handle *h, unsigned *grid) {
       if (h->st[li].P) pick = li;
     sa.sel[want] = pick < 0 ? 0 : pick;
   }
-  sa.g56 = h->g56 && h->st[3].P;
-  sa.base56 = h->base56;
   if (grid) *grid = g;
   return sa;
 }
@@ -3104,21 +3001,6 @@ int fu__create_common(int32_t n, int64_t e, const int64_t *rowptr, const int32_t
       (e && hipMemcpy(h->col, col, sizeof(int) * e, hipMemcpyHostToDevice) != hipSuccess) ||
       hipMemcpy(h->v, value, sizeof(double) * n, hipMemcpyHostToDevice) != hipSuccess)
     return cleanup(fail(FU_ERR_HIP, "fu_create: upload failed"));
-  {  // kernel 8's 7-byte codes: a window of 2^56 keys (16 binades) centred on the values' median
-    std::vector<double> fin;
-    fin.reserve(n);
-    for (int32_t i = 0; i < n; ++i)
-      if (std::isfinite(value[i])) fin.push_back(value[i]);
-    double c = 1.0;
-    if (!fin.empty()) {
-      std::nth_element(fin.begin(), fin.begin() + fin.size() / 2, fin.end());
-      c = fin[fin.size() / 2];
-    }
-    uint64_t b;
-    std::memcpy(&b, &c, 8);
-    const uint64_t key = (b >> 63) ? ~b : (b | (1ull << 63));
-    h->base56 = key > (1ull << 55) ? key - (1ull << 55) : 0ull;
-  }
   if ((e == 0 && hipMemset(h->col, 0, sizeof(int)) != hipSuccess) ||
       hipMemset(h->f[0], 0, sizeof(double) * std::max<int64_t>(fe, 1)) != hipSuccess ||
       hipMemset(h->f[1], 0, sizeof(double) * std::max<int64_t>(fe, 1)) != hipSuccess ||
@@ -3271,11 +3153,6 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
   }
   if (!std::strcmp(key, "staged_lo")) {  // kernel 8: staged indices before the flows (1) or interleaved (0)
     h->staged_lo = value != 0;
-    return FU_OK;
-  }
-  if (!std::strcmp(key, "g56")) {  // kernel 8: 7-byte staged codes for unpacked tables (1) or doubles (0)
-    if (value != 0 && value != 1) return fail(FU_ERR_ARG, "fu_set_option: g56 must be 0 or 1");
-    h->g56 = (int)value;
     return FU_OK;
   }
   if (!std::strcmp(key, "tr_bpx")) {  // kernel 9: transpose blocks per XCD (0 = one per bucket)

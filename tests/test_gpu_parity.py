@@ -157,10 +157,10 @@ def test_option_errors():
         with pytest.raises(fu.FuError, match="kernel must be"):
             eng.set_option("kernel", k)
     for key in ("nope", "bins", "hub_scan", "pipe_bpc", "wave_edges", "diag", "hub_multi", "hub_blocks", "fuse",
-                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride", "st_split", "tr_hot", "nt"):
+                "tr_pipe", "hub_prio", "side_tiles", "split_tr", "hub_cus", "hub_cu_stride", "st_split", "tr_hot", "nt", "g56"):
         with pytest.raises(fu.FuError):
             eng.set_option(key, 1)
-    for key, val in (("tr_nt", 2), ("tr_nt", -1), ("g56", 2)):
+    for key, val in (("tr_nt", 2), ("tr_nt", -1)):
         with pytest.raises(fu.FuError):
             eng.set_option(key, val)
     with pytest.raises(fu.FuError):
@@ -781,42 +781,6 @@ def test_tile_geometries_bitwise(kernel, opts, kind):
     a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 30, nthreads=16)
     assert np.array_equal(eng.estimates(), a_ref)
     assert np.array_equal(eng.flows(), f_ref)
-
-
-@pytest.mark.parametrize("spread", ["uniform", "wide"])
-def test_stage_g56_codes_bitwise(spread):
-    """Kernel 8 with the table unpacked stages 7-byte codes (key(x) - base56, a window of 16
-    binades around the values' median; stage_body56): uniform values (every code in the
-    window) and values over 60 decades with signs, zeros, subnormals, infinities and NaN (many
-    escapes, each gathered as the double through the edge's column). Packing off, so every
-    round is unpacked; estimates and flows equal the C oracle's, and the doubles path (option
-    g56 0) gives the same bits."""
-    g = fu.Graph.erdos_renyi(60_000, 240_000, seed=7)
-    if spread == "uniform":
-        v = fu.uniform_values(g.n, seed=3)
-    else:
-        rng = np.random.default_rng(5)
-        v = rng.choice([-1.0, 1.0], g.n) * 10.0 ** rng.uniform(-30, 30, g.n)
-        v[::97] = 0.0
-        v[1::101] = -0.0
-        v[2::103] = 5e-320
-        v[3::5003] = np.inf
-        v[4::7001] = np.nan
-    out = []
-    for g56 in (1, 0):
-        eng = fu.CollectAll(g, v, kernel="stage")
-        eng.set_option("pack", 0)
-        eng.set_option("g56", g56)
-        eng.run(25)
-        out.append((eng.estimates(), eng.flows()))
-        eng.close()
-    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 25, nthreads=16)
-    for x, x_ref in ((out[0][0], a_ref), (out[0][1], f_ref)):
-        nan = np.isnan(x_ref)  # NaN payloads may differ between the CPU and the GPU
-        assert np.array_equal(np.isnan(x), nan)
-        assert np.array_equal(x[~nan].view(np.uint64), x_ref[~nan].view(np.uint64))
-    for x, y in zip(out[0], out[1]):  # 7-byte codes and doubles: the same bits, NaNs included
-        assert np.array_equal(x.view(np.uint64), y.view(np.uint64))
 
 
 @pytest.mark.parametrize("layout", [0, 1, 2, 3])
