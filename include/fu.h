@@ -171,8 +171,10 @@ int fu_run_collectall_timed(fu_handle *h, int32_t rounds, float *ms);
 int fu_tune(fu_handle *h);
 /* A timed window in one call: runs rounds_at[n_marks - 1] rounds and records mark k (the
  * event of fu_mark slot k) once rounds_at[k] of them are queued (non-decreasing, rounds_at[0]
- * = 0 marks the start; n_marks <= 64). Asynchronous; read the times with fu_mark_elapsed.
- * bench.py times its windows with it, so no host interpreter runs between the marks. */
+ * = 0 marks the start; n_marks <= 64). A single-GPU window that starts at round 0 takes mark 0
+ * from round 0's own kernel start and, when rounds_at[1] == 1, mark 1 from its end (events of
+ * the launch itself: an event on the idle stream ahead of it would hold the dispatch latency).
+ * Asynchronous; read the times with fu_mark_elapsed. bench.py times its windows with it. */
 int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *rounds_at);
 /* Record HIP event `slot` (0..63) on the handle's stream (asynchronous). */
 int fu_mark(fu_handle *h, int32_t slot);
