@@ -3475,7 +3475,10 @@ int fu_run_collectall_marked(fu_handle *h, int32_t n_marks, const int32_t *round
   const bool r0_end = r0 && rounds_at[1] == 1;
   for (int k = 0; k < n_marks; ++k) {
     if (rounds_at[k] > done) {
-      if (int rc = run_rounds(h, rounds_at[k] - done, 0, 0)) return rc;
+      if (int rc = run_rounds(h, rounds_at[k] - done, 0, 0)) {
+        h->r0_start = h->r0_stop = nullptr;  // a failed call leaves no event armed for a later round 0
+        return rc;
+      }
       done = rounds_at[k];
     }
     if (h->dist) {  // a mark after a round includes that round's halo (comm stream)
