@@ -417,9 +417,9 @@ def _dist_sequence_rank(rank, world, port, outdir, table):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dist_sequence_identical_on_every_rank(tmp_path, world):
-    """bench.py --gpus N (N = 2, 4): every rank runs the same sequence of round counts and
+    """bench.py --gpus N (N = 2, 4, 8): every rank runs the same sequence of round counts and
     collectives -- the RCCL parity prelude (30 rounds), the kernel option, the autotune pass,
     the warmup, the fixed 80-round settle, the timed window, the halo samples and the
     convergence run with its per-round error all-reduce -- although the ranks' own autotune

@@ -1,5 +1,5 @@
 """Multi-rank partition + halo plan (fu.dist.partition), exercised on the CPU with
-torch.distributed/gloo at world_size 2 and 3.
+torch.distributed/gloo at world_size 2, 3 and 8 (the driver's scaling node).
 
 Each rank runs the collect-all rounds on its local CSR in the ghost-slot numbering that
 fu_dist_create consumes, and exchanges the halo exactly as fu_dist.hip does: it packs
@@ -105,7 +105,7 @@ def _worker(rank, world, port, rowptr, col, rev, v, rounds, mode, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 @pytest.mark.parametrize("mode", ["pull", "recon"])
 @pytest.mark.parametrize("kind", ["er", "rgg"])
 def test_partitioned_rounds_match_oracle(world, mode, kind):
@@ -162,7 +162,7 @@ def test_plan_shapes_and_symmetry():
         assert p.rev.max() < p.e_local + p.n_ghost_f
 
 
-@pytest.mark.parametrize("nparts", [1, 2, 3, 5])
+@pytest.mark.parametrize("nparts", [1, 2, 3, 5, 8])
 def test_rgg_slab_generator_matches_global_and_partition(nparts):
     """fu_part_gen_rgg: each rank's slab (built without the global graph) has the global
     generator's rows, and the same ghost numbering / halo plan as fu.dist.partition with the
@@ -211,7 +211,7 @@ def _cm_worker(rank, world, port, kind, n, out_q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [1, 2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
 @pytest.mark.parametrize("kind", ["rgg", "er"])
 def test_component_means_dist_bitwise(world, kind):
     """The N > 1 line's convergence targets: per-component exact means of a partitioned graph
