@@ -139,6 +139,8 @@ def main():
         rows = np.nonzero((deg > lo) & (deg <= 8192))[0]
         rows = rows[np.argsort(-deg[rows], kind="stable")]
         eh = int(deg[rows].sum())
+        if eh == 0:  # a small graph may have no rows in this class
+            continue
         nseg = segments(rp, col, rows, 14)
         hist = np.zeros(P, dtype=np.int64)
         for r in rows:
@@ -185,7 +187,7 @@ def main():
     gate = {"GB": 24.0, "ms": 5.5}
     rep["gate"] = gate
     rep["verdict"] = {k: (rep[k]["GB"] <= gate["GB"] and rep[k]["ms"] <= gate["ms"])
-                      for k in rep if k.startswith("alt_")}
+                      for k in list(rep) if k.startswith("alt_")}
     txt = json.dumps(rep, indent=1)
     print(txt)
     if a.out:
