@@ -2183,6 +2183,7 @@ struct fu_handle {
   int fork_heavy = 1;    // kernel 4: heavy tiles on stream2, concurrently with the light tiles
   bool autotune = true;  // kernel "auto": candidates timed on real rounds, fastest kept
   bool tuned = false;
+  bool tune_for_width = false;  // the pending pass was armed by a packing-width change (poll_pack_width)
   bool tuning = false;     // inside an autotune pass: packing plans wait until it ends
   float tune_ms[8] = {};  // per candidate (tune_cands order), ms per round of the last pass
   int tune_out[8] = {};   // passes in which the candidate was > 1.3x the best (2: dropped)
@@ -3111,6 +3112,7 @@ int fu_set_option(fu_handle *h, const char *key, int64_t value) {
     h->kernel = value == 0 ? 4 : (int)value;
     h->autotune = value == 0;
     h->tuned = false;
+    h->tune_for_width = false;
     return FU_OK;
   }
   if (!std::strcmp(key, "stage_layout")) {  // kernel 8: -1 = by packing width, 0..3 forced
@@ -3231,9 +3233,14 @@ int fu_reset(fu_handle *h) {
   h->plan_pending = false;  // round 0 clears the plan
   *h->h_pw = 0;           // round 0 clears the packing plan
   h->seen_width = 0;
-  if (h->autotune && h->tuned && h->tune_cache[0] >= 0) {  // unpacked again: its winner
+  // unpacked again: its winner. A pass still pending for a width the rounds before the reset
+  // reached (seen in calls too short for a pass) no longer applies; one armed by the kernel
+  // option still runs.
+  if (h->autotune && (h->tuned || h->tune_for_width) && h->tune_cache[0] >= 0) {
     use_cand(h, kCands[h->tune_cache[0]]);
     h->tuned_width = 0;
+    h->tuned = true;
+    h->tune_for_width = false;
   }
   return FU_OK;
   FU_TRY_END
@@ -3376,6 +3383,7 @@ static int autotune_kernel(fu_handle *h, int32_t *budget, int width) {
   h->tune_cache[width_class(width)] = bi;
   h->tuned_width = width;
   h->tuned = true;
+  h->tune_for_width = false;
   h->n_tunes++;
   return FU_OK;
 }
@@ -3393,6 +3401,7 @@ static void poll_pack_width(fu_handle *h) {
     h->tuned_width = *h->h_pw;
   } else if (h->n_tunes < kMaxTunes) {
     h->tuned = false;
+    h->tune_for_width = true;
   }
 }
 

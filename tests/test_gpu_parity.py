@@ -681,6 +681,39 @@ def test_autotune_width_cache_across_reset_bitwise():
     assert np.array_equal(eng.flows(), f_ref)
 
 
+def test_reset_drops_a_width_pass_left_pending():
+    """Calls too short for an autotune pass (bench.prepare's settle: 16 rounds each) see the
+    packing width change and leave a pass pending for that width. fu_reset returns to the
+    unpacked table, whose winner is cached, so the pending pass is dropped: the next call
+    runs no pass at width 0 again, and the bits stay the oracle's."""
+    g = fu.Graph.erdos_renyi(200_000, 800_000, seed=13)
+    v = fu.uniform_values(g.n, seed=13)
+    eng = fu.CollectAll(g, v)
+    eng.set_option("pack_every", 4)
+    eng.tune()
+    passes = eng.info()["tune_passes"]
+    assert passes == 1 and eng.info()["autotune"] == "done"
+    for _ in range(30):
+        eng.run(16)
+        eng.synchronize()
+    assert eng.pack_widths()[2] > 0
+    assert eng.info()["autotune"] == "pending"
+    assert eng.info()["tune_passes"] == passes
+    eng.reset()
+    assert eng.info()["autotune"] == "done"
+    eng.run(64)
+    eng.synchronize()
+    assert eng.info()["tune_passes"] == passes
+    a_ref, f_ref = coracle.ca_sync(g.rowptr, g.col, g.rev, v, 64, nthreads=16)
+    assert np.array_equal(eng.estimates(), a_ref)
+    assert np.array_equal(eng.flows(), f_ref)
+    # a pass armed by the kernel option is not dropped by a reset
+    eng.reset()
+    eng.set_option("kernel", 0)
+    eng.reset()
+    assert eng.info()["autotune"] == "pending"
+
+
 def _er_with_outlier_pairs(n, m, pairs, seed):
     """ER(n, m) plus `pairs` disjoint 2-node components whose values are far from the giant
     component's mean: their estimates never enter the packed window, so every gather of
