@@ -17,8 +17,9 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
+# SimGrid's time units (a bare number is seconds)
 _UNITS_T = {"": 1.0, "s": 1.0, "ms": 1e-3, "us": 1e-6, "ns": 1e-9, "ps": 1e-12,
-            "m": 60.0, "h": 3600.0}
+            "m": 60.0, "h": 3600.0, "d": 86400.0, "w": 604800.0}
 
 # LV08 network model defaults of SimGrid (latency factor, bandwidth factor).
 LV08_LATENCY_FACTOR = 13.01

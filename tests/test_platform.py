@@ -14,6 +14,10 @@ def test_units():
     assert parse_time("59.904us") == pytest.approx(59.904e-6)
     assert parse_time("1.461517ms") == pytest.approx(1.461517e-3)
     assert parse_time("15us") == pytest.approx(15e-6)
+    assert parse_time("2") == 2.0 and parse_time("1.5h") == 5400.0
+    assert parse_time("1d") == 86400.0 and parse_time("2w") == 1209600.0
+    with pytest.raises(ValueError):
+        parse_time("3parsecs")
 
 
 def test_small_platform_routes_fit_in_one_tick(tmp_path):
